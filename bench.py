@@ -1,0 +1,182 @@
+#!/usr/bin/env python
+"""Benchmark of the render-and-compare hot path (BASELINE.json metric, config C2 per GPU).
+
+One step = one pass of the hot path over one batch: render + unproject + 1-NN + score 10k 6-DoF
+candidate poses of the 003_cracker_box proxy at 640x480 (stride 8, no ICP) and fold the per-model argmin
+keys; with N > 1 GPUs every rank scores its own 10k-pose shard (weak scaling) and the keys meet in one
+RCCL all-reduce(MIN).  Inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--poses P] [--cpu-seconds S]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+Rank 0 prints ONE JSON line (see DESIGN.md "Measurement" for the roofline / cpu_baseline fields).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes_per_pose(width, height, stride, p_r_mean):
+    """B_r + B_c + B_s = 4*W*H*(1 + 1/s) + 24*P_r + 12 (render + score, no GICP)."""
+    return 4.0 * width * height * (1.0 + 1.0 / stride) + 24.0 * p_r_mean + 12.0
+
+
+def cpu_baseline(w, seconds: float):
+    """Time the CPU oracle pipeline (same poses, same scene) on a bounded sample."""
+    import oracle
+
+    sc = w.scene
+    poses = w.poses.cpu().numpy()
+    pm = w.pose_model.cpu().numpy()
+    tot = w.pose_obs_total.cpu().numpy()
+    obs_xyz = w.obs_xyz.cpu().numpy()
+    obs_lab = w.obs_label.cpu().numpy()
+    order = np.argsort(obs_lab, kind="stable")
+    oxyz, olab = obs_xyz[order], obs_lab[order]
+    nl = int(olab.max()) + 1 if len(olab) else 0
+    ls = np.array([np.searchsorted(olab, L, "left") for L in range(nl)], np.int32)
+    le = np.array([np.searchsorted(olab, L, "right") for L in range(nl)], np.int32)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 64))
+    done, t0, batch = 0, time.perf_counter(), max(threads * 4, 32)
+    rng = np.random.default_rng(7)
+    while time.perf_counter() - t0 < seconds:
+        idx = rng.choice(len(poses), size=min(batch, len(poses)), replace=False)
+        oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, poses[idx], pm[idx], pm[idx], sc.width, sc.height,
+                        sc.proj, sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz,
+                        ls, le, tot[idx], 2, True, 0.01, nthreads=threads)
+        done += len(idx)
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "poses/s", "cores": threads, "kind": "port",
+            "sample": f"{done} random poses of the same C2 workload through the CPU oracle (full-frame "
+                      f"render + stride-8 cloud + brute-force 1-NN + costs), OpenMP over poses, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--poses", type=int, default=10000, help="candidate poses per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from perception_amd import distributed as pdist
+    from perception_amd import workloads
+    from perception_amd._native import PCORE_KEY_NONE
+    from perception_amd.core import decode_keys
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    pdist.init_from_env()
+    dev = torch.device("cuda", local)
+
+    w = workloads.build(poses_per_model=args.poses, device=local, rank=rank)
+    n = int(w.poses.shape[0])
+    out = tuple(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3))
+    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev)
+
+    # rendered points per pose (for the algorithmic byte count), measured once outside the timed region
+    s = w.stride
+    hs, ws = (w.scene.height + s - 1) // s, w.scene.width // s
+    chunk = 2000
+    pr_total = 0
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        dbg = torch.empty((hi - lo, hs, ws), dtype=torch.int32, device=dev)
+        w.core.evaluate(w.poses[lo:hi], w.pose_model[lo:hi], w.pose_label[lo:hi], w.pose_obs_total[lo:hi],
+                        stride=s, dbg_zs=dbg)
+        pr_total += int((dbg > 0).sum().item())
+    p_r_mean = pr_total / max(n, 1)
+
+    for _ in range(args.warmup):
+        keys.fill_(PCORE_KEY_NONE)
+        workloads.step(w, out, keys)
+        pdist.allreduce_min_keys(keys)
+    torch.cuda.synchronize()
+
+    # per-launch duration of the dominant (fused) kernel, on the stream it runs on
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        keys.fill_(PCORE_KEY_NONE)
+        ev[i][0].record(stream)
+        w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=s, out=out)
+        ev[i][1].record(stream)
+        w.core.select(out[0], out[1], w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
+        pdist.allreduce_min_keys(keys)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    best_cost, best_idx = decode_keys(keys)
+    if rank != 0:
+        return
+    total_poses = n * world * args.steps
+    value = total_poses / elapsed
+    bpp = algorithmic_bytes_per_pose(w.scene.width, w.scene.height, s, p_r_mean)
+    achieved = bpp * n / (kern_ms * 1e-3)
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("poses_per_launch") == n:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    line = {
+        "metric": "candidate poses rendered+scored/sec @640x480",
+        "value": value,
+        "unit": "poses/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (003_cracker_box proxy mesh, GT-rendered 16-bit depth + 2 mm noise, label mask)",
+        "config": {"workload": "C2: 1 YCB mesh (12,288 tris), 10k 6-DoF poses/GPU render+score, 640x480, "
+                               "stride 8, no ICP", "poses_per_gpu": n, "width": w.scene.width,
+                   "height": w.scene.height, "stride": s, "parallelism": f"pose-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_BPS, "traffic": traffic,
+                     "kernel": "fused_cost_kernel", "kernel_ms": kern_ms,
+                     "bytes_per_pose": bpp, "p_r_mean": p_r_mean},
+        "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},
+    }
+    if world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * pcore.h -- C ABI of the MI355X render-and-compare pose-search core (libpcore.so).
+ *
+ * Drop-in boundary for the reference's GPU seam
+ *   cuda_renderer::render_cuda_multi_unified(...)   (cuda_renderer/include/cuda_renderer/renderer.h:221-268,
+ *                                                     cuda_renderer/src/cuda/renderer.cu:1431-1934)
+ *   cuda_renderer::depth2cloud_global(...)          (renderer.h:131-153, renderer.cu:1936-2069)
+ * and for the host selection it feeds
+ *   EnvObjectRecognition::ComputeGreedyCostsInParallelGPU / ComputeGreedyRenderPoses
+ *                                                    (sbpl_perception/src/search_env.cpp:1987-2051, 2542-2636).
+ *
+ * Conventions (differences from the reference are deliberate and listed in INTEGRATION.md):
+ *   - Plain C types only.  Large per-batch arrays are DEVICE pointers (e.g. tensor.data_ptr() of a
+ *     PyTorch-ROCm tensor); mesh and camera setup take HOST pointers (copied once).
+ *   - Every call is asynchronous on the caller's stream (`stream` may be NULL = default stream); the
+ *     caller synchronises.  One context per (host thread, device); calls on a context are not re-entrant.
+ *   - Caller-allocated outputs.  The context owns persistent device scratch and never frees caller memory.
+ *   - Return value: PCORE_OK or an error code; pcore_last_error() describes the last failure.
+ *     The reference's in-band "invalid pose" convention (rendered cost -1, compute_costs.cuh:28-31) is kept.
+ *   - Poses are the reference's Model::mat4x4 (model.h:76-107): 16 floats a0..d3, row-major, rotation AND
+ *     translation scaled by 100 (mat4x4::init_from_eigen(pose_in_cam, 100)), so vertices land in cm.
+ */
+#ifndef PCORE_H_
+#define PCORE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCORE_ABI_VERSION 1
+
+enum pcore_status {
+    PCORE_OK = 0,
+    PCORE_E_INVALID_ARG = 1, /* bad size / pointer / parameter */
+    PCORE_E_HIP = 2,         /* a HIP runtime call failed */
+    PCORE_E_OOM = 3,         /* device allocation failed */
+    PCORE_E_STATE = 4        /* required setup call missing (meshes / camera / observation) */
+};
+
+/* Cost types of render_cuda_multi_unified (renderer.cu:1498): 0 = 3-DoF depth, 1 = 3-DoF RGB-D
+ * (CIEDE2000 colour gate; not implemented yet -> PCORE_E_INVALID_ARG), 2 = 6-DoF depth + labels. */
+enum pcore_cost_type { PCORE_COST_DEPTH_3DOF = 0, PCORE_COST_RGBD_3DOF = 1, PCORE_COST_DEPTH_6DOF = 2 };
+
+typedef struct pcore_ctx pcore_ctx;
+typedef void* pcore_stream; /* hipStream_t */
+
+/* Image geometry + intrinsics.  `proj` replaces the reference's proj_mat argument (renderer.h:225,
+ * built by compute_proj, renderer.cu:1386-1410); fx/fy/cx/cy are kCameraFX.. (renderer.h:231-234). */
+typedef struct pcore_camera {
+    int32_t width, height;
+    float fx, fy, cx, cy;
+    float proj[16];
+} pcore_camera;
+
+/* Per-batch parameters of render_cuda_multi_unified that are not arrays (renderer.h:228-252). */
+typedef struct pcore_eval_params {
+    int32_t cost_type;           /* enum pcore_cost_type */
+    int32_t calc_obs_cost;       /* calculate_observed_cost */
+    int32_t stride;              /* gpu_stride; width % stride == 0 (compute_point_clouds.cuh:271) */
+    float depth_factor;          /* rendered cm -> metres (the reference passes 100) */
+    float sensor_resolution;     /* metres; squared internally like renderer.cu:1877 */
+    float occlusion_threshold;   /* 3-DoF source-occlusion threshold in cm (gpu_occlusion_threshold) */
+} pcore_eval_params;
+
+/* ---- lifetime ---------------------------------------------------------------------------------- */
+int pcore_create(int device, pcore_ctx** out_ctx);
+void pcore_destroy(pcore_ctx* ctx);
+const char* pcore_last_error(const pcore_ctx* ctx);
+int pcore_abi_version(void);
+
+/* ---- static inputs ----------------------------------------------------------------------------- */
+/* Triangles of all models concatenated + triangles per model: the `tris` and `tris_model_count`
+ * arguments (renderer.h:223-226; filled by LoadObjFiles, search_env.cpp:253-307 / Model::LoadModel,
+ * model.cpp:16-135).  tri_xyz: num_tris x 9 floats (v0,v1,v2) in metres, HOST.  tri_rgb: num_tris x 3
+ * (vertex-0 colour, model.cpp:81-97), HOST, may be NULL (colour 128).  The context deduplicates
+ * vertices and builds meshlets once here. */
+int pcore_upload_meshes(pcore_ctx* ctx, const float* tri_xyz, const uint8_t* tri_rgb, int32_t num_tris,
+                        const int32_t* tris_model_count, int32_t num_models);
+
+int pcore_set_camera(pcore_ctx* ctx, const pcore_camera* cam);
+
+/* ---- per-scene inputs -------------------------------------------------------------------------- */
+/* depth2cloud_global (renderer.h:131-153; used by SetInput, search_env.cpp:5993-6017): unproject the
+ * observed depth image (raw sensor units, e.g. YCB uint16 widened to int32) at `stride`, keeping pixels
+ * with depth > 0 and (if label_mask != NULL) label > 0.  Writes xyz (cap x 3, metres) and label
+ * (mask - 1) in the reference's compaction order; *out_count (HOST) receives the point count (the call
+ * synchronises `stream` to return it).  Device pointers. */
+int pcore_observed_cloud(pcore_ctx* ctx, const int32_t* d_depth, const uint8_t* d_label_mask, int32_t width,
+                         int32_t height, int32_t stride, float depth_factor, float* d_out_xyz,
+                         int32_t* d_out_label, int32_t cap, int32_t* out_count, pcore_stream stream);
+
+/* Observation used by every evaluate call until replaced: the source depth in cm (H x W int32; the
+ * reference's source_depth after search_env.cpp:2487-2498), the source mask label (H x W uint8, the
+ * reference's source_mask_label; NULL for 3-DoF) and the observed cloud with its labels (the
+ * observed_depth_eigen / result_observed_cloud_label pair, renderer.h:236-242).  The context sorts the
+ * cloud by label (stable, renderer.cu:1674-1686) and builds its fixed-radius neighbour grids for
+ * `sensor_resolution` metres.  Device pointers; the call synchronises `stream`. */
+int pcore_set_observation(pcore_ctx* ctx, const int32_t* d_src_depth_cm, const uint8_t* d_src_mask,
+                          const float* d_obs_xyz, const int32_t* d_obs_label, int32_t num_obs,
+                          float sensor_resolution, pcore_stream stream);
+
+/* ---- per-batch hot path ------------------------------------------------------------------------ */
+/* Stage "COST" of render_cuda_multi_unified with do_icp = false: render every pose, unproject at
+ * stride, 1-NN against the same-label observed points, and the rendered / observed / points-diff
+ * costs (compute_costs.cuh:293-457).  d_pose_label NULL selects 3-DoF (all observed points, occlusion
+ * by threshold).  d_pose_obs_total: pose_observed_points_total (renderer.h:240).  Outputs N floats each
+ * (d_out_oc / d_out_diff are written as 0 when calc_obs_cost == 0).  d_dbg_zs (nullable): the sampled
+ * z-buffer after source occlusion, N x ceil(H/stride) x (W/stride) int32 (parity / debugging). */
+int pcore_evaluate(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model,
+                   const int32_t* d_pose_label, const float* d_pose_obs_total, int32_t num_poses,
+                   const pcore_eval_params* params, float* d_out_rc, float* d_out_oc, float* d_out_diff,
+                   int32_t* d_dbg_zs, pcore_stream stream);
+
+/* Stage "RENDER": full-resolution int32 z-buffers (cm) with source occlusion and INT_MAX -> 0
+ * (image_render, image_renderer.cuh:336-496).  d_out_depth: N x H x W.  Parity mode. */
+int pcore_render(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
+                 int32_t num_poses, float occlusion_threshold, int32_t* d_out_depth, pcore_stream stream);
+
+/* Stage "CLOUD": compute_point_clouds (compute_point_clouds.cuh:188-367) over N z-buffers: stride mask,
+ * pose-major / row / column compaction, unprojection.  xyz AoS (cap x 3).  d_label_mask (H x W) only
+ * for num_poses == 1; d_pose_label gives the rendered-cloud label.  *out_count (HOST) = total points
+ * (the call synchronises `stream`). */
+int pcore_depth_to_cloud(pcore_ctx* ctx, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,
+                         int32_t stride, float depth_factor, const uint8_t* d_label_mask,
+                         const int32_t* d_pose_label, float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label,
+                         int32_t cap, int32_t* out_count, pcore_stream stream);
+
+/* Host selection of the reference moved on device: cost = (int)(rc + oc) (x86 conversion semantics),
+ * skip invalid (-1/-2), keep |(int)rc - (int)oc| < 30, per-model minimum with strict '<' (lowest global
+ * index wins ties) -- search_env.cpp:2022-2048, 2554-2566.  Result is folded into d_keys[num_models]
+ * (int64, atomic min) as key = ((uint32)(cost ^ 0x80000000) << 31) | (index_base + i); initialise
+ * d_keys to PCORE_KEY_NONE.  Keys from several batches / ranks combine with a MIN reduction
+ * (RCCL all-reduce). */
+#define PCORE_KEY_NONE ((int64_t)0x7fffffffffffffffLL)
+int pcore_select(pcore_ctx* ctx, const float* d_rc, const float* d_oc, const int32_t* d_pose_model,
+                 int32_t num_poses, int64_t index_base, int32_t num_models, int64_t* d_keys, pcore_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCORE_H_ */

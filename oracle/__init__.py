@@ -1,0 +1,163 @@
+"""CPU oracle for the render-and-compare hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this package.  The
+product package (perception_amd) never imports, links or calls it.
+
+This is a literal restatement of the reference's CUDA/host code (file:line citations in
+pcore_oracle.cpp).  Parity against the reference *binary* is unpinned: the reference path cannot be
+built here and holds no golden vectors for this path ("Oracle").
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    """Compile oracle/build/liboracle.so with the oracle's Makefile (g++, no FMA contraction)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def _opt(ptype):
+    """ndpointer that also accepts None (NULL)."""
+
+    class _Opt(ptype):
+        @classmethod
+        def from_param(cls, obj):
+            if obj is None:
+                return None
+            return super().from_param(obj)
+
+    return _Opt
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        c_int, c_float = ctypes.c_int, ctypes.c_float
+        L.orc_compute_proj.argtypes = [c_float] * 4 + [c_int, c_int, c_float, c_float, _f32p]
+        L.orc_render_depth.argtypes = [_f32p, c_int, _i32p, c_int, _f32p, _i32p, _opt(_i32p), c_int,
+                                       c_int, c_int, _f32p, _i32p, _opt(_u8p), c_float, _i32p, c_int]
+        L.orc_depth_to_cloud.restype = c_int
+        L.orc_depth_to_cloud.argtypes = [_i32p, c_int, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
+                                         c_float, _opt(_u8p), _opt(_i32p), _f32p, _opt(_i32p), _opt(_i32p), c_int]
+        L.orc_knn1.argtypes = [_f32p, _opt(_i32p), c_int, _f32p, c_int, _opt(_i32p), _opt(_i32p), c_int,
+                               _f32p, _i32p]
+        L.orc_costs.argtypes = [c_int, c_int, c_int, c_float, _f32p, _i32p, _i32p, c_int, c_int,
+                                _opt(_f32p), _f32p, _f32p, _f32p]
+        L.orc_select.argtypes = [c_int, _f32p, _f32p, _i32p, c_int, ctypes.c_int64, _i32p, _i64p]
+        L.orc_evaluate.argtypes = [_f32p, c_int, _i32p, c_int, _f32p, _i32p, _opt(_i32p), c_int, c_int, c_int,
+                                   _f32p, _i32p, _opt(_u8p), c_float, c_int, c_float, c_float, c_float, c_float,
+                                   c_float, _f32p, c_int, _opt(_i32p), _opt(_i32p), c_int, _opt(_f32p), c_int,
+                                   c_int, c_float, _f32p, _f32p, _f32p, c_int]
+        _lib = L
+    return _lib
+
+
+def _c(a, dt):
+    return None if a is None else np.ascontiguousarray(a, dtype=dt)
+
+
+def compute_proj(fx, fy, cx, cy, width, height, near=10.0, far=10000.0) -> np.ndarray:
+    out = np.zeros(16, np.float32)
+    lib().orc_compute_proj(fx, fy, cx, cy, width, height, near, far, out)
+    return out
+
+
+def render_depth(tris, tris_model_count, poses, pose_model, pose_label, width, height, proj,
+                 src_depth, src_mask, occlusion_threshold=1.0, nthreads=0) -> np.ndarray:
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    out = np.empty((n, height, width), np.int32)
+    lib().orc_render_depth(tris, tris.size // 9, _c(tris_model_count, np.int32), len(tris_model_count), poses,
+                           _c(pose_model, np.int32), _c(pose_label, np.int32), n, width, height,
+                           _c(proj, np.float32), _c(src_depth, np.int32).reshape(-1),
+                           None if src_mask is None else _c(src_mask, np.uint8).reshape(-1),
+                           float(occlusion_threshold), out.reshape(-1), nthreads)
+    return out
+
+
+def depth_to_cloud(depth, stride, cx, cy, fx, fy, depth_factor, label_mask=None, pose_label=None):
+    """Returns (xyz (P,3) f32, pose (P,) i32, label (P,) i32) in the reference's compaction order."""
+    depth = _c(depth, np.int32)
+    n, h, w = depth.shape if depth.ndim == 3 else (1,) + depth.shape
+    cap = n * ((h + stride - 1) // stride) * ((w + stride - 1) // stride)
+    xyz = np.zeros((max(cap, 1), 3), np.float32)
+    pose = np.zeros(max(cap, 1), np.int32)
+    lab = np.zeros(max(cap, 1), np.int32)
+    cnt = lib().orc_depth_to_cloud(depth.reshape(-1), n, w, h, stride, cx, cy, fx, fy, depth_factor,
+                                   None if label_mask is None else _c(label_mask, np.uint8).reshape(-1),
+                                   _c(pose_label, np.int32), xyz.reshape(-1), pose, lab, cap)
+    return xyz[:cnt].copy(), pose[:cnt].copy(), lab[:cnt].copy()
+
+
+def knn1(r_xyz, r_label, o_xyz, label_start=None, label_end=None):
+    r_xyz = _c(r_xyz, np.float32).reshape(-1, 3)
+    o_xyz = _c(o_xyz, np.float32).reshape(-1, 3)
+    nr = r_xyz.shape[0]
+    d2 = np.zeros(max(nr, 1), np.float32)
+    idx = np.zeros(max(nr, 1), np.int32)
+    nl = 0 if label_start is None else len(label_start)
+    lib().orc_knn1(r_xyz.reshape(-1) if nr else np.zeros(3, np.float32), _c(r_label, np.int32), nr,
+                   o_xyz.reshape(-1) if o_xyz.size else np.zeros(3, np.float32), o_xyz.shape[0],
+                   _c(label_start, np.int32), _c(label_end, np.int32), nl, d2, idx)
+    return d2[:nr], idx[:nr]
+
+
+def costs(num_poses, cost_type, calc_obs, sensor_resolution, d2, idx, r_pose, num_o, pose_obs_total):
+    rc = np.zeros(num_poses, np.float32)
+    oc = np.zeros(num_poses, np.float32)
+    df = np.zeros(num_poses, np.float32)
+    d2 = _c(d2, np.float32)
+    lib().orc_costs(num_poses, cost_type, int(calc_obs), sensor_resolution,
+                    d2 if d2.size else np.zeros(1, np.float32), _c(idx, np.int32) if len(idx) else np.zeros(1, np.int32),
+                    _c(r_pose, np.int32) if len(r_pose) else np.zeros(1, np.int32), len(d2), num_o,
+                    _c(pose_obs_total, np.float32), rc, oc, df)
+    return rc, oc, df
+
+
+def select(rc, oc, pose_model, num_models, index_base=0):
+    best_cost = np.zeros(num_models, np.int32)
+    best_idx = np.zeros(num_models, np.int64)
+    lib().orc_select(len(rc), _c(rc, np.float32), _c(oc, np.float32), _c(pose_model, np.int32), num_models,
+                     index_base, best_cost, best_idx)
+    return best_cost, best_idx
+
+
+def evaluate(tris, tris_model_count, poses, pose_model, pose_label, width, height, proj, src_depth, src_mask,
+             occlusion_threshold, stride, cx, cy, fx, fy, depth_factor, o_xyz, label_start, label_end,
+             pose_obs_total, cost_type, calc_obs, sensor_resolution, nthreads=0):
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    o_xyz = _c(o_xyz, np.float32).reshape(-1)
+    rc = np.zeros(n, np.float32)
+    oc = np.zeros(n, np.float32)
+    df = np.zeros(n, np.float32)
+    nl = 0 if label_start is None else len(label_start)
+    lib().orc_evaluate(tris, tris.size // 9, _c(tris_model_count, np.int32), len(tris_model_count), poses,
+                       _c(pose_model, np.int32), _c(pose_label, np.int32), n, width, height, _c(proj, np.float32),
+                       _c(src_depth, np.int32).reshape(-1),
+                       None if src_mask is None else _c(src_mask, np.uint8).reshape(-1), float(occlusion_threshold),
+                       stride, cx, cy, fx, fy, depth_factor,
+                       o_xyz if o_xyz.size else np.zeros(3, np.float32), o_xyz.size // 3,
+                       _c(label_start, np.int32), _c(label_end, np.int32), nl, _c(pose_obs_total, np.float32),
+                       cost_type, int(calc_obs), sensor_resolution, rc, oc, df, nthreads)
+    return rc, oc, df

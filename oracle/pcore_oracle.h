@@ -1,0 +1,85 @@
+/*
+ * pcore_oracle.h -- CPU restatement of the reference render-and-compare hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in perception_amd/ links, loads or calls this
+ * library: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it,
+ * and only as the checker / the reported CPU baseline.
+ *
+ * Parity status (see DESIGN.md "Oracle"):
+ *   - The reference's own path (CUDA + Thrust + Eigen + assimp + OpenCV + fast_gicp) cannot be
+ *     built in this image (no nvcc, no Eigen/OpenCV/assimp headers, fast_gicp not vendored), and
+ *     the reference holds no golden vectors for this path.  The raster,
+ *     unprojection, cost and selection restatements are therefore pinned only by analytic
+ *     known-answer tests: "parity unpinned" against the reference binary.
+ *   - KNN tie-break and GICP arithmetic live in the un-vendored fast_gicp fork: build-owned spec,
+ *     parity unpinned.
+ *
+ * Float semantics: compiled with -ffp-contract=off -fno-fast-math, IEEE f32 (SSE) division, no FMA.
+ * The GPU kernels follow the same explicit operation order; the reference's NVIDIA conversions
+ * (cvt.rzi.s32.f32 / cvt.rzi.u64.f32: NaN -> 0, saturating) are spelled out as helpers.
+ */
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* renderer.cu:1386-1410 compute_proj (near/far defaults renderer.h:87). out: mat4x4 a0..d3 row-major. */
+void orc_compute_proj(float fx, float fy, float cx, float cy, int width, int height,
+                      float near_plane, float far_plane, float out[16]);
+
+/* image_renderer.cuh:212-321 render_triangle_multi + 59-210 rasterization_with_source + 465-472
+ * max2zero, executed serially (triangle order) per pose.  tris: T x 9 floats (v0,v1,v2 xyz).
+ * tris_model_count: triangles per model (image_renderer.cuh:371-380 scans).  pose_label NULL = 3-DoF
+ * (no segmentation label, image_renderer.cuh:426-432).  src_mask used only when pose_label != NULL.
+ * out: N x H x W int32 (cm). */
+void orc_render_depth(const float* tris, int num_tris, const int32_t* tris_model_count, int num_models,
+                      const float* poses, const int32_t* pose_model, const int32_t* pose_label, int num_poses,
+                      int width, int height, const float* proj,
+                      const int32_t* src_depth, const uint8_t* src_mask, float occlusion_threshold,
+                      int32_t* out, int nthreads);
+
+/* compute_point_clouds.cuh:37-184 + 265-346: stride mask, exclusive scan (pose-major, row, col),
+ * unprojection.  label_mask (H x W, only valid for num_poses == 1) -> observed cloud, label = mask-1;
+ * else pose_label (nullable) -> rendered cloud label.  Writes at most `cap` points; returns the
+ * total count.  xyz: AoS cap x 3. */
+int orc_depth_to_cloud(const int32_t* depth, int num_poses, int width, int height, int stride,
+                       float cx, float cy, float fx, float fy, float depth_factor,
+                       const uint8_t* label_mask, const int32_t* pose_label,
+                       float* out_xyz, int32_t* out_pose, int32_t* out_label, int cap);
+
+/* fast_gicp::brute_force_knn_search(k=1) as called at renderer.cu:1852-1871 (label-restricted
+ * via observed_label_indices).  Build-owned spec: squared distance ((dx*dx + dy*dy) + dz*dz),
+ * dx = r - o; minimum, ties -> lowest observed index; empty range -> (+inf, -1).
+ * label_start/label_end == NULL: search the whole observed cloud (3-DoF). */
+void orc_knn1(const float* r_xyz, const int32_t* r_label, int num_r,
+              const float* o_xyz, int num_o, const int32_t* label_start, const int32_t* label_end,
+              int num_labels, float* out_d2, int32_t* out_idx);
+
+/* compute_costs.cuh:293-457 for cost_type 0 / 2 (depth only).  sensor_resolution is squared here,
+ * as renderer.cu:1877 does before calling compute_costs. */
+void orc_costs(int num_poses, int cost_type, int calc_obs, float sensor_resolution,
+               const float* d2, const int32_t* idx, const int32_t* r_pose, int num_r, int num_o,
+               const float* pose_obs_total, float* out_rc, float* out_oc, float* out_diff);
+
+/* search_env.cpp:1987-2051 (int cost) + 2542-2583 (per-model argmin, strict '<', |t-s| < 30).
+ * Host int conversions follow x86 cvttss2si (NaN / out of range -> INT_MIN).
+ * out_best_cost[m] = INT_MAX and out_best_index[m] = -1 when no pose qualifies. */
+void orc_select(int num_poses, const float* rc, const float* oc, const int32_t* pose_model,
+                int num_models, int64_t index_base, int32_t* out_best_cost, int64_t* out_best_index);
+
+/* Fused per-pose CPU pipeline (render full frame -> stride cloud -> 1-NN -> costs), OpenMP over
+ * poses.  Used as the timed CPU baseline and as the large-N checker.  o_xyz is label-sorted AoS. */
+void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_count, int num_models,
+                  const float* poses, const int32_t* pose_model, const int32_t* pose_label, int num_poses,
+                  int width, int height, const float* proj,
+                  const int32_t* src_depth, const uint8_t* src_mask, float occlusion_threshold,
+                  int stride, float cx, float cy, float fx, float fy, float depth_factor,
+                  const float* o_xyz, int num_o, const int32_t* label_start, const int32_t* label_end,
+                  int num_labels, const float* pose_obs_total, int cost_type, int calc_obs,
+                  float sensor_resolution, float* out_rc, float* out_oc, float* out_diff, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,92 @@
+"""ctypes binding of libpcore.so (include/pcore.h).
+
+The product path has no CPU fallback: if the HIP library is missing or fails to load, importing the
+binding raises.  `load()` never builds implicitly on a machine without hipcc.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+PCORE_OK = 0
+PCORE_E_INVALID_ARG = 1
+PCORE_E_HIP = 2
+PCORE_E_OOM = 3
+PCORE_E_STATE = 4
+PCORE_KEY_NONE = 0x7FFFFFFFFFFFFFFF
+
+COST_DEPTH_3DOF = 0
+COST_RGBD_3DOF = 1
+COST_DEPTH_6DOF = 2
+
+# every symbol declared in include/pcore.h
+EXPORTED_SYMBOLS = (
+    "pcore_create", "pcore_destroy", "pcore_last_error", "pcore_abi_version", "pcore_upload_meshes",
+    "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_render",
+    "pcore_depth_to_cloud", "pcore_select",
+)
+
+
+class PcoreError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"pcore error {code}: {msg}")
+        self.code = code
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("fx", ctypes.c_float),
+                ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("proj", ctypes.c_float * 16)]
+
+
+class EvalParams(ctypes.Structure):
+    _fields_ = [("cost_type", ctypes.c_int32), ("calc_obs_cost", ctypes.c_int32), ("stride", ctypes.c_int32),
+                ("depth_factor", ctypes.c_float), ("sensor_resolution", ctypes.c_float),
+                ("occlusion_threshold", ctypes.c_float)]
+
+
+_lib = None
+
+
+def library_path() -> str:
+    return _build.LIB
+
+
+def load(auto_build: bool = True) -> ctypes.CDLL:
+    """Load libpcore.so (building it in-tree first when hipcc is available and sources are newer)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if auto_build:
+        try:
+            if _build.needs_build():
+                _build.build()
+        except (RuntimeError, OSError) as e:  # no hipcc on this machine: fall through to the prebuilt .so
+            if not os.path.exists(_build.LIB):
+                raise RuntimeError(f"libpcore.so is missing and cannot be built: {e}") from e
+    if not os.path.exists(_build.LIB):
+        raise RuntimeError(f"libpcore.so not found at {_build.LIB}; run `python -m perception_amd.build`")
+    L = ctypes.CDLL(_build.LIB)
+    vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    L.pcore_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.pcore_destroy.argtypes = [vp]
+    L.pcore_destroy.restype = None
+    L.pcore_last_error.argtypes = [vp]
+    L.pcore_last_error.restype = ctypes.c_char_p
+    L.pcore_abi_version.argtypes = []
+    L.pcore_upload_meshes.argtypes = [vp, vp, vp, i32, vp, i32]
+    L.pcore_set_camera.argtypes = [vp, ctypes.POINTER(Camera)]
+    L.pcore_observed_cloud.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, vp, i32, ctypes.POINTER(i32), vp]
+    L.pcore_set_observation.argtypes = [vp, vp, vp, vp, vp, i32, f32, vp]
+    L.pcore_evaluate.argtypes = [vp, vp, vp, vp, vp, i32, ctypes.POINTER(EvalParams), vp, vp, vp, vp, vp]
+    L.pcore_render.argtypes = [vp, vp, vp, vp, i32, f32, vp, vp]
+    L.pcore_depth_to_cloud.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, i32,
+                                       ctypes.POINTER(i32), vp]
+    L.pcore_select.argtypes = [vp, vp, vp, vp, i32, i64, i32, vp, vp]
+    for name in EXPORTED_SYMBOLS:
+        if name not in ("pcore_destroy", "pcore_last_error"):
+            getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L

@@ -1,0 +1,192 @@
+"""PoseCore: the device-side context of the pose-search core, driven with PyTorch-ROCm tensors.
+
+This is the Python face of include/pcore.h.  Every array argument of the per-batch calls is a CUDA
+(HIP) torch tensor; its data_ptr() goes straight into the C ABI, and the work runs on torch's
+current stream.  There is no CPU fallback: a missing libpcore.so or a non-GPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _native
+from ._native import Camera, EvalParams, PcoreError
+
+
+def _ptr(t: Optional[torch.Tensor], dtype: torch.dtype, name: str):
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name}: expected a GPU torch tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream: Optional[torch.cuda.Stream]):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class PoseCore:
+    """One context per (host thread, device), like the reference's single-threaded caller
+    (search_env.cpp:2506-2525)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _native.load()
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        rc = self.lib.pcore_create(self.device, ctypes.byref(h))
+        if rc != _native.PCORE_OK:
+            raise PcoreError(rc, f"pcore_create(device={device}) failed")
+        self._h = h
+        self.width = self.height = 0
+        self.num_models = 0
+
+    # -- lifetime ---------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.pcore_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != _native.PCORE_OK:
+            msg = self.lib.pcore_last_error(self._h)
+            raise PcoreError(rc, msg.decode() if msg else "")
+
+    # -- static inputs ----------------------------------------------------------------------------
+    def upload_meshes(self, tris: np.ndarray, tris_model_count, colors: Optional[np.ndarray] = None):
+        tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        cnt = np.ascontiguousarray(tris_model_count, dtype=np.int32)
+        col = None if colors is None else np.ascontiguousarray(colors, dtype=np.uint8).reshape(-1, 3)
+        self._check(self.lib.pcore_upload_meshes(
+            self._h, tris.ctypes.data_as(ctypes.c_void_p),
+            None if col is None else col.ctypes.data_as(ctypes.c_void_p), tris.shape[0],
+            cnt.ctypes.data_as(ctypes.c_void_p), cnt.shape[0]))
+        self.num_models = int(cnt.shape[0])
+
+    def set_camera(self, width: int, height: int, fx: float, fy: float, cx: float, cy: float, proj: np.ndarray):
+        cam = Camera()
+        cam.width, cam.height = int(width), int(height)
+        cam.fx, cam.fy, cam.cx, cam.cy = float(fx), float(fy), float(cx), float(cy)
+        pj = np.asarray(proj, dtype=np.float32).reshape(16)
+        for i in range(16):
+            cam.proj[i] = float(pj[i])
+        self._check(self.lib.pcore_set_camera(self._h, ctypes.byref(cam)))
+        self.width, self.height = int(width), int(height)
+
+    # -- per-scene inputs -------------------------------------------------------------------------
+    def observed_cloud(self, depth: torch.Tensor, label_mask: Optional[torch.Tensor], stride: int,
+                       depth_factor: float, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """depth2cloud_global (renderer.cu:1936-2069): returns (xyz (P,3) f32, label (P,) i32) on the GPU."""
+        h, w = depth.shape[-2:]
+        cap = ((w + stride - 1) // stride) * ((h + stride - 1) // stride)
+        xyz = torch.empty((max(cap, 1), 3), dtype=torch.float32, device=depth.device)
+        lab = torch.empty((max(cap, 1),), dtype=torch.int32, device=depth.device)
+        cnt = ctypes.c_int32(0)
+        self._check(self.lib.pcore_observed_cloud(
+            self._h, _ptr(depth, torch.int32, "depth"), _ptr(label_mask, torch.uint8, "label_mask"), w, h, stride,
+            float(depth_factor), _ptr(xyz, torch.float32, "xyz"), _ptr(lab, torch.int32, "label"), cap,
+            ctypes.byref(cnt), _stream(stream)))
+        n = cnt.value
+        return xyz[:n], lab[:n]
+
+    def set_observation(self, src_depth_cm: torch.Tensor, src_mask: Optional[torch.Tensor],
+                        obs_xyz: torch.Tensor, obs_label: Optional[torch.Tensor], sensor_resolution: float,
+                        stream=None):
+        obs_xyz = obs_xyz.contiguous()
+        n = int(obs_xyz.shape[0])
+        self._check(self.lib.pcore_set_observation(
+            self._h, _ptr(src_depth_cm.contiguous(), torch.int32, "src_depth"),
+            _ptr(None if src_mask is None else src_mask.contiguous(), torch.uint8, "src_mask"),
+            _ptr(obs_xyz, torch.float32, "obs_xyz") if n else None,
+            _ptr(None if obs_label is None else obs_label.contiguous(), torch.int32, "obs_label") if n else None,
+            n, float(sensor_resolution), _stream(stream)))
+
+    # -- per-batch hot path -----------------------------------------------------------------------
+    def evaluate(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
+                 pose_obs_total: Optional[torch.Tensor], cost_type: int = _native.COST_DEPTH_6DOF,
+                 calc_obs_cost: bool = True, stride: int = 8, depth_factor: float = 100.0,
+                 sensor_resolution: float = 0.01, occlusion_threshold: float = 1.0,
+                 out: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
+                 dbg_zs: Optional[torch.Tensor] = None, stream=None):
+        """Stage COST (do_icp = false).  Returns (rendered_cost, observed_cost, points_diff_cost)."""
+        n = int(poses.shape[0])
+        dev = poses.device
+        if out is None:
+            out = tuple(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3))
+        rc, oc, df = out
+        p = EvalParams(int(cost_type), int(bool(calc_obs_cost)), int(stride), float(depth_factor),
+                       float(sensor_resolution), float(occlusion_threshold))
+        self._check(self.lib.pcore_evaluate(
+            self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
+            _ptr(pose_label, torch.int32, "pose_label"), _ptr(pose_obs_total, torch.float32, "pose_obs_total"),
+            n, ctypes.byref(p), _ptr(rc, torch.float32, "rc"), _ptr(oc, torch.float32, "oc"),
+            _ptr(df, torch.float32, "diff"), _ptr(dbg_zs, torch.int32, "dbg_zs"), _stream(stream)))
+        return rc, oc, df
+
+    def render(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
+               occlusion_threshold: float = 1.0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Stage RENDER: (N, H, W) int32 z-buffers in cm."""
+        n = int(poses.shape[0])
+        if out is None:
+            out = torch.empty((n, self.height, self.width), dtype=torch.int32, device=poses.device)
+        self._check(self.lib.pcore_render(
+            self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
+            _ptr(pose_label, torch.int32, "pose_label"), n, float(occlusion_threshold),
+            _ptr(out, torch.int32, "out"), _stream(stream)))
+        return out
+
+    def depth_to_cloud(self, depth: torch.Tensor, stride: int, depth_factor: float,
+                       label_mask: Optional[torch.Tensor] = None, pose_label: Optional[torch.Tensor] = None,
+                       stream=None):
+        """Stage CLOUD (compute_point_clouds): returns (xyz (P,3), pose (P,), label (P,))."""
+        if depth.dim() == 2:
+            depth = depth.unsqueeze(0)
+        n, h, w = depth.shape
+        cap = n * ((w + stride - 1) // stride) * ((h + stride - 1) // stride)
+        xyz = torch.empty((max(cap, 1), 3), dtype=torch.float32, device=depth.device)
+        pose = torch.empty((max(cap, 1),), dtype=torch.int32, device=depth.device)
+        lab = torch.empty((max(cap, 1),), dtype=torch.int32, device=depth.device)
+        cnt = ctypes.c_int32(0)
+        self._check(self.lib.pcore_depth_to_cloud(
+            self._h, _ptr(depth.contiguous(), torch.int32, "depth"), n, w, h, stride, float(depth_factor),
+            _ptr(label_mask, torch.uint8, "label_mask"), _ptr(pose_label, torch.int32, "pose_label"),
+            _ptr(xyz, torch.float32, "xyz"), _ptr(pose, torch.int32, "pose"), _ptr(lab, torch.int32, "label"),
+            cap, ctypes.byref(cnt), _stream(stream)))
+        k = cnt.value
+        return xyz[:k], pose[:k], lab[:k]
+
+    def select(self, rc: torch.Tensor, oc: torch.Tensor, pose_model: torch.Tensor, num_models: int,
+               index_base: int = 0, keys: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Per-model argmin keys (int64), folded into `keys` (initialised to PCORE_KEY_NONE)."""
+        if keys is None:
+            keys = torch.full((num_models,), _native.PCORE_KEY_NONE, dtype=torch.int64, device=rc.device)
+        self._check(self.lib.pcore_select(
+            self._h, _ptr(rc, torch.float32, "rc"), _ptr(oc, torch.float32, "oc"),
+            _ptr(pose_model, torch.int32, "pose_model"), int(rc.shape[0]), int(index_base), int(num_models),
+            _ptr(keys, torch.int64, "keys"), _stream(stream)))
+        return keys
+
+
+def decode_keys(keys) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-model key -> (best cost, best global index); (INT_MAX, -1) where no pose qualified."""
+    k = np.asarray(keys.cpu() if isinstance(keys, torch.Tensor) else keys, dtype=np.int64)
+    none = k == _native.PCORE_KEY_NONE
+    hi = (k >> 31).astype(np.uint64).astype(np.uint32)
+    cost = (hi ^ np.uint32(0x80000000)).view(np.int32).astype(np.int32)
+    idx = (k & 0x7FFFFFFF).astype(np.int64)
+    cost = np.where(none, np.int32(2**31 - 1), cost)
+    idx = np.where(none, -1, idx)
+    return cost, idx

@@ -1,0 +1,587 @@
+// pcore_api.hip -- C ABI (include/pcore.h) of the MI355X pose-search core: context, static inputs
+// (mesh dedupe + meshlets, camera), per-scene observation (label sort + neighbour grids) and dispatch of
+// the kernels in pcore_kernels.hip.  Host code; no hidden allocations on the per-batch path (evaluate /
+// select), scratch for the parity stages grows monotonically.
+#include "../../include/pcore.h"
+#include "pcore_internal.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace pcore;
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct pcore_ctx {
+    int device = 0;
+    std::string err;
+    hipDeviceProp_t prop{};
+    // mesh
+    int num_models = 0;
+    int num_tris = 0;
+    DevBuf<float> tris;          // original triangle soup (parity render)
+    DevBuf<int32_t> tri_lo, tri_hi;
+    DevBuf<float4> mverts;
+    DevBuf<uint32_t> mtris;
+    DevBuf<Meshlet> meshlets;
+    DevBuf<int32_t> model_ml_lo, model_ml_hi;
+    bool have_mesh = false;
+    // camera
+    pcore_camera cam{};
+    DevBuf<float> proj;
+    bool have_cam = false;
+    // observation
+    DevBuf<int32_t> src_depth;
+    DevBuf<uint8_t> src_mask;
+    bool obs_has_mask = false;
+    int sampled_stride = 0;
+    DevBuf<int32_t> src_s;
+    DevBuf<uint8_t> lab_s;
+    DevBuf<LabelGrid> grids;
+    DevBuf<int32_t> cell_start;
+    DevBuf<float4> grid_pts;
+    int num_grids = 0;
+    int bitmap_words = 1;
+    bool have_obs = false;
+    // scratch (parity stages)
+    DevBuf<int32_t> scratch_counts, scratch_offsets, scratch_total;
+};
+
+namespace {
+
+int fail(pcore_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPC(ctx, call)                                                                         \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? PCORE_E_OOM : PCORE_E_HIP,             \
+                        std::string(#call) + ": " + hipGetErrorString(e_));                     \
+    } while (0)
+
+template <typename T>
+hipError_t dev_free(DevBuf<T>& b) {
+    hipError_t e = hipSuccess;
+    if (b.p) e = hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    return e;
+}
+
+template <typename T>
+hipError_t dev_reserve(DevBuf<T>& b, size_t n) {
+    if (b.n >= n && b.p) return hipSuccess;
+    hipError_t e = dev_free(b);
+    if (e != hipSuccess) return e;
+    e = hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) b.n = n;
+    return e;
+}
+
+template <typename T>
+hipError_t dev_upload(DevBuf<T>& b, const std::vector<T>& v) {
+    hipError_t e = dev_reserve(b, v.size());
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
+struct VKey {
+    uint32_t x, y, z;
+    bool operator==(const VKey& o) const { return x == o.x && y == o.y && z == o.z; }
+};
+struct VKeyHash {
+    size_t operator()(const VKey& k) const {
+        uint64_t h = k.x * 0x9E3779B97F4A7C15ull;
+        h ^= (k.y + 0x632BE59BD9B4E019ull) + (h << 6) + (h >> 2);
+        h ^= (k.z + 0x85EBCA77C2B2AE63ull) + (h << 6) + (h >> 2);
+        return (size_t)h;
+    }
+};
+
+// Greedy adjacency-growth meshlet builder for one model.  verts: unique vertex ids per triangle corner.
+void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std::vector<float>& vxyz,
+                    std::vector<float4>& out_v, std::vector<uint32_t>& out_t, std::vector<Meshlet>& out_m) {
+    const int T = (int)tri_verts.size() / 3;
+    std::vector<std::vector<int>> adj(num_verts);
+    for (int t = 0; t < T; t++)
+        for (int k = 0; k < 3; k++) adj[tri_verts[3 * t + k]].push_back(t);
+    std::vector<char> assigned(T, 0);
+    std::vector<int> local(num_verts, -1);
+    int next_seed = 0;
+    std::vector<int> mv;  // meshlet vertex ids
+    std::vector<int> mt;  // meshlet triangles
+    while (true) {
+        while (next_seed < T && assigned[next_seed]) next_seed++;
+        if (next_seed >= T) break;
+        mv.clear();
+        mt.clear();
+        auto add_tri = [&](int t) {
+            assigned[t] = 1;
+            mt.push_back(t);
+            for (int k = 0; k < 3; k++) {
+                const int v = tri_verts[3 * t + k];
+                if (local[v] < 0) {
+                    local[v] = (int)mv.size();
+                    mv.push_back(v);
+                }
+            }
+        };
+        add_tri(next_seed);
+        while ((int)mt.size() < kMeshletMaxTris) {
+            int best = -1, best_score = -1;
+            for (size_t i = 0; i < mv.size(); i++)
+                for (int t : adj[mv[i]]) {
+                    if (assigned[t]) continue;
+                    int shared = 0;
+                    for (int k = 0; k < 3; k++) shared += local[tri_verts[3 * t + k]] >= 0 ? 1 : 0;
+                    if ((int)mv.size() + (3 - shared) > kMeshletMaxVerts) continue;
+                    if (shared > best_score || (shared == best_score && t < best)) {
+                        best_score = shared;
+                        best = t;
+                    }
+                }
+            if (best < 0) break;
+            add_tri(best);
+        }
+        Meshlet m;
+        m.vbase = (int)out_v.size();
+        m.tbase = (int)out_t.size();
+        m.nv = (int)mv.size();
+        m.nt = (int)mt.size();
+        for (int v : mv) out_v.push_back(make_float4(vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], 0.0f));
+        for (int t : mt)
+            out_t.push_back((uint32_t)local[tri_verts[3 * t]] | ((uint32_t)local[tri_verts[3 * t + 1]] << 8) |
+                            ((uint32_t)local[tri_verts[3 * t + 2]] << 16));
+        out_m.push_back(m);
+        for (int v : mv) local[v] = -1;
+    }
+}
+
+// Neighbour grid over one point set.  `pts` are (x,y,z, local index) in label-sorted order.
+void build_grid(const std::vector<float4>& pts, float radius, LabelGrid& g, std::vector<int32_t>& cell_start,
+                std::vector<float4>& grid_pts) {
+    g = LabelGrid{};
+    g.pt_count = (int)pts.size();
+    g.cell_base = (int)cell_start.size();
+    if (pts.empty()) {
+        g.ox = g.oy = g.oz = 0.0f;
+        g.inv_c = 1.0f;
+        g.nx = g.ny = g.nz = 1;
+        cell_start.push_back((int32_t)grid_pts.size());
+        cell_start.push_back((int32_t)grid_pts.size());
+        return;
+    }
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const float4& p : pts) {
+        const float c[3] = {p.x, p.y, p.z};
+        for (int k = 0; k < 3; k++) {
+            if (!std::isfinite(c[k])) continue;
+            lo[k] = std::min(lo[k], c[k]);
+            hi[k] = std::max(hi[k], c[k]);
+        }
+    }
+    for (int k = 0; k < 3; k++)
+        if (!(lo[k] <= hi[k])) { lo[k] = 0.0f; hi[k] = 0.0f; }
+    // cell >= 2r so a query's radius box touches <= 2 cells per axis; at most 64 cells per axis
+    const float ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+    float cell = std::max(2.0f * radius * 1.01f, ext / 64.0f);
+    if (!(cell > 0.0f)) cell = 1.0f;
+    g.ox = lo[0];
+    g.oy = lo[1];
+    g.oz = lo[2];
+    g.inv_c = 1.0f / cell;
+    g.nx = std::max(1, (int)std::floor((hi[0] - lo[0]) * g.inv_c) + 1);
+    g.ny = std::max(1, (int)std::floor((hi[1] - lo[1]) * g.inv_c) + 1);
+    g.nz = std::max(1, (int)std::floor((hi[2] - lo[2]) * g.inv_c) + 1);
+    const int ncell = g.nx * g.ny * g.nz;
+    std::vector<int> cell_of(pts.size());
+    std::vector<int> cnt(ncell + 1, 0);
+    for (size_t i = 0; i < pts.size(); i++) {
+        // same float formula as the device query (pcore_kernels.hip, process_points)
+        const float fx = (pts[i].x - g.ox) * g.inv_c, fy = (pts[i].y - g.oy) * g.inv_c, fz = (pts[i].z - g.oz) * g.inv_c;
+        int ix = (int)std::floor(std::max(fx, 0.0f)), iy = (int)std::floor(std::max(fy, 0.0f)),
+            iz = (int)std::floor(std::max(fz, 0.0f));
+        if (!std::isfinite(fx) || !std::isfinite(fy) || !std::isfinite(fz)) {
+            cell_of[i] = -1;  // non-finite points can never be within the radius of a finite query
+            continue;
+        }
+        ix = std::min(ix, g.nx - 1);
+        iy = std::min(iy, g.ny - 1);
+        iz = std::min(iz, g.nz - 1);
+        cell_of[i] = (iz * g.ny + iy) * g.nx + ix;
+        cnt[cell_of[i] + 1]++;
+    }
+    for (int c = 0; c < ncell; c++) cnt[c + 1] += cnt[c];
+    const int base = (int)grid_pts.size();
+    grid_pts.resize(base + cnt[ncell]);
+    std::vector<int> fillp(cnt.begin(), cnt.end() - 1);
+    for (size_t i = 0; i < pts.size(); i++)
+        if (cell_of[i] >= 0) grid_pts[base + fillp[cell_of[i]]++] = pts[i];
+    for (int c = 0; c <= ncell; c++) cell_start.push_back(base + cnt[c]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pcore_abi_version(void) { return PCORE_ABI_VERSION; }
+
+int pcore_create(int device, pcore_ctx** out_ctx) {
+    if (!out_ctx) return PCORE_E_INVALID_ARG;
+    *out_ctx = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return PCORE_E_INVALID_ARG;
+    pcore_ctx* c = new pcore_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&c->prop, device) != hipSuccess) {
+        delete c;
+        return PCORE_E_HIP;
+    }
+    *out_ctx = c;
+    return PCORE_OK;
+}
+
+void pcore_destroy(pcore_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)dev_free(c->tris); (void)dev_free(c->tri_lo); (void)dev_free(c->tri_hi);
+    (void)dev_free(c->mverts); (void)dev_free(c->mtris); (void)dev_free(c->meshlets);
+    (void)dev_free(c->model_ml_lo); (void)dev_free(c->model_ml_hi); (void)dev_free(c->proj);
+    (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
+    (void)dev_free(c->grids); (void)dev_free(c->cell_start); (void)dev_free(c->grid_pts);
+    (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
+    delete c;
+}
+
+const char* pcore_last_error(const pcore_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_rgb, int32_t num_tris,
+                        const int32_t* tris_model_count, int32_t num_models) {
+    (void)tri_rgb;  // colour is only used by cost type 1 (not implemented yet)
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!tri_xyz || num_tris <= 0 || !tris_model_count || num_models <= 0)
+        return fail(c, PCORE_E_INVALID_ARG, "upload_meshes: empty mesh");
+    long long acc = 0;
+    for (int m = 0; m < num_models; m++) {
+        if (tris_model_count[m] < 0) return fail(c, PCORE_E_INVALID_ARG, "upload_meshes: negative count");
+        acc += tris_model_count[m];
+    }
+    if (acc != num_tris) return fail(c, PCORE_E_INVALID_ARG, "upload_meshes: sum(tris_model_count) != num_tris");
+    HIPC(c, hipSetDevice(c->device));
+
+    std::vector<float4> mv;
+    std::vector<uint32_t> mt;
+    std::vector<Meshlet> ml;
+    std::vector<int32_t> mlo(num_models), mhi(num_models), tlo(num_models), thi(num_models);
+    int t0 = 0;
+    for (int m = 0; m < num_models; m++) {
+        const int T = tris_model_count[m];
+        tlo[m] = t0;
+        thi[m] = t0 + T;
+        // exact-bit vertex dedupe within the model
+        std::unordered_map<VKey, int, VKeyHash> idx;
+        idx.reserve((size_t)T * 2);
+        std::vector<int> tv((size_t)T * 3);
+        std::vector<float> vxyz;
+        for (int t = 0; t < T; t++)
+            for (int k = 0; k < 3; k++) {
+                const float* p = tri_xyz + (size_t)9 * (t0 + t) + 3 * k;
+                VKey key;
+                std::memcpy(&key.x, &p[0], 4);
+                std::memcpy(&key.y, &p[1], 4);
+                std::memcpy(&key.z, &p[2], 4);
+                auto it = idx.find(key);
+                int id;
+                if (it == idx.end()) {
+                    id = (int)(vxyz.size() / 3);
+                    idx.emplace(key, id);
+                    vxyz.push_back(p[0]);
+                    vxyz.push_back(p[1]);
+                    vxyz.push_back(p[2]);
+                } else {
+                    id = it->second;
+                }
+                tv[(size_t)3 * t + k] = id;
+            }
+        mlo[m] = (int)ml.size();
+        build_meshlets(tv, (int)(vxyz.size() / 3), vxyz, mv, mt, ml);
+        mhi[m] = (int)ml.size();
+        t0 += T;
+    }
+    std::vector<float> soup(tri_xyz, tri_xyz + (size_t)9 * num_tris);
+    HIPC(c, dev_upload(c->tris, soup));
+    HIPC(c, dev_upload(c->tri_lo, tlo));
+    HIPC(c, dev_upload(c->tri_hi, thi));
+    HIPC(c, dev_upload(c->mverts, mv));
+    HIPC(c, dev_upload(c->mtris, mt));
+    HIPC(c, dev_upload(c->meshlets, ml));
+    HIPC(c, dev_upload(c->model_ml_lo, mlo));
+    HIPC(c, dev_upload(c->model_ml_hi, mhi));
+    c->num_models = num_models;
+    c->num_tris = num_tris;
+    c->have_mesh = true;
+    return PCORE_OK;
+}
+
+int pcore_set_camera(pcore_ctx* c, const pcore_camera* cam) {
+    if (!c || !cam) return PCORE_E_INVALID_ARG;
+    if (cam->width <= 0 || cam->height <= 0 || cam->width > 16384 || cam->height > 16384)
+        return fail(c, PCORE_E_INVALID_ARG, "set_camera: bad image size");
+    HIPC(c, hipSetDevice(c->device));
+    c->cam = *cam;
+    std::vector<float> pj(cam->proj, cam->proj + 16);
+    HIPC(c, dev_upload(c->proj, pj));
+    c->have_cam = true;
+    c->have_obs = false;  // observation is tied to the image size
+    c->sampled_stride = 0;
+    return PCORE_OK;
+}
+
+int pcore_observed_cloud(pcore_ctx* c, const int32_t* d_depth, const uint8_t* d_label_mask, int32_t width,
+                         int32_t height, int32_t stride, float depth_factor, float* d_out_xyz, int32_t* d_out_label,
+                         int32_t cap, int32_t* out_count, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!c->have_cam) return fail(c, PCORE_E_STATE, "observed_cloud: camera not set");
+    return pcore_depth_to_cloud(c, d_depth, 1, width, height, stride, depth_factor, d_label_mask, nullptr, d_out_xyz,
+                                nullptr, d_out_label, cap, out_count, stream);
+}
+
+int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uint8_t* d_src_mask,
+                          const float* d_obs_xyz, const int32_t* d_obs_label, int32_t num_obs,
+                          float sensor_resolution, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!c->have_cam) return fail(c, PCORE_E_STATE, "set_observation: camera not set");
+    if (!d_src_depth_cm || num_obs < 0 || (num_obs > 0 && !d_obs_xyz))
+        return fail(c, PCORE_E_INVALID_ARG, "set_observation: bad arguments");
+    if (!(sensor_resolution >= 0.0f)) return fail(c, PCORE_E_INVALID_ARG, "set_observation: bad sensor_resolution");
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t npx = (size_t)c->cam.width * c->cam.height;
+    HIPC(c, dev_reserve(c->src_depth, npx));
+    HIPC(c, hipMemcpyAsync(c->src_depth.p, d_src_depth_cm, npx * 4, hipMemcpyDeviceToDevice, s));
+    c->obs_has_mask = d_src_mask != nullptr;
+    HIPC(c, dev_reserve(c->src_mask, npx));
+    if (d_src_mask) HIPC(c, hipMemcpyAsync(c->src_mask.p, d_src_mask, npx, hipMemcpyDeviceToDevice, s));
+    else HIPC(c, hipMemsetAsync(c->src_mask.p, 0, npx, s));
+
+    // observed cloud -> host: stable label sort (renderer.cu:1674-1686) + neighbour grids
+    std::vector<float> xyz((size_t)num_obs * 3);
+    std::vector<int32_t> lab(num_obs, 0);
+    if (num_obs > 0) {
+        HIPC(c, hipMemcpyAsync(xyz.data(), d_obs_xyz, xyz.size() * 4, hipMemcpyDeviceToHost, s));
+        if (d_obs_label) HIPC(c, hipMemcpyAsync(lab.data(), d_obs_label, lab.size() * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPC(c, hipStreamSynchronize(s));
+    int max_label = -1;
+    for (int i = 0; i < num_obs; i++) max_label = std::max(max_label, lab[i]);
+    const int num_labels = std::max(0, max_label + 1);
+    std::vector<int> order(num_obs);
+    for (int i = 0; i < num_obs; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lab[a] < lab[b]; });
+    std::vector<LabelGrid> grids(num_labels + 1);
+    std::vector<int32_t> cell_start;
+    std::vector<float4> gpts;
+    int max_cnt = 0;
+    // per-label grids (6-DoF): points with negative labels are never matched (no rendered label < 0)
+    for (int L = 0; L < num_labels; L++) {
+        std::vector<float4> pts;
+        int local = 0;
+        for (int i : order)
+            if (lab[i] == L) {
+                float4 p = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.0f);
+                int li = local++;
+                std::memcpy(&p.w, &li, 4);
+                pts.push_back(p);
+            }
+        max_cnt = std::max(max_cnt, (int)pts.size());
+        build_grid(pts, sensor_resolution, grids[L], cell_start, gpts);
+    }
+    // 3-DoF grid over the whole cloud, in label-sorted order
+    {
+        std::vector<float4> pts;
+        for (int k = 0; k < num_obs; k++) {
+            const int i = order[k];
+            float4 p = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.0f);
+            std::memcpy(&p.w, &k, 4);
+            pts.push_back(p);
+        }
+        max_cnt = std::max(max_cnt, (int)pts.size());
+        build_grid(pts, sensor_resolution, grids[num_labels], cell_start, gpts);
+    }
+    HIPC(c, dev_upload(c->grids, grids));
+    HIPC(c, dev_upload(c->cell_start, cell_start));
+    HIPC(c, dev_upload(c->grid_pts, gpts));
+    c->num_grids = num_labels;
+    c->bitmap_words = std::max(1, (max_cnt + 31) / 32);
+    c->sampled_stride = 0;
+    c->have_obs = true;
+    return PCORE_OK;
+}
+
+static int ensure_sampled(pcore_ctx* c, int stride, hipStream_t s) {
+    if (c->sampled_stride == stride) return PCORE_OK;
+    const int ws = (c->cam.width + stride - 1) / stride, hs = (c->cam.height + stride - 1) / stride;
+    HIPC(c, dev_reserve(c->src_s, (size_t)ws * hs));
+    HIPC(c, dev_reserve(c->lab_s, (size_t)ws * hs));
+    HIPC(c, launch_sample_source(c->src_depth.p, c->src_mask.p, c->cam.width, c->cam.height, stride, c->src_s.p,
+                                 c->lab_s.p, s));
+    c->sampled_stride = stride;
+    return PCORE_OK;
+}
+
+int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
+                   const float* d_pose_obs_total, int32_t num_poses, const pcore_eval_params* p, float* d_out_rc,
+                   float* d_out_oc, float* d_out_diff, int32_t* d_dbg_zs, pcore_stream stream) {
+    if (!c || !p) return PCORE_E_INVALID_ARG;
+    if (!c->have_mesh || !c->have_cam || !c->have_obs)
+        return fail(c, PCORE_E_STATE, "evaluate: meshes, camera and observation must be set first");
+    if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_rc)))
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate: null pose / output pointer");
+    if (p->cost_type == PCORE_COST_RGBD_3DOF)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate: cost_type 1 (CIEDE2000 colour) is not implemented");
+    if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate: unknown cost_type");
+    if (num_poses == 0) return PCORE_OK;
+    if (p->cost_type == PCORE_COST_DEPTH_6DOF && (!d_pose_label || !c->obs_has_mask))
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate: cost_type 2 needs pose labels and a source mask");
+    if (p->calc_obs_cost && (!d_pose_obs_total || !d_out_oc || !d_out_diff))
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate: calc_obs_cost needs pose_obs_total and oc/diff outputs");
+    const int W = c->cam.width, H = c->cam.height;
+    if (p->stride <= 0 || W % p->stride != 0)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate: width must be a multiple of stride");
+    const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
+    if (ws > 4095 || hs > 4095) return fail(c, PCORE_E_INVALID_ARG, "evaluate: sampled image too large");
+    const size_t lds = fused_lds_bytes(ws, hs, c->bitmap_words);
+    if (lds > (size_t)c->prop.sharedMemPerBlock)
+        return fail(c, PCORE_E_INVALID_ARG,
+                    "evaluate: sampled z-buffer does not fit in LDS (use a larger stride); need " +
+                        std::to_string(lds) + " B");
+    if (num_poses == 0) return PCORE_OK;
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_sampled(c, p->stride, s);
+    if (rc != PCORE_OK) return rc;
+
+    FusedArgs a{};
+    a.poses = d_poses;
+    a.pose_model = d_pose_model;
+    a.pose_label = (p->cost_type == PCORE_COST_DEPTH_6DOF) ? d_pose_label : nullptr;
+    a.pose_obs_total = d_pose_obs_total;
+    a.num_poses = num_poses;
+    a.mverts = c->mverts.p;
+    a.mtris = c->mtris.p;
+    a.meshlets = c->meshlets.p;
+    a.model_ml_lo = c->model_ml_lo.p;
+    a.model_ml_hi = c->model_ml_hi.p;
+    a.num_models = c->num_models;
+    const float* pj = c->cam.proj;
+    a.p00 = pj[0]; a.p01 = pj[1]; a.p02 = pj[2]; a.p03 = pj[3];
+    a.p10 = pj[4]; a.p11 = pj[5]; a.p12 = pj[6]; a.p13 = pj[7];
+    a.width = W;
+    a.height = H;
+    a.stride = p->stride;
+    a.ws = ws;
+    a.hs = hs;
+    a.cx = c->cam.cx; a.cy = c->cam.cy; a.fx = c->cam.fx; a.fy = c->cam.fy;
+    a.depth_factor = p->depth_factor;
+    a.src_s = c->src_s.p;
+    a.lab_s = c->lab_s.p;
+    a.grids = c->grids.p;
+    a.cell_start = c->cell_start.p;
+    a.grid_pts = c->grid_pts.p;
+    a.num_grids = c->num_grids;
+    a.bitmap_words = c->bitmap_words;
+    a.r2 = p->sensor_resolution * p->sensor_resolution;  // renderer.cu:1877
+    a.occlusion_threshold = p->occlusion_threshold;
+    a.calc_obs = p->calc_obs_cost;
+    a.out_rc = d_out_rc;
+    a.out_oc = d_out_oc;
+    a.out_diff = d_out_diff;
+    a.dbg_zs = d_dbg_zs;
+    HIPC(c, launch_fused_cost(a, s));
+    return PCORE_OK;
+}
+
+int pcore_render(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
+                 int32_t num_poses, float occlusion_threshold, int32_t* d_out_depth, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!c->have_mesh || !c->have_cam || !c->have_obs)
+        return fail(c, PCORE_E_STATE, "render: meshes, camera and observation must be set first");
+    if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_depth)))
+        return fail(c, PCORE_E_INVALID_ARG, "render: null pointer");
+    if (d_pose_label && !c->obs_has_mask)
+        return fail(c, PCORE_E_INVALID_ARG, "render: pose labels need a source mask");
+    if (num_poses == 0) return PCORE_OK;
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    const int W = c->cam.width, H = c->cam.height;
+    HIPC(c, launch_fill_i32(d_out_depth, INT_MAX, (size_t)num_poses * W * H, s));
+    HIPC(c, launch_render_full(c->tris.p, c->num_tris, c->tri_lo.p, c->tri_hi.p, d_poses, d_pose_model, num_poses, W,
+                               H, c->proj.p, d_out_depth, s));
+    HIPC(c, launch_render_finalize(d_out_depth, c->src_depth.p, c->src_mask.p, d_pose_label, num_poses, W, H,
+                                   occlusion_threshold, s));
+    return PCORE_OK;
+}
+
+int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,
+                         int32_t stride, float depth_factor, const uint8_t* d_label_mask, const int32_t* d_pose_label,
+                         float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label, int32_t cap, int32_t* out_count,
+                         pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!c->have_cam) return fail(c, PCORE_E_STATE, "depth_to_cloud: camera not set");
+    if (num_poses < 0 || width <= 0 || height <= 0 || stride <= 0 || !d_depth || cap < 0 ||
+        (cap > 0 && !d_out_xyz) || !out_count)
+        return fail(c, PCORE_E_INVALID_ARG, "depth_to_cloud: bad arguments");
+    if (width % stride != 0) return fail(c, PCORE_E_INVALID_ARG, "depth_to_cloud: width % stride != 0");
+    if (d_label_mask && num_poses != 1)
+        return fail(c, PCORE_E_INVALID_ARG, "depth_to_cloud: label mask needs num_poses == 1");
+    *out_count = 0;
+    if (num_poses == 0) return PCORE_OK;
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(c, dev_reserve(c->scratch_counts, num_poses));
+    HIPC(c, dev_reserve(c->scratch_offsets, num_poses));
+    HIPC(c, dev_reserve(c->scratch_total, 1));
+    HIPC(c, launch_cloud_count(d_depth, num_poses, width, height, stride, d_label_mask, c->scratch_counts.p, s));
+    HIPC(c, launch_exclusive_scan(c->scratch_counts.p, c->scratch_offsets.p, num_poses, c->scratch_total.p, s));
+    HIPC(c, launch_cloud_write(d_depth, num_poses, width, height, stride, c->cam.cx, c->cam.cy, c->cam.fx, c->cam.fy,
+                               depth_factor, d_label_mask, d_pose_label, c->scratch_offsets.p, d_out_xyz, d_out_pose,
+                               d_out_label, cap, s));
+    int32_t total = 0;
+    HIPC(c, hipMemcpyAsync(&total, c->scratch_total.p, 4, hipMemcpyDeviceToHost, s));
+    HIPC(c, hipStreamSynchronize(s));
+    *out_count = total;
+    return PCORE_OK;
+}
+
+int pcore_select(pcore_ctx* c, const float* d_rc, const float* d_oc, const int32_t* d_pose_model, int32_t num_poses,
+                 int64_t index_base, int32_t num_models, int64_t* d_keys, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (num_poses < 0 || num_models <= 0 || index_base < 0 || index_base + num_poses > 0x7fffffffLL ||
+        (num_poses > 0 && (!d_rc || !d_oc || !d_pose_model || !d_keys)))
+        return fail(c, PCORE_E_INVALID_ARG, "select: bad arguments");
+    if (num_poses == 0) return PCORE_OK;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, launch_select(d_rc, d_oc, d_pose_model, num_poses, index_base, num_models, d_keys, (hipStream_t)stream));
+    return PCORE_OK;
+}
+
+}  // extern "C"

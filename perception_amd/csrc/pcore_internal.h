@@ -1,0 +1,91 @@
+// pcore_internal.h -- data layouts shared by the host API (pcore_api.hip) and the kernels
+// (pcore_kernels.hip).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pcore {
+
+// Meshlet: <= 64 unique vertices and <= 128 triangles of one model.  Vertices are stored per meshlet
+// (float4 x,y,z,0 in metres) so one lane loads one vertex with a single 16-byte load; triangles are
+// packed local indices i0 | i1 << 8 | i2 << 16.
+constexpr int kMeshletMaxVerts = 64;
+constexpr int kMeshletMaxTris = 128;
+struct Meshlet {
+    int32_t vbase;  // first vertex in mverts
+    int32_t tbase;  // first triangle in mtris
+    int32_t nv;
+    int32_t nt;
+};
+
+// Fixed-radius neighbour grid over the observed points of one label (6-DoF) or of the whole cloud
+// (3-DoF).  Cells are >= 2 * sensor_resolution wide, so every point within the radius of a query lies
+// in the <= 2 x 2 x 2 cells its radius box touches.  Points are stored cell-sorted as float4
+// (x, y, z, bitcast(label-local index)).
+struct LabelGrid {
+    float ox, oy, oz, inv_c;
+    int32_t nx, ny, nz;
+    int32_t cell_base;  // offset of this grid's CSR row pointer in cell_start (nx*ny*nz + 1 entries)
+    int32_t pt_count;   // points of this label (bitmap size)
+    int32_t pad0, pad1, pad2;
+};
+
+struct FusedArgs {
+    // batch
+    const float* poses;
+    const int32_t* pose_model;
+    const int32_t* pose_label;  // nullptr: 3-DoF
+    const float* pose_obs_total;
+    int32_t num_poses;
+    // mesh
+    const float4* mverts;
+    const uint32_t* mtris;
+    const Meshlet* meshlets;
+    const int32_t* model_ml_lo;
+    const int32_t* model_ml_hi;
+    int32_t num_models;
+    // camera
+    float p00, p01, p02, p03, p10, p11, p12, p13;  // rows 0 and 1 of proj
+    int32_t width, height, stride, ws, hs;
+    float cx, cy, fx, fy, depth_factor;
+    // observation (sampled source depth / mask at the stride grid)
+    const int32_t* src_s;
+    const uint8_t* lab_s;  // nullptr when 3-DoF
+    const LabelGrid* grids;
+    const int32_t* cell_start;
+    const float4* grid_pts;
+    int32_t num_grids;  // labels; the 3-DoF grid is grids[num_grids]
+    int32_t bitmap_words;
+    // cost
+    float r2;
+    float occlusion_threshold;
+    int32_t calc_obs;
+    float* out_rc;
+    float* out_oc;
+    float* out_diff;
+    int32_t* dbg_zs;
+};
+
+// launchers (pcore_kernels.hip)
+hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
+size_t fused_lds_bytes(int ws, int hs, int bitmap_words);
+hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
+                              const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
+                              const float* proj, int32_t* depth, hipStream_t s);
+hipError_t launch_render_finalize(int32_t* depth, const int32_t* src_depth, const uint8_t* src_mask,
+                                  const int32_t* pose_label, int num_poses, int width, int height,
+                                  float occlusion_threshold, hipStream_t s);
+hipError_t launch_fill_i32(int32_t* p, int32_t v, size_t n, hipStream_t s);
+hipError_t launch_cloud_count(const int32_t* depth, int num_poses, int width, int height, int stride,
+                              const uint8_t* label_mask, int32_t* counts, hipStream_t s);
+hipError_t launch_exclusive_scan(const int32_t* in, int32_t* out, int n, int32_t* total, hipStream_t s);
+hipError_t launch_cloud_write(const int32_t* depth, int num_poses, int width, int height, int stride, float cx,
+                              float cy, float fx, float fy, float depth_factor, const uint8_t* label_mask,
+                              const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose,
+                              int32_t* label, int cap, hipStream_t s);
+hipError_t launch_sample_source(const int32_t* src_depth, const uint8_t* src_mask, int width, int height,
+                                int stride, int32_t* src_s, uint8_t* lab_s, hipStream_t s);
+hipError_t launch_select(const float* rc, const float* oc, const int32_t* pose_model, int num_poses,
+                         int64_t index_base, int num_models, int64_t* keys, hipStream_t s);
+
+}  // namespace pcore

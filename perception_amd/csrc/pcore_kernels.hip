@@ -1,0 +1,767 @@
+// pcore_kernels.hip -- CDNA4 (gfx950) kernels of the render-and-compare hot path.
+//
+// Float semantics: every kernel here is compiled with -ffp-contract=off (plus the pragma below), IEEE
+// f32 division and no fast-math, so each expression is evaluated in the explicit order of the
+// reference CUDA code it restates (file:line cited per function).  Integer z-buffers are therefore
+// bit-identical to the CPU oracle (oracle/pcore_oracle.cpp), which follows the same order.
+//
+// Kernels
+//   fused_cost_kernel      stage COST: one workgroup per candidate pose; z-buffer of the stride-sampled
+//                          pixels kept in LDS, meshlet vertex transform, per-wave compaction of the
+//                          (triangle, sample) work, source occlusion, unprojection, fixed-radius 1-NN and
+//                          the three per-pose costs.  No per-pose HBM traffic except 64 B of pose in and
+//                          12 B of costs out.
+//   render_full_kernel     stage RENDER (parity): full-resolution z-buffer in HBM via atomicMin.
+//   render_finalize_kernel source occlusion + INT_MAX -> 0 on the full z-buffer.
+//   cloud_count / cloud_write  stage CLOUD and depth2cloud_global: stride mask, ordered compaction, unprojection.
+//   select_kernel          host selection of the reference (int cost, filter, per-model argmin key).
+#include "pcore_internal.h"
+
+#include <climits>
+#include <cfloat>
+
+#pragma clang fp contract(off)
+
+namespace pcore {
+
+constexpr int kWave = 64;
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kRecCap = 128;  // per-wave ring of queued triangle records
+constexpr int64_t PCORE_KEY_NONE_DEV = 0x7fffffffffffffffLL;
+constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queued; larger ones are
+                              // processed cooperatively by the whole wave
+
+// ------------------------------------------------------------------------------------------------
+// Exact-semantics helpers (shared by every kernel)
+// ------------------------------------------------------------------------------------------------
+
+// NVIDIA cvt.rzi.s32.f32 semantics of `int32_t(float)` (image_renderer.cuh:129): NaN -> 0, saturate.
+__device__ __forceinline__ int32_t cvt_i32_gpu(float f) {
+    if (!(f == f)) return 0;
+    if (f >= 2147483648.0f) return INT_MAX;
+    if (f <= -2147483648.0f) return INT_MIN;
+    return (int32_t)f;
+}
+
+// x86 cvttss2si semantics of the host `(int) float` casts (search_env.cpp:2022-2048).
+__device__ __forceinline__ int32_t cvt_i32_x86(float f) {
+    if (!(f == f) || f >= 2147483648.0f || f < -2147483648.0f) return INT_MIN;
+    return (int32_t)f;
+}
+
+// CUDA abs() of a wrapped int32 difference (image_renderer.cuh:163-165).
+__device__ __forceinline__ int32_t iabs_wrap(int32_t a, int32_t b) {
+    int32_t d = (int32_t)((uint32_t)a - (uint32_t)b);
+    return d < 0 ? (int32_t)(0u - (uint32_t)d) : d;
+}
+
+__device__ __forceinline__ float ref_max(float a, float b) { return (a > b) ? a : b; }  // image_renderer.cuh:14-15
+__device__ __forceinline__ float ref_min(float a, float b) { return (a < b) ? a : b; }  // image_renderer.cuh:17-18
+
+// mat_mul_v row (image_renderer.cuh:20-27): ((m0*x + m1*y) + m2*z) + m3
+__device__ __forceinline__ float row4(float m0, float m1, float m2, float m3, float x, float y, float z) {
+    return m0 * x + m1 * y + m2 * z + m3;
+}
+
+// Source-occlusion rule applied to the per-pixel minimum fragment depth.  Equals the reference's
+// serial z-test + black-out sequence (image_renderer.cuh:146-196) for every fragment order because the
+// black-out predicate is monotone in the stored depth ("Deterministic raster contract").
+__device__ __forceinline__ int32_t occlusion_rule(int32_t z, int32_t src, int lab, bool use_seg, int32_t pl,
+                                                  float occlusion_threshold) {
+    if (z == INT_MAX) return 0;  // no fragment: max2zero (image_renderer.cuh:465-466)
+    bool cond;
+    if (use_seg) cond = (pl != lab - 1) && ((float)iabs_wrap(z, src) > 0.5f);
+    else cond = (float)iabs_wrap(z, src) > occlusion_threshold;
+    if (cond && z > src && src > 0) return 0;  // blacked out -> INT_MAX -> max2zero
+    return z;
+}
+
+// Reference bounding box (image_renderer.cuh:86-107) with its exact NaN behaviour.
+__device__ __forceinline__ void bbox_ref(const float (&p)[3][2], float cmax0, float cmax1, float (&bmin)[2],
+                                         float (&bmax)[2]) {
+    bmin[0] = FLT_MAX; bmin[1] = FLT_MAX;
+    bmax[0] = -FLT_MAX; bmax[1] = -FLT_MAX;
+    const float cmax[2] = {cmax0, cmax1};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            bmin[j] = ref_max(0.0f, ref_min(bmin[j], p[i][j]));
+            bmax[j] = ref_min(cmax[j], ref_max(bmax[j], p[i][j]));
+        }
+}
+
+// Loop bounds of `for (P = size_t(bmin + 0.5f); P <= bmax; ++P)` (image_renderer.cuh:110-111) with
+// NVIDIA float->u64 conversion (NaN/negative -> 0, saturating).  Returns false if the loop is empty.
+__device__ __forceinline__ bool loop_bounds(float bmin, float bmax, int& lo, int& hi) {
+    if (!(bmax >= 0.0f)) return false;  // NaN or negative upper bound: P (>= 0) <= bmax never holds
+    const float st = bmin + 0.5f;
+    int start;
+    if (!(st > 0.0f)) start = 0;
+    else if (st >= 1.0e9f) return false;  // bmax <= width-1, so a start this large never iterates
+    else start = (int)st;
+    hi = (int)floorf(bmax);
+    lo = start;
+    return lo <= hi;
+}
+
+// One fragment test at raster pixel (P0, P1) (image_renderer.cuh:44-57, 112-129).  Returns true and the
+// int depth if the pixel is inside the triangle (NaN barycentrics count as inside, as in the reference).
+__device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1, float C0, float C1, float z0,
+                                         float z1, float z2, float P0, float P1, int32_t& depth) {
+    const float area = 0.5f * ((C0 - A0) * (B1 - A1) - (B0 - A0) * (C1 - A1));
+    const float base_inv = 1.0f / area;
+    const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
+    const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
+    const float alpha = 1.0f - beta - gamma;
+    if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
+    const float ox = alpha / z0, oy = beta / z1, oz = gamma / z2;
+    const float frag = (alpha + beta + gamma) / (ox + oy + oz);
+    depth = cvt_i32_gpu(frag + 0.5f);
+    return true;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
+
+__device__ __forceinline__ int mbcnt64(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage COST: fused sampled render + unproject + 1-NN + cost
+// ------------------------------------------------------------------------------------------------
+
+struct TriRec {  // 40 bytes: screen-space vertices, camera z, sample window
+    float a0, a1, b0, b1, c0, c1, z0, z1, z2;
+    uint32_t meta;  // kx0 | ky0 << 12 | (nx-1) << 24 | (ny-1) << 28   (nx, ny <= kSmallK... or 16)
+};
+
+template <int STRIDE>
+__device__ __forceinline__ int sdiv(int v, int s) {
+    if constexpr (STRIDE > 0) return v / STRIDE;
+    else return v / s;
+}
+
+// Sample window of a triangle with exact reference bbox (bmin, bmax): kx in [kx0, kx0+nx),
+// ky in [ky0, ky0+ny) where the sampled output pixel is (kx*s, ky*s) and raster row P1 = H-1-ky*s.
+template <int STRIDE>
+__device__ __forceinline__ int sample_window(const float (&bmin)[2], const float (&bmax)[2], int s, int H, int& kx0,
+                                             int& ky0, int& nx, int& ny) {
+    int lo0, hi0, lo1, hi1;
+    if (!loop_bounds(bmin[0], bmax[0], lo0, hi0)) return 0;
+    if (!loop_bounds(bmin[1], bmax[1], lo1, hi1)) return 0;
+    const int ss = STRIDE > 0 ? STRIDE : s;
+    kx0 = sdiv<STRIDE>(lo0 + ss - 1, s);
+    const int kx1 = sdiv<STRIDE>(hi0, s);
+    // output rows y = H-1-P1 for P1 in [lo1, hi1]
+    ky0 = sdiv<STRIDE>(H - 1 - hi1 + ss - 1, s);
+    const int ky1 = sdiv<STRIDE>(H - 1 - lo1, s);
+    nx = kx1 - kx0 + 1;
+    ny = ky1 - ky0 + 1;
+    if (nx <= 0 || ny <= 0) return 0;
+    return nx * ny;
+}
+
+struct FusedSmem {
+    int32_t* zbuf;  // hs * ws
+    float* vx;      // kWaves * 64
+    float* vy;
+    float* vz;
+    TriRec* ring;   // kWaves * kRecCap (phase 1); reused as int32 point queues in phase 2
+    uint32_t* bitmap;
+    int32_t* counters;  // [0] bad, [1] explained, [2] points
+};
+
+__device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, int s, int H, int ws, int32_t* zbuf) {
+    const float P0 = (float)(kx * s);
+    const float P1 = (float)(H - 1 - ky * s);
+    int32_t d;
+    if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d))
+        atomicMin(&zbuf[ky * ws + kx], d);
+}
+
+size_t fused_lds_bytes(int ws, int hs, int bitmap_words) {
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    size_t b = al((size_t)ws * hs * 4);
+    b += al((size_t)kWaves * kWave * 4) * 3;
+    b += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+    b += al((size_t)bitmap_words * 4);
+    b += 16;
+    return b;
+}
+
+template <int STRIDE>
+__global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int pose = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    const int s = STRIDE > 0 ? STRIDE : a.stride;
+    const int W = a.width, H = a.height, ws = a.ws, hs = a.hs;
+    const int nsamp = ws * hs;
+
+    FusedSmem sm;
+    {
+        auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+        unsigned char* p = smem_raw;
+        sm.zbuf = (int32_t*)p; p += al((size_t)nsamp * 4);
+        sm.vx = (float*)p; p += al((size_t)kWaves * kWave * 4);
+        sm.vy = (float*)p; p += al((size_t)kWaves * kWave * 4);
+        sm.vz = (float*)p; p += al((size_t)kWaves * kWave * 4);
+        sm.ring = (TriRec*)p; p += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+        sm.bitmap = (uint32_t*)p; p += al((size_t)a.bitmap_words * 4);
+        sm.counters = (int32_t*)p;
+    }
+    for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
+    for (int i = tid; i < a.bitmap_words; i += kThreads) sm.bitmap[i] = 0u;
+    if (tid < 4) sm.counters[tid] = 0;
+
+    // pose (wave-uniform -> scalar loads)
+    const float* P = a.poses + (size_t)16 * pose;
+    const float m00 = P[0], m01 = P[1], m02 = P[2], m03 = P[3];
+    const float m10 = P[4], m11 = P[5], m12 = P[6], m13 = P[7];
+    const float m20 = P[8], m21 = P[9], m22 = P[10], m23 = P[11];
+    const int model = a.pose_model[pose];
+    const bool use_seg = a.pose_label != nullptr;
+    const int32_t pl = use_seg ? a.pose_label[pose] : 0;
+    __syncthreads();
+
+    // ---------------- phase 1: raster of the sampled pixels ----------------
+    const float Wf = (float)W, Hf = (float)H;
+    const float cmax0 = (float)(W - 1), cmax1 = (float)(H - 1);
+    float* vx = sm.vx + wave * kWave;
+    float* vy = sm.vy + wave * kWave;
+    float* vz = sm.vz + wave * kWave;
+    TriRec* ring = sm.ring + wave * kRecCap;
+    int rec_count = 0;  // wave-uniform
+
+    auto flush = [&](int count) {
+        wave_sync();
+        for (int base = 0; base < count; base += kWave) {
+            const int j = base + lane;
+            if (j < count) {
+                const TriRec r = ring[j];
+                const int kx0 = r.meta & 0xfff, ky0 = (r.meta >> 12) & 0xfff;
+                const int nx = ((r.meta >> 24) & 0xf) + 1, ny = ((r.meta >> 28) & 0xf) + 1;
+                for (int iy = 0; iy < ny; iy++)
+                    for (int ix = 0; ix < nx; ix++) raster_sample(r, kx0 + ix, ky0 + iy, s, H, ws, sm.zbuf);
+            }
+        }
+        wave_sync();
+    };
+
+    if (model >= 0 && model < a.num_models) {
+        const int ml_lo = a.model_ml_lo[model], ml_hi = a.model_ml_hi[model];
+        for (int m = ml_lo + wave; m < ml_hi; m += kWaves) {
+            const Meshlet ml = a.meshlets[m];
+            // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
+            // (image_renderer.cuh:296-305, 82-84)
+            bool bad_vertex = false;
+            if (lane < ml.nv) {
+                const float4 v = a.mverts[ml.vbase + lane];
+                const float lx = row4(m00, m01, m02, m03, v.x, v.y, v.z);
+                const float ly = row4(m10, m11, m12, m13, v.x, v.y, v.z);
+                const float lz = row4(m20, m21, m22, m23, v.x, v.y, v.z);
+                const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
+                const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
+                const float sx = px / lz * Wf / 2.0f + Wf / 2.0f;
+                const float sy = py / lz * Hf / 2.0f + Hf / 2.0f;
+                vx[lane] = sx;
+                vy[lane] = sy;
+                vz[lane] = lz;
+                bad_vertex = !(sx == sx) || !(sy == sy);
+            }
+            const uint64_t nanmask = __ballot(bad_vertex);
+            wave_sync();
+            for (int t0 = 0; t0 < ml.nt; t0 += kWave) {
+                const int t = t0 + lane;
+                int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
+                TriRec r;
+                if (t < ml.nt) {
+                    const uint32_t pk = a.mtris[ml.tbase + t];
+                    const int i0 = pk & 0xff, i1 = (pk >> 8) & 0xff, i2 = (pk >> 16) & 0xff;
+                    r.a0 = vx[i0]; r.a1 = vy[i0];
+                    r.b0 = vx[i1]; r.b1 = vy[i1];
+                    r.c0 = vx[i2]; r.c1 = vy[i2];
+                    float bmin[2], bmax[2];
+                    const bool nan_tri = nanmask != 0 && (((nanmask >> i0) | (nanmask >> i1) | (nanmask >> i2)) & 1ull);
+                    if (!nan_tri) {
+                        // finite (or +-inf) coordinates: min/max form equals the reference's iterative clamp
+                        bmin[0] = fmaxf(0.0f, fminf(fminf(r.a0, r.b0), r.c0));
+                        bmin[1] = fmaxf(0.0f, fminf(fminf(r.a1, r.b1), r.c1));
+                        bmax[0] = fminf(cmax0, fmaxf(fmaxf(r.a0, r.b0), r.c0));
+                        bmax[1] = fminf(cmax1, fmaxf(fmaxf(r.a1, r.b1), r.c1));
+                    } else {
+                        const float p[3][2] = {{r.a0, r.a1}, {r.b0, r.b1}, {r.c0, r.c1}};
+                        bbox_ref(p, cmax0, cmax1, bmin, bmax);
+                    }
+                    nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
+                    if (nk > 0) {
+                        r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
+                    }
+                }
+                // large triangles: whole-wave cooperative
+                uint64_t big = __ballot(nk > kSmallK);
+                while (big) {
+                    const int j = __ffsll((unsigned long long)big) - 1;
+                    big &= big - 1;
+                    TriRec rb;
+                    rb.a0 = __shfl(r.a0, j); rb.a1 = __shfl(r.a1, j);
+                    rb.b0 = __shfl(r.b0, j); rb.b1 = __shfl(r.b1, j);
+                    rb.c0 = __shfl(r.c0, j); rb.c1 = __shfl(r.c1, j);
+                    rb.z0 = __shfl(r.z0, j); rb.z1 = __shfl(r.z1, j); rb.z2 = __shfl(r.z2, j);
+                    const int bkx0 = __shfl(kx0, j), bky0 = __shfl(ky0, j), bnx = __shfl(nx, j), bnk = __shfl(nk, j);
+                    for (int q = lane; q < bnk; q += kWave) {
+                        const int iy = q / bnx, ix = q - iy * bnx;
+                        raster_sample(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf);
+                    }
+                }
+                // small triangles: queue into the wave's ring
+                const bool qd = nk > 0 && nk <= kSmallK;
+                const uint64_t bq = __ballot(qd);
+                if (qd) {
+                    r.meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) | ((uint32_t)(ny - 1) << 28);
+                    ring[rec_count + mbcnt64(bq)] = r;
+                }
+                rec_count += __popcll(bq);
+                if (rec_count > kRecCap - kWave) {
+                    flush(rec_count);
+                    rec_count = 0;
+                }
+            }
+            wave_sync();  // vertex slots are rewritten by the next meshlet
+        }
+        if (rec_count > 0) flush(rec_count);
+    }
+    __syncthreads();
+
+    // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
+    int32_t* queue = reinterpret_cast<int32_t*>(sm.ring) + wave * (kRecCap * (int)sizeof(TriRec) / 4);
+    int qcount = 0;
+    const int grid_id = use_seg ? pl : a.num_grids;
+    const bool grid_ok = use_seg ? (pl >= 0 && pl < a.num_grids) : true;
+    LabelGrid g;
+    if (grid_ok) g = a.grids[grid_id];
+    const float r_eff = sqrtf(a.r2) * 1.0001f + 1e-7f;
+    int my_bad = 0;
+
+    auto process_points = [&](int count) {
+        wave_sync();
+        for (int base = 0; base < count; base += kWave) {
+            const int j = base + lane;
+            bool is_bad = false;
+            if (j < count) {
+                const int k = queue[j];
+                const int32_t Z = sm.zbuf[k];
+                const int ky = k / ws, kx = k - ky * ws;
+                // compute_point_clouds.cuh:14-22 with depth_factor (cm -> m)
+                const float zp = (float)Z / a.depth_factor;
+                const float xp = ((float)(kx * s) - a.cx) / a.fx * zp;
+                const float yp = ((float)(ky * s) - a.cy) / a.fy * zp;
+                float best = INFINITY;
+                int bidx = 0x7fffffff;
+                if (grid_ok) {
+                    const float rc = r_eff * g.inv_c;
+                    const float fx0 = (xp - g.ox) * g.inv_c, fy0 = (yp - g.oy) * g.inv_c, fz0 = (zp - g.oz) * g.inv_c;
+                    const float lx = fx0 - rc, hx = fx0 + rc, ly = fy0 - rc, hy = fy0 + rc, lz = fz0 - rc, hz = fz0 + rc;
+                    if (hx >= 0.0f && lx < (float)g.nx && hy >= 0.0f && ly < (float)g.ny && hz >= 0.0f && lz < (float)g.nz) {
+                        const int ix0 = (int)floorf(fmaxf(lx, 0.0f)), ix1 = min(g.nx - 1, (int)floorf(hx));
+                        const int iy0 = (int)floorf(fmaxf(ly, 0.0f)), iy1 = min(g.ny - 1, (int)floorf(hy));
+                        const int iz0 = (int)floorf(fmaxf(lz, 0.0f)), iz1 = min(g.nz - 1, (int)floorf(hz));
+                        for (int iz = iz0; iz <= iz1; iz++)
+                            for (int iy = iy0; iy <= iy1; iy++)
+                                for (int ix = ix0; ix <= ix1; ix++) {
+                                    const int c = g.cell_base + (iz * g.ny + iy) * g.nx + ix;
+                                    const int pe = a.cell_start[c + 1];
+                                    for (int pi = a.cell_start[c]; pi < pe; pi++) {
+                                        const float4 o = a.grid_pts[pi];
+                                        const float dx = xp - o.x, dy = yp - o.y, dz = zp - o.z;
+                                        const float d = dx * dx + dy * dy + dz * dz;
+                                        const int oi = __float_as_int(o.w);
+                                        if (d < best || (d == best && oi < bidx)) { best = d; bidx = oi; }
+                                    }
+                                }
+                    }
+                }
+                // compute_costs.cuh:201-270 (cost types 0 / 2: explained marking only)
+                if (best > a.r2) is_bad = true;
+                else if (bidx != 0x7fffffff) atomicOr(&sm.bitmap[bidx >> 5], 1u << (bidx & 31));
+            }
+            my_bad += is_bad ? 1 : 0;
+        }
+        wave_sync();
+    };
+
+    for (int base = wave * kWave; base < nsamp; base += kThreads) {
+        const int k = base + lane;
+        bool valid = false;
+        if (k < nsamp) {
+            const int32_t z = sm.zbuf[k];
+            const int32_t zf = occlusion_rule(z, a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg, pl,
+                                              a.occlusion_threshold);
+            if (zf != z) sm.zbuf[k] = zf;
+            if (a.dbg_zs) a.dbg_zs[(size_t)pose * nsamp + k] = zf;
+            valid = zf > 0;  // depth_to_mask, compute_point_clouds.cuh:64
+        }
+        const uint64_t bv = __ballot(valid);
+        if (valid) queue[qcount + mbcnt64(bv)] = k;
+        qcount += __popcll(bv);
+        if (qcount >= kWave) {
+            process_points(qcount);
+            qcount = 0;
+        }
+    }
+    if (qcount > 0) process_points(qcount);
+    // per-wave totals
+    int wave_bad = my_bad;
+    for (int off = 32; off > 0; off >>= 1) wave_bad += __shfl_xor(wave_bad, off);
+    __syncthreads();  // all points counted / marked
+    if (lane == 0) atomicAdd(&sm.counters[0], wave_bad);
+    // number of points = number of valid samples, counted again cheaply from the final z-buffer
+    int my_pts = 0, my_expl = 0;
+    for (int k = tid; k < nsamp; k += kThreads) my_pts += sm.zbuf[k] > 0 ? 1 : 0;
+    for (int w = tid; w < a.bitmap_words; w += kThreads) my_expl += __popc(sm.bitmap[w]);
+    for (int off = 32; off > 0; off >>= 1) {
+        my_pts += __shfl_xor(my_pts, off);
+        my_expl += __shfl_xor(my_expl, off);
+    }
+    if (lane == 0) {
+        atomicAdd(&sm.counters[1], my_expl);
+        atomicAdd(&sm.counters[2], my_pts);
+    }
+    __syncthreads();
+
+    // ---------------- phase 3: costs (compute_costs.cuh:362-446), exact float order ----------------
+    if (tid == 0) {
+        const float num = (float)sm.counters[2];
+        const float badf = (float)sm.counters[0];
+        const float rendered_explained = num - badf;
+        float rc = (num == 0.0f) ? -1.0f : badf / num;
+        rc = (rc == -1.0f) ? -1.0f : rc * 100.0f;
+        a.out_rc[pose] = rc;
+        if (a.calc_obs) {
+            const float expl = (float)sm.counters[1];
+            const float tot = a.pose_obs_total[pose];
+            a.out_diff[pose] = rendered_explained - expl;
+            float oc = tot - expl;
+            oc = oc / tot;
+            a.out_oc[pose] = oc * 100.0f;
+        } else {
+            if (a.out_oc) a.out_oc[pose] = 0.0f;
+            if (a.out_diff) a.out_diff[pose] = 0.0f;
+        }
+    }
+}
+
+hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s) {
+    const size_t lds = fused_lds_bytes(a.ws, a.hs, a.bitmap_words);
+    if (a.num_poses <= 0) return hipSuccess;
+    if (a.stride == 8)
+        hipLaunchKernelGGL(fused_cost_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL(fused_cost_kernel<0>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage RENDER (parity): full-resolution z-buffer
+// ------------------------------------------------------------------------------------------------
+
+// One thread per (triangle, pose), as render_triangle_multi (image_renderer.cuh:212-321); the per-pixel
+// spin-lock is replaced by atomicMin and the black-out by render_finalize_kernel.
+__global__ void __launch_bounds__(256) render_full_kernel(const float* tris, int num_tris, const int32_t* tri_lo,
+                                                          const int32_t* tri_hi, const float* poses,
+                                                          const int32_t* pose_model, int width, int height,
+                                                          const float* proj, int32_t* depth) {
+    const int pose = blockIdx.y;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tris) return;
+    const int m = pose_model[pose];
+    if (!(t >= tri_lo[m] && t < tri_hi[m])) return;
+    const float* M = poses + (size_t)16 * pose;
+    const float* tp = tris + (size_t)9 * t;
+    const float Wf = (float)width, Hf = (float)height;
+    float p[3][2], z[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float x = tp[3 * k], y = tp[3 * k + 1], zz = tp[3 * k + 2];
+        const float lx = row4(M[0], M[1], M[2], M[3], x, y, zz);
+        const float ly = row4(M[4], M[5], M[6], M[7], x, y, zz);
+        const float lz = row4(M[8], M[9], M[10], M[11], x, y, zz);
+        const float px = row4(proj[0], proj[1], proj[2], proj[3], lx, ly, lz);
+        const float py = row4(proj[4], proj[5], proj[6], proj[7], lx, ly, lz);
+        p[k][0] = px / lz * Wf / 2.0f + Wf / 2.0f;
+        p[k][1] = py / lz * Hf / 2.0f + Hf / 2.0f;
+        z[k] = lz;
+    }
+    float bmin[2], bmax[2];
+    bbox_ref(p, (float)(width - 1), (float)(height - 1), bmin, bmax);
+    int lo0, hi0, lo1, hi1;
+    if (!loop_bounds(bmin[0], bmax[0], lo0, hi0) || !loop_bounds(bmin[1], bmax[1], lo1, hi1)) return;
+    int32_t* img = depth + (size_t)pose * width * height;
+    for (int P1 = lo1; P1 <= hi1; P1++)
+        for (int P0 = lo0; P0 <= hi0; P0++) {
+            int32_t d;
+            if (fragment(p[0][0], p[0][1], p[1][0], p[1][1], p[2][0], p[2][1], z[0], z[1], z[2], (float)P0, (float)P1, d))
+                atomicMin(&img[P0 + (size_t)(height - 1 - P1) * width], d);
+        }
+}
+
+__global__ void render_finalize_kernel(int32_t* depth, const int32_t* src_depth, const uint8_t* src_mask,
+                                       const int32_t* pose_label, int width, int height, float occlusion_threshold) {
+    const int pose = blockIdx.y;
+    const size_t npx = (size_t)width * height;
+    const bool use_seg = pose_label != nullptr;
+    const int32_t pl = use_seg ? pose_label[pose] : 0;
+    int32_t* img = depth + npx * pose;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x)
+        img[i] = occlusion_rule(img[i], src_depth[i], use_seg ? (int)src_mask[i] : 0, use_seg, pl, occlusion_threshold);
+}
+
+__global__ void fill_i32_kernel(int32_t* p, int32_t v, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+hipError_t launch_fill_i32(int32_t* p, int32_t v, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, v, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
+                              const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
+                              const float* proj, int32_t* depth, hipStream_t s) {
+    if (num_poses <= 0 || num_tris <= 0) return hipSuccess;
+    dim3 grid((num_tris + 255) / 256, num_poses);
+    hipLaunchKernelGGL(render_full_kernel, grid, dim3(256), 0, s, tris, num_tris, tri_lo, tri_hi, poses, pose_model,
+                       width, height, proj, depth);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_finalize(int32_t* depth, const int32_t* src_depth, const uint8_t* src_mask,
+                                  const int32_t* pose_label, int num_poses, int width, int height,
+                                  float occlusion_threshold, hipStream_t s) {
+    if (num_poses <= 0) return hipSuccess;
+    const size_t npx = (size_t)width * height;
+    unsigned bx = (unsigned)((npx + 255) / 256);
+    if (bx > 256) bx = 256;
+    hipLaunchKernelGGL(render_finalize_kernel, dim3(bx, num_poses), dim3(256), 0, s, depth, src_depth, src_mask,
+                       pose_label, width, height, occlusion_threshold);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stage CLOUD / depth2cloud_global (compute_point_clouds.cuh:37-184, 265-346)
+// ------------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ bool cloud_valid(const int32_t* depth, const uint8_t* label_mask, size_t idx) {
+    if (depth[idx] <= 0) return false;                                 // :64, :123
+    if (label_mask != nullptr && label_mask[idx] <= 0) return false;  // :74, :127
+    return true;
+}
+
+// one block per image: number of valid stride samples
+__global__ void cloud_count_kernel(const int32_t* depth, int width, int height, int stride, const uint8_t* label_mask,
+                                   int32_t* counts) {
+    const int n = blockIdx.x;
+    const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
+    const size_t npx = (size_t)width * height;
+    int c = 0;
+    for (int k = threadIdx.x; k < ws * hs; k += blockDim.x) {
+        const int ky = k / ws, kx = k - ky * ws;
+        c += cloud_valid(depth, label_mask, npx * n + (size_t)(kx * stride) + (size_t)(ky * stride) * width) ? 1 : 0;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    __shared__ int part[16];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += part[w];
+        counts[n] = t;
+    }
+}
+
+// single-block exclusive scan (n up to millions: chunked)
+__global__ void exclusive_scan_kernel(const int32_t* in, int32_t* out, int n, int32_t* total) {
+    __shared__ int wsum[16];
+    __shared__ int carry_s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? in[i] : 0;
+        int incl = v;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        int woff = 0;
+        for (int w = 0; w < wave; w++) woff += wsum[w];
+        int chunk_total = 0;
+        for (int w = 0; w < nw; w++) chunk_total += wsum[w];
+        const int carry = carry_s;
+        if (i < n) out[i] = carry + woff + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 0) carry_s = carry + chunk_total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry_s;
+}
+
+__global__ void cloud_write_kernel(const int32_t* depth, int width, int height, int stride, float cx, float cy,
+                                   float fx, float fy, float depth_factor, const uint8_t* label_mask,
+                                   const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose_out,
+                                   int32_t* label_out, int cap) {
+    __shared__ int wsum[16];
+    __shared__ int carry_s;
+    const int n = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
+    const size_t npx = (size_t)width * height;
+    if (threadIdx.x == 0) carry_s = offsets[n];
+    __syncthreads();
+    for (int base = 0; base < ws * hs; base += blockDim.x) {
+        const int k = base + threadIdx.x;
+        bool v = false;
+        int kx = 0, ky = 0;
+        size_t idx = 0;
+        if (k < ws * hs) {
+            ky = k / ws; kx = k - ky * ws;
+            idx = npx * n + (size_t)(kx * stride) + (size_t)(ky * stride) * width;
+            v = cloud_valid(depth, label_mask, idx);
+        }
+        const uint64_t b = __ballot(v);
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int woff = 0, tot = 0;
+        for (int w = 0; w < nw; w++) {
+            if (w < wave) woff += wsum[w];
+            tot += wsum[w];
+        }
+        const int carry = carry_s;
+        if (v) {
+            const int o = carry + woff + mbcnt64(b);
+            if (o < cap) {
+                const int32_t d = depth[idx];
+                const float zp = (float)d / depth_factor;
+                const float xp = ((float)(kx * stride) - cx) / fx * zp;
+                const float yp = ((float)(ky * stride) - cy) / fy * zp;
+                xyz[3 * (size_t)o + 0] = xp;
+                xyz[3 * (size_t)o + 1] = yp;
+                xyz[3 * (size_t)o + 2] = zp;
+                if (pose_out) pose_out[o] = n;
+                if (label_out) {
+                    if (label_mask) label_out[o] = (int32_t)label_mask[idx] - 1;
+                    else if (pose_label) label_out[o] = pose_label[n];
+                    else label_out[o] = 0;
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) carry_s = carry + tot;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_cloud_count(const int32_t* depth, int num_poses, int width, int height, int stride,
+                              const uint8_t* label_mask, int32_t* counts, hipStream_t s) {
+    if (num_poses <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cloud_count_kernel, dim3(num_poses), dim3(256), 0, s, depth, width, height, stride, label_mask,
+                       counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_exclusive_scan(const int32_t* in, int32_t* out, int n, int32_t* total, hipStream_t s) {
+    hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, s, in, out, n, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_cloud_write(const int32_t* depth, int num_poses, int width, int height, int stride, float cx,
+                              float cy, float fx, float fy, float depth_factor, const uint8_t* label_mask,
+                              const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose,
+                              int32_t* label, int cap, hipStream_t s) {
+    if (num_poses <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cloud_write_kernel, dim3(num_poses), dim3(256), 0, s, depth, width, height, stride, cx, cy, fx,
+                       fy, depth_factor, label_mask, pose_label, offsets, xyz, pose, label, cap);
+    return hipGetLastError();
+}
+
+// sampled copy of the source depth / mask at the stride grid (used by the fused kernel)
+__global__ void sample_source_kernel(const int32_t* src_depth, const uint8_t* src_mask, int width, int height,
+                                     int stride, int32_t* src_s, uint8_t* lab_s) {
+    const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ws * hs; k += gridDim.x * blockDim.x) {
+        const int ky = k / ws, kx = k - ky * ws;
+        const size_t idx = (size_t)(kx * stride) + (size_t)(ky * stride) * width;
+        src_s[k] = src_depth[idx];
+        if (lab_s) lab_s[k] = src_mask ? src_mask[idx] : 0;
+    }
+}
+
+hipError_t launch_sample_source(const int32_t* src_depth, const uint8_t* src_mask, int width, int height, int stride,
+                                int32_t* src_s, uint8_t* lab_s, hipStream_t s) {
+    hipLaunchKernelGGL(sample_source_kernel, dim3(64), dim3(256), 0, s, src_depth, src_mask, width, height, stride,
+                       src_s, lab_s);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Selection (search_env.cpp:1987-2051, 2542-2583) as per-model int64 argmin keys
+// ------------------------------------------------------------------------------------------------
+
+__global__ void select_kernel(const float* rc, const float* oc, const int32_t* pose_model, int num_poses,
+                              int64_t index_base, int num_models, int64_t* keys) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t key = PCORE_KEY_NONE_DEV;
+    int m = -1;
+    if (i < num_poses) {
+        m = pose_model[i];
+        const int32_t target = cvt_i32_x86(rc[i]);
+        const int32_t source = cvt_i32_x86(oc[i]);
+        const int32_t cost = (target < 0) ? -1 : cvt_i32_x86(rc[i] + oc[i]);
+        const int32_t adiff = iabs_wrap(target, source);
+        const bool ok = !(cost == -1 || cost == -2) && adiff < 30 && cost != INT_MAX && m >= 0 && m < num_models;
+        if (ok) {
+            const uint64_t hi = (uint64_t)((uint32_t)cost ^ 0x80000000u);
+            key = (int64_t)((hi << 31) | ((uint64_t)(index_base + i) & 0x7fffffffull));
+        }
+    }
+    // wave-level minimum when the wave's poses share one model (the common case)
+    const int m0 = __shfl(m, 0);
+    const bool uniform = __all(m == m0 || m < 0);
+    if (uniform) {
+        int64_t k = key;
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t o = __shfl_xor(k, off);
+            k = o < k ? o : k;
+        }
+        if ((threadIdx.x & 63) == 0 && k != PCORE_KEY_NONE_DEV && m0 >= 0 && m0 < num_models)
+            atomicMin((unsigned long long*)&keys[m0], (unsigned long long)k);
+    } else if (key != PCORE_KEY_NONE_DEV) {
+        atomicMin((unsigned long long*)&keys[m], (unsigned long long)key);
+    }
+}
+
+hipError_t launch_select(const float* rc, const float* oc, const int32_t* pose_model, int num_poses,
+                         int64_t index_base, int num_models, int64_t* keys, hipStream_t s) {
+    if (num_poses <= 0) return hipSuccess;
+    hipLaunchKernelGGL(select_kernel, dim3((num_poses + 255) / 256), dim3(256), 0, s, rc, oc, pose_model, num_poses,
+                       index_base, num_models, keys);
+    return hipGetLastError();
+}
+
+}  // namespace pcore

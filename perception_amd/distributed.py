@@ -1,0 +1,44 @@
+"""Multi-GPU pose sharding and the argmin exchange.
+
+One process per GPU.  The candidate-pose grid is split into contiguous global index ranges, every rank
+scores its shard with no data-path collective, and the per-model selection keys
+key = ((cost ^ 0x80000000) << 31) | global_index (int64, see include/pcore.h) are combined with ONE
+all-reduce(MIN) -- RCCL over xGMI with the "nccl" backend on GPUs, gloo on CPU.  MIN over the keys is
+exactly the reference's strict '<' first-index-wins scan (search_env.cpp:2560-2566).
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [lo, hi) pose range of `rank` (remainder spread over the first ranks)."""
+    base, rem = divmod(total, world)
+    lo = rank * base + min(rank, rem)
+    hi = lo + base + (1 if rank < rem else 0)
+    return lo, hi
+
+
+def init_from_env(backend: str = None):
+    """Initialise torch.distributed from torchrun's env (RANK / WORLD_SIZE / MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1 or dist.is_initialized():
+        return
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend, **kw)
+
+
+def allreduce_min_keys(keys: torch.Tensor) -> torch.Tensor:
+    """In-place MIN all-reduce of the per-model int64 selection keys (no-op on one process)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(keys, op=dist.ReduceOp.MIN)
+    return keys

@@ -1,0 +1,89 @@
+"""Benchmark / smoke workloads (BASELINE.json configs) built on the GPU path.
+
+C2: single YCB mesh (003_cracker_box proxy, 12,288 triangles), 10k 6-DoF candidate poses rendered and
+scored at 640x480, stride 8, no ICP.  The observed scene is the GPU RENDER stage of a GT pose, turned
+into 16-bit depth (depth_factor 10000, N(0, 2 mm) noise), a background plane and a label mask, then
+unprojected with depth2cloud_global on the GPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import synthetic as syn
+from ._native import COST_DEPTH_6DOF
+from .core import PoseCore
+from .model import init_from_eigen_batch
+
+
+@dataclass
+class Workload:
+    core: PoseCore
+    scene: syn.Scene
+    poses: torch.Tensor          # (N, 16) f32
+    pose_model: torch.Tensor     # (N,) i32
+    pose_label: torch.Tensor     # (N,) i32
+    pose_obs_total: torch.Tensor  # (N,) f32
+    obs_xyz: torch.Tensor
+    obs_label: torch.Tensor
+    stride: int
+    index_base: int
+    num_models: int
+    gt_index: Sequence[int]
+
+
+def gpu_render_fn(core: PoseCore, device):
+    def fn(tris, cnt, p16, pm, W, H, proj):
+        poses = torch.from_numpy(np.ascontiguousarray(p16)).to(device)
+        pmt = torch.from_numpy(np.ascontiguousarray(pm, dtype=np.int32)).to(device)
+        return core.render(poses, pmt, None).cpu().numpy()
+    return fn
+
+
+def build(names: Sequence[str] = ("003_cracker_box",), poses_per_model: int = 10000, cam: dict = syn.CAM_640,
+          stride: int = 8, device: int = 0, rank: int = 0, seed: int = syn.SEED, k: int = 32) -> Workload:
+    dev = torch.device("cuda", device)
+    rng = np.random.default_rng(seed)
+    K = len(names)
+    bank = syn.model_bank(names, k)
+    core = PoseCore(device)
+    core.upload_meshes(bank.tris, bank.tris_model_count, bank.colors)
+    from .model import compute_proj
+    proj = compute_proj(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["width"], cam["height"])
+    core.set_camera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"], proj)
+    # empty observation (no source occlusion) to render the GT scene
+    W, H = cam["width"], cam["height"]
+    zero = torch.zeros((H, W), dtype=torch.int32, device=dev)
+    core.set_observation(zero, None, torch.zeros((0, 3), dtype=torch.float32, device=dev), None, 0.01)
+    centers = [(0.03 + 0.12 * (i - (K - 1) / 2), -0.02, 0.80 + 0.05 * i) for i in range(K)]
+    gts = np.stack([syn.default_gt_pose(rng, c) for c in centers])
+    scene = syn.make_scene(list(names), gts, gpu_render_fn(core, dev), cam=cam, rng=rng, k=k)
+    raw = torch.from_numpy(scene.depth_raw).to(dev)
+    mask = torch.from_numpy(scene.mask).to(dev)
+    obs_xyz, obs_label = core.observed_cloud(raw, mask, stride, scene.depth_factor)
+    core.set_observation(torch.from_numpy(scene.src_depth_cm).to(dev), mask, obs_xyz, obs_label, 0.01)
+    seg = np.bincount(obs_label.cpu().numpy(), minlength=K).astype(np.float32)
+    poses, models, gt_index = [], [], []
+    prng = np.random.default_rng(seed + 1 + rank)
+    for obj in range(K):
+        P = syn.candidate_poses(gts[obj][:3, 3], poses_per_model, prng, include=gts[obj])
+        gt_index.append(sum(len(p) for p in poses) + poses_per_model // 3)
+        poses.append(P)
+        models.append(np.full(len(P), obj, np.int32))
+    p16 = init_from_eigen_batch(np.concatenate(poses))
+    pm = np.concatenate(models)
+    n = len(pm)
+    return Workload(core, scene, torch.from_numpy(p16).to(dev), torch.from_numpy(pm).to(dev),
+                    torch.from_numpy(pm.copy()).to(dev), torch.from_numpy(seg[pm]).to(dev), obs_xyz, obs_label,
+                    stride, rank * n, K, gt_index)
+
+
+def step(w: Workload, out, keys):
+    """One pass of the hot path over the batch: render + score every pose, fold the argmin keys."""
+    rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, cost_type=COST_DEPTH_6DOF,
+                                 stride=w.stride, out=out)
+    w.core.select(rc, oc, w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
+    return rc, oc, df

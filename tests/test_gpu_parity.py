@@ -1,0 +1,209 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on the same inputs.
+
+Bar: bit-exact for every integer / index output (z-buffers, clouds' order, argmin) and for the float
+costs (same explicit operation order on both sides, no FMA contraction).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle
+from perception_amd import synthetic as syn
+from perception_amd.core import PoseCore, decode_keys
+from perception_amd.model import init_from_eigen_batch
+from tests.helpers import SceneCase
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    if a.shape != b.shape:
+        return False
+    if a.dtype.kind == "f":
+        return np.array_equal(a.view(np.uint32), b.view(np.uint32)) or np.array_equal(a, b, equal_nan=True)
+    return np.array_equal(a, b)
+
+
+def _setup(case: SceneCase, stride=8):
+    sc = case.scene
+    core = PoseCore(0)
+    core.upload_meshes(sc.bank.tris, sc.bank.tris_model_count)
+    core.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+    dev = torch.device("cuda", 0)
+    t = {
+        "raw": torch.from_numpy(sc.depth_raw).to(dev),
+        "mask": torch.from_numpy(sc.mask).to(dev),
+        "src": torch.from_numpy(sc.src_depth_cm).to(dev),
+        "poses": torch.from_numpy(case.poses).to(dev),
+        "pm": torch.from_numpy(case.pose_model).to(dev),
+        "pl": torch.from_numpy(case.pose_label).to(dev),
+        "tot": torch.from_numpy(case.pose_obs_total).to(dev),
+    }
+    xyz, lab = core.observed_cloud(t["raw"], t["mask"], stride, sc.depth_factor)
+    t["obs_xyz"], t["obs_lab"] = xyz, lab
+    core.set_observation(t["src"], t["mask"], xyz, lab, 0.01)
+    return core, t
+
+
+@pytest.fixture(scope="module")
+def one_object():
+    case = SceneCase(("003_cracker_box",), n_poses=96)
+    core, t = _setup(case)
+    return case, core, t
+
+
+@pytest.fixture(scope="module")
+def three_objects():
+    case = SceneCase(("003_cracker_box", "005_tomato_soup_can", "061_foam_brick"), n_poses=48)
+    core, t = _setup(case)
+    return case, core, t
+
+
+def test_observed_cloud_matches_oracle(one_object):
+    case, core, t = one_object
+    xyz, lab = t["obs_xyz"].cpu().numpy(), t["obs_lab"].cpu().numpy()
+    assert _bits_equal(xyz, case.obs_xyz_raw)
+    assert _bits_equal(lab, case.obs_label_raw)
+
+
+@pytest.mark.parametrize("fixture", ["one_object", "three_objects"])
+def test_render_full_zbuffer_bit_exact(fixture, request):
+    case, core, t = request.getfixturevalue(fixture)
+    sc = case.scene
+    n = min(24, len(case.poses))
+    zb = core.render(t["poses"][:n], t["pm"][:n], t["pl"][:n]).cpu().numpy()
+    ref = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n],
+                              case.pose_label[:n], sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0)
+    assert (ref > 0).sum() > 0
+    mism = np.argwhere(zb != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatching pixels, first {mism[:5]}"
+
+
+def test_render_3dof_occlusion_threshold(one_object):
+    case, core, t = one_object
+    sc = case.scene
+    n = 16
+    zb = core.render(t["poses"][:n], t["pm"][:n], None, occlusion_threshold=1.0).cpu().numpy()
+    ref = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n], None,
+                              sc.width, sc.height, sc.proj, sc.src_depth_cm, None, 1.0)
+    assert np.array_equal(zb, ref)
+
+
+@pytest.mark.parametrize("fixture", ["one_object", "three_objects"])
+def test_evaluate_costs_bit_exact(fixture, request):
+    case, core, t = request.getfixturevalue(fixture)
+    rc, oc, df = core.evaluate(t["poses"], t["pm"], t["pl"], t["tot"], cost_type=2, stride=case.stride)
+    torch.cuda.synchronize()
+    orc, ooc, odf = case.oracle_costs(cost_type=2)
+    rc, oc, df = rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy()
+    bad = np.nonzero(~((rc == orc) & (oc == ooc) & (df == odf)))[0]
+    assert len(bad) == 0, f"{len(bad)} poses differ, e.g. {bad[:5]}: gpu {rc[bad[:3]]} {oc[bad[:3]]} oracle {orc[bad[:3]]} {ooc[bad[:3]]}"
+    # the GT pose (written at n//3 of each object's block) must be a perfect fit
+    assert (rc >= 0).sum() > len(rc) // 4
+
+
+def test_evaluate_3dof_bit_exact(one_object):
+    case, core, t = one_object
+    tot = torch.full((len(case.poses),), float(len(case.obs_xyz)), device=t["poses"].device)
+    rc, oc, df = core.evaluate(t["poses"], t["pm"], None, tot, cost_type=0, stride=case.stride)
+    orc, ooc, odf = case.oracle_costs(cost_type=0)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+
+
+def test_sampled_zbuffer_equals_full_render(one_object):
+    case, core, t = one_object
+    sc = case.scene
+    n = 24
+    s = case.stride
+    hs, ws = (sc.height + s - 1) // s, sc.width // s
+    dbg = torch.empty((n, hs, ws), dtype=torch.int32, device=t["poses"].device)
+    core.evaluate(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n], cost_type=2, stride=s, dbg_zs=dbg)
+    full = core.render(t["poses"][:n], t["pm"][:n], t["pl"][:n]).cpu().numpy()
+    assert np.array_equal(dbg.cpu().numpy(), full[:, ::s, ::s])
+
+
+def test_depth_to_cloud_matches_oracle(one_object):
+    case, core, t = one_object
+    sc = case.scene
+    n = 12
+    zb = core.render(t["poses"][:n], t["pm"][:n], t["pl"][:n])
+    xyz, pose, lab = core.depth_to_cloud(zb, case.stride, 100.0, pose_label=t["pl"][:n])
+    oxyz, opose, olab = oracle.depth_to_cloud(zb.cpu().numpy(), case.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0,
+                                              pose_label=case.pose_label[:n])
+    assert _bits_equal(xyz.cpu().numpy(), oxyz)
+    assert np.array_equal(pose.cpu().numpy(), opose)
+    assert np.array_equal(lab.cpu().numpy(), olab)
+
+
+def test_select_matches_oracle(three_objects):
+    case, core, t = three_objects
+    rc, oc, df = core.evaluate(t["poses"], t["pm"], t["pl"], t["tot"], cost_type=2, stride=case.stride)
+    keys = core.select(rc, oc, t["pm"], case.K, index_base=1000)
+    cost, idx = decode_keys(keys)
+    ocost, oidx = oracle.select(rc.cpu().numpy(), oc.cpu().numpy(), case.pose_model, case.K, 1000)
+    assert np.array_equal(cost, ocost)
+    assert np.array_equal(idx, oidx)
+
+
+def test_select_ties_lowest_index():
+    core = PoseCore(0)
+    dev = torch.device("cuda", 0)
+    rc = torch.tensor([5.0, 3.0, 3.0, -1.0, 3.0, 90.0], device=dev)
+    oc = torch.tensor([5.0, 4.0, 4.0, 0.0, 4.0, 10.0], device=dev)
+    pm = torch.tensor([0, 0, 0, 0, 1, 1], dtype=torch.int32, device=dev)
+    cost, idx = decode_keys(core.select(rc, oc, pm, 2))
+    ocost, oidx = oracle.select(rc.cpu().numpy(), oc.cpu().numpy(), pm.cpu().numpy(), 2)
+    assert list(cost) == [7, 7] and list(idx) == [1, 4]
+    assert np.array_equal(cost, ocost) and np.array_equal(idx, oidx)
+
+
+def test_edge_poses(one_object):
+    """Poses behind the camera, straddling z = 0, out of view and very close (large triangles)."""
+    case, core, t = one_object
+    sc = case.scene
+    P = []
+    for tz in (-0.5, 0.0, 0.02, 0.12, 0.25, 3.0):
+        T = np.eye(4)
+        T[:3, 3] = (0.0, 0.0, tz)
+        P.append(T)
+    T = np.eye(4); T[:3, 3] = (2.0, 0.0, 0.8); P.append(T)       # out of view
+    T = np.eye(4); T[:3, 3] = (0.0, 0.0, 0.10); T[:3, :3] = syn._rot_z(0.3); P.append(T)
+    p16 = init_from_eigen_batch(np.stack(P))
+    n = len(P)
+    dev = t["poses"].device
+    poses = torch.from_numpy(p16).to(dev)
+    pm = torch.zeros(n, dtype=torch.int32, device=dev)
+    pl = torch.zeros(n, dtype=torch.int32, device=dev)
+    tot = torch.full((n,), float(case.pose_obs_total[0]), device=dev)
+    zb = core.render(poses, pm, pl).cpu().numpy()
+    ref = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, p16, np.zeros(n, np.int32),
+                              np.zeros(n, np.int32), sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0)
+    assert np.array_equal(zb, ref)
+    rc, oc, df = core.evaluate(poses, pm, pl, tot, cost_type=2, stride=8)
+    orc, ooc, odf = oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, p16, np.zeros(n, np.int32),
+                                    np.zeros(n, np.int32), sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask,
+                                    1.0, 8, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz, case.label_start,
+                                    case.label_end, np.full(n, case.pose_obs_total[0], np.float32), 2, True, 0.01)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+
+
+def test_empty_batch_and_errors(one_object):
+    case, core, t = one_object
+    dev = t["poses"].device
+    e = torch.empty((0, 16), dtype=torch.float32, device=dev)
+    ei = torch.empty((0,), dtype=torch.int32, device=dev)
+    ef = torch.empty((0,), dtype=torch.float32, device=dev)
+    rc, oc, df = core.evaluate(e, ei, ei, ef, cost_type=2, stride=8)
+    assert rc.numel() == 0
+    from perception_amd._native import PcoreError
+    with pytest.raises(PcoreError):
+        core.evaluate(t["poses"][:2], t["pm"][:2], t["pl"][:2], t["tot"][:2], cost_type=1, stride=8)
+    with pytest.raises(PcoreError):
+        core.evaluate(t["poses"][:2], t["pm"][:2], t["pl"][:2], t["tot"][:2], cost_type=2, stride=7)
