@@ -190,3 +190,11 @@ def decode_keys(keys) -> Tuple[np.ndarray, np.ndarray]:
     cost = np.where(none, np.int32(2**31 - 1), cost)
     idx = np.where(none, -1, idx)
     return cost, idx
+
+
+def encode_key(cost: int, index: int) -> int:
+    """The int64 selection key of pcore_select (include/pcore.h): ((cost ^ 0x80000000) << 31) | index."""
+    if cost == 2**31 - 1 and index < 0:
+        return _native.PCORE_KEY_NONE
+    hi = (int(cost) & 0xFFFFFFFF) ^ 0x80000000
+    return (hi << 31) | (int(index) & 0x7FFFFFFF)

@@ -1,0 +1,58 @@
+"""N > 1 path on CPU: world_size-2 gloo ranks each select over their pose shard; one all-reduce(MIN)
+of the int64 keys must equal the single-process selection over all poses."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, rc, oc, pm, K, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from perception_amd.core import decode_keys, encode_key
+    from perception_amd.distributed import allreduce_min_keys, init_from_env, shard_range
+
+    init_from_env("gloo")
+    lo, hi = shard_range(len(rc), rank, world)
+    cost, idx = oracle.select(rc[lo:hi], oc[lo:hi], pm[lo:hi], K, index_base=lo)
+    keys = torch.tensor([encode_key(int(c), int(i)) for c, i in zip(cost, idx)], dtype=torch.int64)
+    allreduce_min_keys(keys)
+    q.put((rank, decode_keys(keys)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_argmin_equals_single_process():
+    rng = np.random.default_rng(3)
+    n, K = 1001, 3
+    rc = rng.integers(0, 40, n).astype(np.float32)
+    oc = rng.integers(0, 40, n).astype(np.float32)
+    rc[rng.integers(0, n, 30)] = -1.0
+    pm = rng.integers(0, K, n).astype(np.int32)
+    import oracle
+
+    ref_cost, ref_idx = oracle.select(rc, oc, pm, K)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rc, oc, pm, K, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, (cost, idx) in res:
+        assert np.array_equal(cost, ref_cost)
+        assert np.array_equal(idx, ref_idx)

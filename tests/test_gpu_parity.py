@@ -207,3 +207,34 @@ def test_empty_batch_and_errors(one_object):
         core.evaluate(t["poses"][:2], t["pm"][:2], t["pl"][:2], t["tot"][:2], cost_type=1, stride=8)
     with pytest.raises(PcoreError):
         core.evaluate(t["poses"][:2], t["pm"][:2], t["pl"][:2], t["tot"][:2], cost_type=2, stride=7)
+
+
+@pytest.mark.parametrize("name", ["oracle_scene_1obj.npz", "oracle_scene_3obj.npz"])
+def test_gpu_reproduces_committed_fixture(name):
+    import hashlib
+    import os
+
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)))
+    W, H = int(g["cam"][0]), int(g["cam"][1])
+    fx, fy, cx, cy = (float(v) for v in g["cam"][2:])
+    stride = int(g["stride"])
+    K = len(g["tris_model_count"])
+    dev = torch.device("cuda", 0)
+    core = PoseCore(0)
+    core.upload_meshes(g["tris"], g["tris_model_count"])
+    core.set_camera(W, H, fx, fy, cx, cy, g["proj"])
+    mask = torch.from_numpy(g["mask"]).to(dev)
+    xyz, lab = core.observed_cloud(torch.from_numpy(g["depth_raw"]).to(dev), mask, stride, float(g["depth_factor"]))
+    assert _bits_equal(xyz.cpu().numpy(), g["obs_xyz"]) and np.array_equal(lab.cpu().numpy(), g["obs_label"])
+    core.set_observation(torch.from_numpy(g["src_depth_cm"]).to(dev), mask, xyz, lab, 0.01)
+    poses = torch.from_numpy(g["poses"]).to(dev)
+    pm = torch.from_numpy(g["pose_model"]).to(dev)
+    z = core.render(poses, pm, pm).cpu().numpy()
+    assert [hashlib.sha256(np.ascontiguousarray(zi).tobytes()).hexdigest() for zi in z] == list(g["z_hash"])
+    rc, oc, df = core.evaluate(poses, pm, pm, torch.from_numpy(g["pose_obs_total"]).to(dev), cost_type=2,
+                               stride=stride)
+    assert _bits_equal(rc.cpu().numpy(), g["rc"])
+    assert _bits_equal(oc.cpu().numpy(), g["oc"])
+    assert _bits_equal(df.cpu().numpy(), g["diff"])
+    cost, idx = decode_keys(core.select(rc, oc, pm, K))
+    assert np.array_equal(cost, g["best_cost"]) and np.array_equal(idx, g["best_index"])

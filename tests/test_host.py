@@ -1,0 +1,74 @@
+"""Host-side logic: mat4x4 helpers, key encoding, sharding, synthetic proxies."""
+import numpy as np
+
+from perception_amd import synthetic as syn
+from perception_amd.core import decode_keys, encode_key
+from perception_amd.distributed import shard_range
+from perception_amd.model import (init_from_eigen, init_from_eigen_batch, matrix_to_quat_xyzw, pose_matrix,
+                                  quat_xyzw_to_matrix, to_eigen)
+
+
+def test_mat4x4_scaling_roundtrip():
+    T = pose_matrix([0.1, -0.2, 0.8], [0.1, 0.2, 0.3, 0.9])
+    m = init_from_eigen(T, 100)
+    assert m.dtype == np.float32 and m.shape == (16,)
+    assert np.allclose(m[:12].reshape(3, 4), T[:3] * 100, rtol=1e-6)
+    assert np.array_equal(m[12:], np.array([0, 0, 0, 1], np.float32))
+    assert np.allclose(to_eigen(m, 100), T, atol=1e-6)
+    assert np.array_equal(init_from_eigen_batch(np.stack([T, T]))[1], m)
+
+
+def test_quaternion_roundtrip():
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        R = quat_xyzw_to_matrix(q)
+        assert np.allclose(R @ R.T, np.eye(3), atol=1e-12)
+        q2 = matrix_to_quat_xyzw(R)
+        assert np.allclose(np.abs(np.dot(q, q2)), 1.0, atol=1e-9)
+
+
+def test_key_encoding_orders_like_the_reference_scan():
+    keys = [encode_key(c, i) for c, i in [(7, 5), (7, 3), (6, 100), (0, 2**31 - 2), (-5, 1)]]
+    order = np.argsort(keys)
+    assert list(order) == [4, 3, 2, 1, 0]
+    cost, idx = decode_keys(np.array(keys, np.int64))
+    assert list(cost) == [7, 7, 6, 0, -5] and list(idx) == [5, 3, 100, 2**31 - 2, 1]
+    none_cost, none_idx = decode_keys(np.array([0x7FFFFFFFFFFFFFFF], np.int64))
+    assert none_cost[0] == 2**31 - 1 and none_idx[0] == -1
+    assert all(0 <= k < 2**63 - 1 for k in keys)
+
+
+def test_shard_range_covers_exactly():
+    for total in (0, 1, 7, 10000, 200003):
+        for world in (1, 2, 3, 8):
+            parts = [shard_range(total, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == total
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_cracker_box_proxy_has_12288_triangles():
+    m = syn.ycb_proxy("003_cracker_box")
+    assert m.tris.shape == (12288, 9)
+    ext = m.tris.reshape(-1, 3).max(0) - m.tris.reshape(-1, 3).min(0)
+    assert np.allclose(ext, [0.060, 0.158, 0.210], atol=1e-6)
+    assert (m.colors == 128).all()
+
+
+def test_all_21_proxies_build():
+    bank = syn.model_bank(list(syn.YCB_PROXIES))
+    assert len(bank.models) == 21
+    assert bank.tris.shape[0] == bank.tris_model_count.sum()
+
+
+def test_candidate_poses_include_gt_and_are_rigid():
+    rng = np.random.default_rng(1)
+    gt = syn.default_gt_pose(rng)
+    P = syn.candidate_poses(gt[:3, 3], 1000, rng, include=gt)
+    assert P.shape == (1000, 4, 4)
+    assert np.array_equal(P[1000 // 3], gt)
+    R = P[:, :3, :3]
+    assert np.allclose(np.einsum("nij,nkj->nik", R, R), np.eye(3), atol=1e-9)
