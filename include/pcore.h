@@ -113,6 +113,26 @@ int pcore_evaluate(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_m
                    const pcore_eval_params* params, float* d_out_rc, float* d_out_oc, float* d_out_diff,
                    int32_t* d_dbg_zs, pcore_stream stream);
 
+/* GICP settings; the reference hard-codes them at renderer.cu:1696-1705. */
+typedef struct pcore_icp_params {
+    int32_t k_correspondences;      /* covariance neighbours, 10 (<= 16) */
+    int32_t max_iterations;         /* 150 */
+    double rotation_epsilon;        /* 2e-3 */
+    double transformation_epsilon;  /* 5e-4 */
+} pcore_icp_params;
+
+/* Stage "COST" with do_icp = true (renderer.cu:1688-1817): render, unproject at stride, per-pose GICP of
+ * the rendered cloud onto the pose's observed label segment (FastGICPCudaCore::optimize_multi), compose
+ * T * pose (concatenate_transforms, renderer.cu:1412-1429), re-render and re-score.  d_out_poses: N x 16
+ * adjusted mat4x4 (the reference's adjusted_poses); d_out_iters (nullable): GICP iterations per pose.
+ * Costs as pcore_evaluate, for the adjusted poses.  Device pointers; needs per-context scratch that
+ * grows on first use (chunks of at most 2048 poses). */
+int pcore_evaluate_icp(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model,
+                       const int32_t* d_pose_label, const float* d_pose_obs_total, int32_t num_poses,
+                       const pcore_eval_params* params, const pcore_icp_params* icp, float* d_out_poses,
+                       int32_t* d_out_iters, float* d_out_rc, float* d_out_oc, float* d_out_diff,
+                       pcore_stream stream);
+
 /* Stage "RENDER": full-resolution int32 z-buffers (cm) with source occlusion and INT_MAX -> 0
  * (image_render, image_renderer.cuh:336-496).  d_out_depth: N x H x W.  Parity mode. */
 int pcore_render(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,

@@ -161,3 +161,82 @@ def evaluate(tris, tris_model_count, poses, pose_model, pose_label, width, heigh
                        _c(label_start, np.int32), _c(label_end, np.int32), nl, _c(pose_obs_total, np.float32),
                        cost_type, int(calc_obs), sensor_resolution, rc, oc, df, nthreads)
     return rc, oc, df
+
+
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+def _gicp_lib():
+    L = lib()
+    if not getattr(L, "_gicp_typed", False):
+        c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        L.orc_covariances.argtypes = [_f32p, c_int, c_int, _f64p]
+        L.orc_gicp.restype = c_int
+        L.orc_gicp.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, _f64p]
+        L.orc_concat_pose.argtypes = [_f64p, _f32p, _f32p]
+        L.orc_evaluate_icp.argtypes = [_f32p, c_int, _i32p, c_int, _f32p, _i32p, _opt(_i32p), c_int, c_int, c_int,
+                                       _f32p, _i32p, _opt(_u8p), c_float, c_int, c_float, c_float, c_float, c_float,
+                                       c_float, _f32p, _f64p, c_int, _opt(_i32p), _opt(_i32p), c_int, _opt(_f32p),
+                                       c_int, c_int, c_float, c_int, c_int, c_double, c_double, _f32p, _opt(_i32p),
+                                       _f32p, _f32p, _f32p, c_int]
+        L._gicp_typed = True
+    return L
+
+
+GICP_K = 10            # renderer.cu:1697 k_correspondences_
+GICP_MAX_ITER = 150    # renderer.cu:1696
+GICP_ROT_EPS = 2e-3    # renderer.cu:1698
+GICP_TRANS_EPS = 5e-4  # renderer.cu:1699
+
+
+def covariances(xyz, k=GICP_K):
+    xyz = _c(xyz, np.float32).reshape(-1, 3)
+    out = np.zeros((max(len(xyz), 1), 6), np.float64)
+    if len(xyz):
+        _gicp_lib().orc_covariances(xyz.reshape(-1), len(xyz), k, out.reshape(-1))
+    return out[:len(xyz)]
+
+
+def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS):
+    src = _c(src, np.float32).reshape(-1, 3)
+    tgt = _c(tgt, np.float32).reshape(-1, 3)
+    T = np.zeros(16, np.float64)
+    z3, z6 = np.zeros(3, np.float32), np.zeros(6, np.float64)
+    it = _gicp_lib().orc_gicp(src.reshape(-1) if len(src) else z3, _c(src_cov, np.float64).reshape(-1) if len(src) else z6,
+                              len(src), tgt.reshape(-1) if len(tgt) else z3,
+                              _c(tgt_cov, np.float64).reshape(-1) if len(tgt) else z6, len(tgt), max_iter, rot_eps,
+                              trans_eps, T)
+    return T.reshape(4, 4), it
+
+
+def concat_pose(T, pose):
+    out = np.zeros(16, np.float32)
+    _gicp_lib().orc_concat_pose(_c(T, np.float64).reshape(-1), _c(pose, np.float32).reshape(-1), out)
+    return out
+
+
+def evaluate_icp(tris, tris_model_count, poses, pose_model, pose_label, width, height, proj, src_depth, src_mask,
+                 occlusion_threshold, stride, cx, cy, fx, fy, depth_factor, o_xyz, o_cov, label_start, label_end,
+                 pose_obs_total, cost_type, calc_obs, sensor_resolution, k=GICP_K, max_iter=GICP_MAX_ITER,
+                 rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS, nthreads=0):
+    """do_icp flow; returns (adjusted poses (N,16), iterations (N,), rc, oc, diff)."""
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    o_xyz = _c(o_xyz, np.float32).reshape(-1)
+    o_cov = _c(o_cov, np.float64).reshape(-1)
+    adj = np.zeros((n, 16), np.float32)
+    iters = np.zeros(n, np.int32)
+    rc = np.zeros(n, np.float32)
+    oc = np.zeros(n, np.float32)
+    df = np.zeros(n, np.float32)
+    nl = 0 if label_start is None else len(label_start)
+    _gicp_lib().orc_evaluate_icp(
+        tris, tris.size // 9, _c(tris_model_count, np.int32), len(tris_model_count), poses, _c(pose_model, np.int32),
+        _c(pose_label, np.int32), n, width, height, _c(proj, np.float32), _c(src_depth, np.int32).reshape(-1),
+        None if src_mask is None else _c(src_mask, np.uint8).reshape(-1), float(occlusion_threshold), stride, cx, cy,
+        fx, fy, depth_factor, o_xyz if o_xyz.size else np.zeros(3, np.float32),
+        o_cov if o_cov.size else np.zeros(6, np.float64), o_xyz.size // 3, _c(label_start, np.int32),
+        _c(label_end, np.int32), nl, _c(pose_obs_total, np.float32), cost_type, int(calc_obs), sensor_resolution, k,
+        max_iter, rot_eps, trans_eps, adj.reshape(-1), iters, rc, oc, df, nthreads)
+    return adj, iters, rc, oc, df

@@ -358,3 +358,342 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
 }
 
 }  // extern "C"
+
+// ==================================================================================================
+// GICP (build-owned spec; see pcore_oracle.h and DESIGN.md "GICP spec")
+// ==================================================================================================
+namespace {
+
+constexpr int kGicpThreads = 256;  // GPU workgroup size whose reduction order the oracle mirrors
+constexpr int kMaxK = 16;
+constexpr double kPlaneScale = 1.0 - 1e-3;  // I - (1 - 1e-3) n n^T == U diag(1, 1, 1e-3) U^T
+
+// k nearest points of the same cloud, ordered by (distance, index).
+int knn_self(const float* xyz, int n, int i, int k, int* nb) {
+    float nd[kMaxK];
+    int cnt = 0;
+    const float* xi = xyz + (size_t)3 * i;
+    for (int j = 0; j < n; j++) {
+        const float d = sqdist(xi, xyz + (size_t)3 * j);
+        int pos;
+        if (cnt < k) pos = cnt++;
+        else if (d < nd[k - 1]) pos = k - 1;
+        else continue;
+        while (pos > 0 && nd[pos - 1] > d) {
+            nd[pos] = nd[pos - 1];
+            nb[pos] = nb[pos - 1];
+            pos--;
+        }
+        nd[pos] = d;
+        nb[pos] = j;
+    }
+    return cnt;
+}
+
+void plane_regularize(const double c[6], double out[6]) {
+    double A[3][3] = {{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}};
+    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+    static const int PQ[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    for (int sweep = 0; sweep < 6; sweep++)
+        for (int r = 0; r < 3; r++) {
+            const int p = PQ[r][0], q = PQ[r][1], o = 3 - p - q;
+            const double apq = A[p][q];
+            if (apq == 0.0) continue;
+            const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+            double t = 1.0 / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+            if (theta < 0.0) t = -t;
+            const double cc = 1.0 / std::sqrt(t * t + 1.0);
+            const double ss = t * cc;
+            const double app = A[p][p], aqq = A[q][q];
+            A[p][p] = app - t * apq;
+            A[q][q] = aqq + t * apq;
+            A[p][q] = 0.0;
+            A[q][p] = 0.0;
+            const double aop = A[o][p], aoq = A[o][q];
+            A[o][p] = cc * aop - ss * aoq;
+            A[p][o] = A[o][p];
+            A[o][q] = ss * aop + cc * aoq;
+            A[q][o] = A[o][q];
+            for (int k = 0; k < 3; k++) {
+                const double vkp = V[k][p], vkq = V[k][q];
+                V[k][p] = cc * vkp - ss * vkq;
+                V[k][q] = ss * vkp + cc * vkq;
+            }
+        }
+    int m = 0;
+    if (A[1][1] < A[m][m]) m = 1;
+    if (A[2][2] < A[m][m]) m = 2;
+    const double n0 = V[0][m], n1 = V[1][m], n2 = V[2][m];
+    out[0] = 1.0 - kPlaneScale * (n0 * n0);
+    out[1] = 0.0 - kPlaneScale * (n0 * n1);
+    out[2] = 0.0 - kPlaneScale * (n0 * n2);
+    out[3] = 1.0 - kPlaneScale * (n1 * n1);
+    out[4] = 0.0 - kPlaneScale * (n1 * n2);
+    out[5] = 1.0 - kPlaneScale * (n2 * n2);
+}
+
+void covariance_one(const float* xyz, int n, int i, int k, double* out6) {
+    int nb[kMaxK];
+    const int ke = knn_self(xyz, n, i, k, nb);
+    double mx = 0.0, my = 0.0, mz = 0.0;
+    for (int q = 0; q < ke; q++) {
+        mx += (double)xyz[3 * (size_t)nb[q] + 0];
+        my += (double)xyz[3 * (size_t)nb[q] + 1];
+        mz += (double)xyz[3 * (size_t)nb[q] + 2];
+    }
+    const double kd = (double)ke;
+    mx = mx / kd; my = my / kd; mz = mz / kd;
+    double c[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < ke; q++) {
+        const double dx = (double)xyz[3 * (size_t)nb[q] + 0] - mx;
+        const double dy = (double)xyz[3 * (size_t)nb[q] + 1] - my;
+        const double dz = (double)xyz[3 * (size_t)nb[q] + 2] - mz;
+        c[0] += dx * dx; c[1] += dx * dy; c[2] += dx * dz;
+        c[3] += dy * dy; c[4] += dy * dz; c[5] += dz * dz;
+    }
+    for (int e = 0; e < 6; e++) c[e] = c[e] / kd;
+    plane_regularize(c, out6);
+}
+
+// per-point Gauss-Newton contribution: acc[0..20] = upper(H) row-major, [21..26] = b, [27] = error
+bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const double* cs, const float* tgt,
+                  const double* tcov, int nt, double acc[28]) {
+    const double s0 = (double)s[0], s1 = (double)s[1], s2 = (double)s[2];
+    double q[3];
+    for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
+    const float qf[3] = {(float)q[0], (float)q[1], (float)q[2]};
+    int j = -1;
+    float best = INFINITY;
+    for (int o = 0; o < nt; o++) {
+        const float d = sqdist(qf, tgt + (size_t)3 * o);
+        if (d < best) { best = d; j = o; }
+    }
+    if (j < 0) return false;
+    const double* ct = tcov + (size_t)6 * j;
+    const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
+    const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
+    double RC[3][3], A[3][3];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) RC[r][c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) A[r][c] = Ct[r][c] + (RC[r][0] * R[c][0] + RC[r][1] * R[c][1] + RC[r][2] * R[c][2]);
+    double m[3][3];
+    m[0][0] = A[1][1] * A[2][2] - A[1][2] * A[2][1];
+    m[0][1] = A[0][2] * A[2][1] - A[0][1] * A[2][2];
+    m[0][2] = A[0][1] * A[1][2] - A[0][2] * A[1][1];
+    m[1][0] = A[1][2] * A[2][0] - A[1][0] * A[2][2];
+    m[1][1] = A[0][0] * A[2][2] - A[0][2] * A[2][0];
+    m[1][2] = A[0][2] * A[1][0] - A[0][0] * A[1][2];
+    m[2][0] = A[1][0] * A[2][1] - A[1][1] * A[2][0];
+    m[2][1] = A[0][1] * A[2][0] - A[0][0] * A[2][1];
+    m[2][2] = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+    const double det = A[0][0] * m[0][0] + A[0][1] * m[1][0] + A[0][2] * m[2][0];
+    const double inv = 1.0 / det;
+    double M[3][3];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
+    const double* tp = nullptr;
+    (void)tp;
+    const double e[3] = {(double)tgt[3 * (size_t)j + 0] - q[0], (double)tgt[3 * (size_t)j + 1] - q[1],
+                         (double)tgt[3 * (size_t)j + 2] - q[2]};
+    const double J[3][6] = {{0.0, -q[2], q[1], -1.0, 0.0, 0.0},
+                            {q[2], 0.0, -q[0], 0.0, -1.0, 0.0},
+                            {-q[1], q[0], 0.0, 0.0, 0.0, -1.0}};
+    double MJ[3][6];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 6; c++) MJ[r][c] = M[r][0] * J[0][c] + M[r][1] * J[1][c] + M[r][2] * J[2][c];
+    int h = 0;
+    for (int a = 0; a < 6; a++)
+        for (int b = a; b < 6; b++) acc[h++] += J[0][a] * MJ[0][b] + J[1][a] * MJ[1][b] + J[2][a] * MJ[2][b];
+    double Me[3];
+    for (int r = 0; r < 3; r++) Me[r] = M[r][0] * e[0] + M[r][1] * e[1] + M[r][2] * e[2];
+    for (int a = 0; a < 6; a++) acc[21 + a] += J[0][a] * Me[0] + J[1][a] * Me[1] + J[2][a] * Me[2];
+    acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+    return true;
+}
+
+// 6x6 LDLT without pivoting; returns false if not positive definite.
+bool ldlt_solve6(const double Hu[21], const double b[6], double d[6]) {
+    double H[6][6];
+    int h = 0;
+    for (int a = 0; a < 6; a++)
+        for (int c = a; c < 6; c++) { H[a][c] = Hu[h]; H[c][a] = Hu[h]; h++; }
+    double L[6][6] = {}, D[6];
+    for (int j = 0; j < 6; j++) {
+        double v = H[j][j];
+        for (int k = 0; k < j; k++) v = v - L[j][k] * L[j][k] * D[k];
+        if (!(v > 0.0) || !std::isfinite(v)) return false;
+        D[j] = v;
+        for (int i = j + 1; i < 6; i++) {
+            double w = H[i][j];
+            for (int k = 0; k < j; k++) w = w - L[i][k] * L[j][k] * D[k];
+            L[i][j] = w / D[j];
+        }
+    }
+    double y[6];
+    for (int i = 0; i < 6; i++) {
+        double v = -b[i];
+        for (int k = 0; k < i; k++) v = v - L[i][k] * y[k];
+        y[i] = v;
+    }
+    for (int i = 5; i >= 0; i--) {
+        double v = y[i] / D[i];
+        for (int k = i + 1; k < 6; k++) v = v - L[k][i] * d[k];
+        d[i] = v;
+    }
+    for (int i = 0; i < 6; i++)
+        if (!std::isfinite(d[i])) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+void orc_covariances(const float* xyz, int n, int k, double* out_cov6) {
+    if (k > kMaxK) k = kMaxK;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) covariance_one(xyz, n, i, k, out_cov6 + (size_t)6 * i);
+}
+
+int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov, int nt,
+             int max_iter, double rot_eps, double trans_eps, double* out_T) {
+    double R[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+    double t[3] = {0.0, 0.0, 0.0};
+    int it = 0;
+    if (ns > 0 && nt > 0) {
+        std::vector<double> part((size_t)kGicpThreads * 28);
+        for (it = 0; it < max_iter;) {
+            std::fill(part.begin(), part.end(), 0.0);
+            for (int i = 0; i < ns; i++)
+                gicp_contrib(R, t, src_xyz + (size_t)3 * i, src_cov + (size_t)6 * i, tgt_xyz, tgt_cov, nt,
+                             part.data() + (size_t)28 * (i % kGicpThreads));
+            // fixed reduction: per wave shuffle-down tree to lane 0, then the 4 waves in order
+            double tot[28];
+            for (int v = 0; v < 28; v++) {
+                double wsum[kGicpThreads / 64];
+                for (int w = 0; w < kGicpThreads / 64; w++) {
+                    double lane[64];
+                    for (int l = 0; l < 64; l++) lane[l] = part[(size_t)28 * (w * 64 + l) + v];
+                    for (int off = 32; off > 0; off >>= 1)
+                        for (int l = 0; l < off; l++) lane[l] = lane[l] + lane[l + off];
+                    wsum[w] = lane[0];
+                }
+                double s = wsum[0];
+                for (int w = 1; w < kGicpThreads / 64; w++) s = s + wsum[w];
+                tot[v] = s;
+            }
+            double d[6];
+            if (!ldlt_solve6(tot, tot + 21, d)) break;
+            it++;
+            double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
+            const double nrm = std::sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+            const double inv = 1.0 / nrm;
+            qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
+            const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
+            const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
+            const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
+                                     {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
+                                     {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
+            double Rn[3][3], tn[3];
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++) Rn[r][c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
+                tn[r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
+            }
+            double dr = 0.0, dt = 0.0;
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++) {
+                    const double v = std::fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
+                    dr = v > dr ? v : dr;
+                }
+                const double v = std::fabs(d[3 + r]);
+                dt = v > dt ? v : dt;
+            }
+            std::memcpy(R, Rn, sizeof(R));
+            std::memcpy(t, tn, sizeof(t));
+            if (dr < rot_eps && dt < trans_eps) break;
+        }
+    }
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) out_T[4 * r + c] = R[r][c];
+        out_T[4 * r + 3] = t[r];
+    }
+    out_T[12] = 0.0; out_T[13] = 0.0; out_T[14] = 0.0; out_T[15] = 1.0;
+    return it;
+}
+
+void orc_concat_pose(const double* T, const float* pose, float* out_pose) {
+    float A[4][4], Tf[4][4], P[4][4];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            A[r][c] = r < 3 ? pose[4 * r + c] / 100.0f : pose[4 * r + c];  // to_eigen(100)
+            Tf[r][c] = (float)T[4 * r + c];                                // Isometry3f
+        }
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) P[r][c] = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) out_pose[4 * r + c] = r < 3 ? (float)((double)P[r][c] * 100) : P[r][c];
+}
+
+void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model_count, int num_models,
+                      const float* poses, const int32_t* pose_model, const int32_t* pose_label, int num_poses,
+                      int width, int height, const float* proj, const int32_t* src_depth, const uint8_t* src_mask,
+                      float occlusion_threshold, int stride, float cx, float cy, float fx, float fy,
+                      float depth_factor, const float* o_xyz, const double* o_cov, int num_o,
+                      const int32_t* label_start, const int32_t* label_end, int num_labels,
+                      const float* pose_obs_total, int cost_type, int calc_obs, float sensor_resolution, int k_corr,
+                      int max_iter, double rot_eps, double trans_eps, float* out_adj, int32_t* out_iters,
+                      float* out_rc, float* out_oc, float* out_diff, int nthreads) {
+    (void)num_tris;
+    std::vector<int> lo, hi;
+    model_ranges(tris_model_count, num_models, lo, hi);
+    const bool use_seg = pose_label != nullptr;
+    const size_t npx = (size_t)width * height;
+    const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+    {
+        std::vector<int32_t> depth(npx);
+        std::vector<float> xyz((size_t)3 * ws * hs);
+        std::vector<double> cov((size_t)6 * ws * hs);
+        std::vector<float> d2((size_t)ws * hs);
+        std::vector<int32_t> nn((size_t)ws * hs), rpose((size_t)ws * hs, 0);
+#pragma omp for schedule(dynamic, 1)
+        for (int n = 0; n < num_poses; n++) {
+            const int m = pose_model[n];
+            const int32_t pl = use_seg ? pose_label[n] : 0;
+            int l0 = 0, l1 = num_o;
+            if (use_seg && label_start != nullptr) {
+                if (pl < 0 || pl >= num_labels) { l0 = 0; l1 = 0; }
+                else { l0 = label_start[pl]; l1 = label_end[pl]; }
+            }
+            const float* pose = poses + (size_t)16 * n;
+            render_one_pose(tris, lo[m], hi[m], pose, width, height, proj, src_depth, src_mask, use_seg, pl,
+                            occlusion_threshold, depth.data());
+            int nr = orc_depth_to_cloud(depth.data(), 1, width, height, stride, cx, cy, fx, fy, depth_factor, nullptr,
+                                        nullptr, xyz.data(), nullptr, nullptr, ws * hs);
+            int k = k_corr > kMaxK ? kMaxK : k_corr;
+            for (int i = 0; i < nr; i++) covariance_one(xyz.data(), nr, i, k, cov.data() + (size_t)6 * i);
+            double T[16];
+            const int iters = orc_gicp(xyz.data(), cov.data(), nr, o_xyz + (size_t)3 * l0, o_cov + (size_t)6 * l0,
+                                       l1 - l0, max_iter, rot_eps, trans_eps, T);
+            if (out_iters) out_iters[n] = iters;
+            float* adj = out_adj + (size_t)16 * n;
+            orc_concat_pose(T, pose, adj);
+            render_one_pose(tris, lo[m], hi[m], adj, width, height, proj, src_depth, src_mask, use_seg, pl,
+                            occlusion_threshold, depth.data());
+            nr = orc_depth_to_cloud(depth.data(), 1, width, height, stride, cx, cy, fx, fy, depth_factor, nullptr,
+                                    nullptr, xyz.data(), nullptr, nullptr, ws * hs);
+            for (int i = 0; i < nr; i++) knn1_range(xyz.data() + (size_t)3 * i, o_xyz, l0, l1, d2[i], nn[i]);
+            float rc, oc, df;
+            const float tot = pose_obs_total ? pose_obs_total[n] : 0.0f;
+            orc_costs(1, cost_type, calc_obs, sensor_resolution, d2.data(), nn.data(), rpose.data(), nr, num_o, &tot,
+                      &rc, &oc, &df);
+            out_rc[n] = rc;
+            out_oc[n] = oc;
+            out_diff[n] = df;
+        }
+    }
+}
+
+}  // extern "C"

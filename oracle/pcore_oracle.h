@@ -80,6 +80,43 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
                   int num_labels, const float* pose_obs_total, int cost_type, int calc_obs,
                   float sensor_resolution, float* out_rc, float* out_oc, float* out_diff, int nthreads);
 
+
+
+/* ---- GICP (a9/a10): build-owned spec, parity unpinned vs fast_gicp (un-vendored fork) --------------
+ * Restates the public fast_gicp GICP at the settings of renderer.cu:1696-1705 with a deterministic
+ * arithmetic order that the GPU kernels follow exactly (DESIGN.md "GICP spec"):
+ *  - covariance: k nearest points of the same cloud (float squared distance, ties -> lower index,
+ *    list ordered by (distance, index)), double mean / covariance over k_eff = min(k, n), PLANE
+ *    regularisation C = U diag(1, 1, 1e-3) U^T from 6 cyclic Jacobi sweeps (double, sqrt/div only);
+ *  - Gauss-Newton on SE(3): correspondences = float 1-NN of (float)(R s + t) in the target segment,
+ *    Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I], H / b reduced in the GPU's fixed order
+ *    (256 per-thread sequential partials, wave shuffle-down tree, 4 wave partials in order), 6x6 LDLT
+ *    without pivoting, left update T <- [R(q(w)) | rho] T with q = normalise(1, w/2), stop when
+ *    max|dR - I| < rot_eps and max|dt| < trans_eps or after max_iter iterations.
+ * Covariances: double[6] (xx, xy, xz, yy, yz, zz) per point. */
+void orc_covariances(const float* xyz, int n, int k, double* out_cov6);
+
+/* Returns iterations run; out_T: double 4x4 row-major (source -> target, metres). */
+int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
+             int nt, int max_iter, double rot_eps, double trans_eps, double* out_T);
+
+/* concatenate_transforms (renderer.cu:1412-1429): pose' = init_from_eigen((float(T) * to_eigen(pose,100)), 100). */
+void orc_concat_pose(const double* T, const float* pose, float* out_pose);
+
+/* do_icp = true flow of render_cuda_multi_unified (renderer.cu:1688-1817) per pose: render, stride cloud,
+ * covariances, GICP against the pose's label segment (tgt_cov = label-sorted target covariances),
+ * concatenate, re-render, re-score.  out_adj: N x 16 adjusted poses; out_iters: N (nullable). */
+void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model_count, int num_models,
+                      const float* poses, const int32_t* pose_model, const int32_t* pose_label, int num_poses,
+                      int width, int height, const float* proj,
+                      const int32_t* src_depth, const uint8_t* src_mask, float occlusion_threshold,
+                      int stride, float cx, float cy, float fx, float fy, float depth_factor,
+                      const float* o_xyz, const double* o_cov, int num_o, const int32_t* label_start,
+                      const int32_t* label_end, int num_labels, const float* pose_obs_total, int cost_type,
+                      int calc_obs, float sensor_resolution, int k_corr, int max_iter, double rot_eps,
+                      double trans_eps, float* out_adj, int32_t* out_iters, float* out_rc, float* out_oc,
+                      float* out_diff, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

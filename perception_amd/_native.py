@@ -24,7 +24,8 @@ COST_DEPTH_6DOF = 2
 # every symbol declared in include/pcore.h
 EXPORTED_SYMBOLS = (
     "pcore_create", "pcore_destroy", "pcore_last_error", "pcore_abi_version", "pcore_upload_meshes",
-    "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_render",
+    "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_evaluate_icp",
+    "pcore_render",
     "pcore_depth_to_cloud", "pcore_select",
 )
 
@@ -46,6 +47,17 @@ class EvalParams(ctypes.Structure):
                 ("depth_factor", ctypes.c_float), ("sensor_resolution", ctypes.c_float),
                 ("occlusion_threshold", ctypes.c_float)]
 
+
+class IcpParams(ctypes.Structure):
+    _fields_ = [("k_correspondences", ctypes.c_int32), ("max_iterations", ctypes.c_int32),
+                ("rotation_epsilon", ctypes.c_double), ("transformation_epsilon", ctypes.c_double)]
+
+
+# renderer.cu:1696-1699
+ICP_K = 10
+ICP_MAX_ITER = 150
+ICP_ROT_EPS = 2e-3
+ICP_TRANS_EPS = 5e-4
 
 _lib = None
 
@@ -81,6 +93,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     L.pcore_observed_cloud.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, vp, i32, ctypes.POINTER(i32), vp]
     L.pcore_set_observation.argtypes = [vp, vp, vp, vp, vp, i32, f32, vp]
     L.pcore_evaluate.argtypes = [vp, vp, vp, vp, vp, i32, ctypes.POINTER(EvalParams), vp, vp, vp, vp, vp]
+    L.pcore_evaluate_icp.argtypes = [vp, vp, vp, vp, vp, i32, ctypes.POINTER(EvalParams), ctypes.POINTER(IcpParams),
+                                     vp, vp, vp, vp, vp, vp]
     L.pcore_render.argtypes = [vp, vp, vp, vp, i32, f32, vp, vp]
     L.pcore_depth_to_cloud.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, i32,
                                        ctypes.POINTER(i32), vp]

@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _native
-from ._native import Camera, EvalParams, PcoreError
+from ._native import Camera, EvalParams, IcpParams, PcoreError
 
 
 def _ptr(t: Optional[torch.Tensor], dtype: torch.dtype, name: str):
@@ -135,6 +135,31 @@ class PoseCore:
             n, ctypes.byref(p), _ptr(rc, torch.float32, "rc"), _ptr(oc, torch.float32, "oc"),
             _ptr(df, torch.float32, "diff"), _ptr(dbg_zs, torch.int32, "dbg_zs"), _stream(stream)))
         return rc, oc, df
+
+    def evaluate_icp(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
+                     pose_obs_total: Optional[torch.Tensor], cost_type: int = _native.COST_DEPTH_6DOF,
+                     calc_obs_cost: bool = True, stride: int = 8, depth_factor: float = 100.0,
+                     sensor_resolution: float = 0.01, occlusion_threshold: float = 1.0,
+                     k: int = _native.ICP_K, max_iterations: int = _native.ICP_MAX_ITER,
+                     rotation_epsilon: float = _native.ICP_ROT_EPS,
+                     transformation_epsilon: float = _native.ICP_TRANS_EPS, out=None, stream=None):
+        """Stage COST with do_icp = true.  Returns (adjusted poses (N,16), iterations (N,), rc, oc, diff)."""
+        n = int(poses.shape[0])
+        dev = poses.device
+        if out is None:
+            out = (torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+                   *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)))
+        adj, iters, rc, oc, df = out
+        p = EvalParams(int(cost_type), int(bool(calc_obs_cost)), int(stride), float(depth_factor),
+                       float(sensor_resolution), float(occlusion_threshold))
+        ip = IcpParams(int(k), int(max_iterations), float(rotation_epsilon), float(transformation_epsilon))
+        self._check(self.lib.pcore_evaluate_icp(
+            self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
+            _ptr(pose_label, torch.int32, "pose_label"), _ptr(pose_obs_total, torch.float32, "pose_obs_total"),
+            n, ctypes.byref(p), ctypes.byref(ip), _ptr(adj, torch.float32, "adjusted_poses"),
+            _ptr(iters, torch.int32, "iterations"), _ptr(rc, torch.float32, "rc"), _ptr(oc, torch.float32, "oc"),
+            _ptr(df, torch.float32, "diff"), _stream(stream)))
+        return adj, iters, rc, oc, df
 
     def render(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
                occlusion_threshold: float = 1.0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:

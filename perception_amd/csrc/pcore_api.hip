@@ -57,6 +57,17 @@ struct pcore_ctx {
     int num_grids = 0;
     int bitmap_words = 1;
     bool have_obs = false;
+    // GICP targets: label-sorted observed points, segments [lo, hi) per label + the whole cloud
+    int num_obs = 0;
+    int max_seg = 0;
+    DevBuf<float4> tgt;
+    DevBuf<int32_t> seg_lo, seg_hi, seg_cnt;
+    DevBuf<double> tgt_cov_label, tgt_cov_all;
+    int cov_k_label = 0, cov_k_all = 0;
+    // GICP scratch
+    DevBuf<float4> icp_cloud;
+    DevBuf<int32_t> icp_count;
+    DevBuf<double> icp_cov;
     // scratch (parity stages)
     DevBuf<int32_t> scratch_counts, scratch_offsets, scratch_total;
 };
@@ -268,6 +279,9 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
     (void)dev_free(c->grids); (void)dev_free(c->cell_start); (void)dev_free(c->grid_pts);
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
+    (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt);
+    (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov);
     delete c;
 }
 
@@ -426,6 +440,36 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
         max_cnt = std::max(max_cnt, (int)pts.size());
         build_grid(pts, sensor_resolution, grids[num_labels], cell_start, gpts);
     }
+    // GICP targets (label-sorted) and their segments; covariances are computed lazily per k
+    {
+        std::vector<float4> tp(std::max(num_obs, 1));
+        for (int k2 = 0; k2 < num_obs; k2++) {
+            const int i = order[k2];
+            tp[k2] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.0f);
+        }
+        std::vector<int32_t> slo(num_labels + 1), shi(num_labels + 1), scnt(num_labels + 1);
+        int pos = 0, mx = num_obs;
+        for (int L = 0; L < num_labels; L++) {
+            while (pos < num_obs && lab[order[pos]] < L) pos++;
+            slo[L] = pos;
+            int e = pos;
+            while (e < num_obs && lab[order[e]] == L) e++;
+            shi[L] = e;
+            scnt[L] = e - pos;
+            mx = std::max(mx, e - pos);
+        }
+        slo[num_labels] = 0;
+        shi[num_labels] = num_obs;
+        scnt[num_labels] = num_obs;
+        HIPC(c, dev_upload(c->tgt, tp));
+        HIPC(c, dev_upload(c->seg_lo, slo));
+        HIPC(c, dev_upload(c->seg_hi, shi));
+        HIPC(c, dev_upload(c->seg_cnt, scnt));
+        c->num_obs = num_obs;
+        c->max_seg = mx;
+        c->cov_k_label = 0;
+        c->cov_k_all = 0;
+    }
     HIPC(c, dev_upload(c->grids, grids));
     HIPC(c, dev_upload(c->cell_start, cell_start));
     HIPC(c, dev_upload(c->grid_pts, gpts));
@@ -518,6 +562,126 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.dbg_zs = d_dbg_zs;
     HIPC(c, launch_fused_cost(a, s));
     return PCORE_OK;
+}
+
+static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& a) {
+    const int W = c->cam.width, H = c->cam.height;
+    const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
+    a = FusedArgs{};
+    a.mverts = c->mverts.p;
+    a.mtris = c->mtris.p;
+    a.meshlets = c->meshlets.p;
+    a.model_ml_lo = c->model_ml_lo.p;
+    a.model_ml_hi = c->model_ml_hi.p;
+    a.num_models = c->num_models;
+    const float* pj = c->cam.proj;
+    a.p00 = pj[0]; a.p01 = pj[1]; a.p02 = pj[2]; a.p03 = pj[3];
+    a.p10 = pj[4]; a.p11 = pj[5]; a.p12 = pj[6]; a.p13 = pj[7];
+    a.width = W;
+    a.height = H;
+    a.stride = p->stride;
+    a.ws = ws;
+    a.hs = hs;
+    a.cx = c->cam.cx; a.cy = c->cam.cy; a.fx = c->cam.fx; a.fy = c->cam.fy;
+    a.depth_factor = p->depth_factor;
+    a.src_s = c->src_s.p;
+    a.lab_s = c->lab_s.p;
+    a.grids = c->grids.p;
+    a.cell_start = c->cell_start.p;
+    a.grid_pts = c->grid_pts.p;
+    a.num_grids = c->num_grids;
+    a.bitmap_words = c->bitmap_words;
+    a.r2 = p->sensor_resolution * p->sensor_resolution;  // renderer.cu:1877
+    a.occlusion_threshold = p->occlusion_threshold;
+    a.calc_obs = p->calc_obs_cost;
+    return PCORE_OK;
+}
+
+int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
+                       const float* d_pose_obs_total, int32_t num_poses, const pcore_eval_params* p,
+                       const pcore_icp_params* ip, float* d_out_poses, int32_t* d_out_iters, float* d_out_rc,
+                       float* d_out_oc, float* d_out_diff, pcore_stream stream) {
+    if (!c || !p || !ip) return PCORE_E_INVALID_ARG;
+    if (ip->k_correspondences <= 0 || ip->k_correspondences > 16 || ip->max_iterations < 0)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: k_correspondences must be in [1, 16]");
+    if (num_poses > 0 && !d_out_poses) return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: null d_out_poses");
+    // validate everything pcore_evaluate validates, without running it
+    if (!c->have_mesh || !c->have_cam || !c->have_obs)
+        return fail(c, PCORE_E_STATE, "evaluate_icp: meshes, camera and observation must be set first");
+    if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_rc)))
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: null pose / output pointer");
+    if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: cost_type must be 0 or 2");
+    if (num_poses == 0) return PCORE_OK;
+    const bool six = p->cost_type == PCORE_COST_DEPTH_6DOF;
+    if (six && (!d_pose_label || !c->obs_has_mask))
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: cost_type 2 needs pose labels and a source mask");
+    const int W = c->cam.width;
+    if (p->stride <= 0 || W % p->stride != 0)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: width must be a multiple of stride");
+    const int ws = W / p->stride, hs = (c->cam.height + p->stride - 1) / p->stride;
+    if (fused_lds_bytes(ws, hs, c->bitmap_words) > (size_t)c->prop.sharedMemPerBlock)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: sampled z-buffer does not fit in LDS");
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_sampled(c, p->stride, s);
+    if (rc != PCORE_OK) return rc;
+    const int k = ip->k_correspondences;
+    // target covariances, once per (observation, k)
+    const int nl = c->num_grids;
+    if (six && c->cov_k_label != k) {
+        HIPC(c, dev_reserve(c->tgt_cov_label, (size_t)6 * std::max(c->num_obs, 1)));
+        HIPC(c, launch_covariances(c->tgt.p, c->seg_lo.p, c->seg_cnt.p, 0, nl, k, c->tgt_cov_label.p, s));
+        c->cov_k_label = k;
+    }
+    if (!six && c->cov_k_all != k) {
+        HIPC(c, dev_reserve(c->tgt_cov_all, (size_t)6 * std::max(c->num_obs, 1)));
+        HIPC(c, launch_covariances(c->tgt.p, c->seg_lo.p + nl, c->seg_cnt.p + nl, 0, 1, k, c->tgt_cov_all.p, s));
+        c->cov_k_all = k;
+    }
+    const int nsamp = ws * hs;
+    const int chunk = std::min(num_poses, 2048);
+    HIPC(c, dev_reserve(c->icp_cloud, (size_t)chunk * nsamp));
+    HIPC(c, dev_reserve(c->icp_count, (size_t)chunk));
+    HIPC(c, dev_reserve(c->icp_cov, (size_t)6 * chunk * nsamp));
+    FusedArgs a;
+    fill_fused_args(c, p, a);
+    GicpArgs g{};
+    g.src = c->icp_cloud.p;
+    g.src_count = c->icp_count.p;
+    g.src_cov = c->icp_cov.p;
+    g.src_cap = nsamp;
+    g.tgt = c->tgt.p;
+    g.tgt_cov = six ? c->tgt_cov_label.p : c->tgt_cov_all.p;
+    g.seg_lo = c->seg_lo.p;
+    g.seg_hi = c->seg_hi.p;
+    g.num_segs = nl;
+    g.whole_seg = nl;
+    g.pose_label = six ? d_pose_label : nullptr;
+    g.poses_in = d_poses;
+    g.poses_out = d_out_poses;
+    g.iters_out = d_out_iters;
+    g.max_iter = ip->max_iterations;
+    g.rot_eps = ip->rotation_epsilon;
+    g.trans_eps = ip->transformation_epsilon;
+    g.tgt_lds_cap = std::min(c->max_seg, 4096);
+    for (int base = 0; base < num_poses; base += chunk) {
+        const int n = std::min(chunk, num_poses - base);
+        a.poses = d_poses + (size_t)16 * base;
+        a.pose_model = d_pose_model + base;
+        a.pose_label = six ? d_pose_label + base : nullptr;
+        a.num_poses = n;
+        a.cloud_out = c->icp_cloud.p;
+        a.cloud_count = c->icp_count.p;
+        a.cloud_cap = nsamp;
+        HIPC(c, launch_render_cloud(a, s));
+        HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
+        g.pose_base = base;
+        HIPC(c, launch_gicp(g, n, s));
+    }
+    // re-render and re-score the adjusted poses (renderer.cu:1757-1907)
+    return pcore_evaluate(c, d_out_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p, d_out_rc,
+                          d_out_oc, d_out_diff, nullptr, stream);
 }
 
 int pcore_render(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,

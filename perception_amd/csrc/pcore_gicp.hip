@@ -1,0 +1,399 @@
+// pcore_gicp.hip -- per-pose GICP refinement on gfx950.
+//
+// Build-owned spec (fast_gicp is an un-vendored fork; see DESIGN.md "GICP spec"), at the reference's
+// settings (renderer.cu:1696-1705): k = 10 covariance neighbours with PLANE regularisation,
+// nearest-neighbour correspondences inside the pose's label segment, Mahalanobis (C_t + R C_s R^T)^-1,
+// Gauss-Newton on SE(3), <= 150 iterations, rotation / translation epsilons 2e-3 / 5e-4.
+// The arithmetic order -- including the reduction tree of the 6x6 normal equations -- is fixed, and
+// the CPU oracle (oracle/pcore_oracle.cpp, orc_gicp) follows the same order, so the refined transforms
+// are reproducible bit for bit.
+//
+//   covariance_kernel  one workgroup per segment (a pose's rendered cloud or an observed label):
+//                      brute-force k-NN of every point inside its segment (broadcast reads), double
+//                      mean / covariance, 6-sweep Jacobi, PLANE regularisation.
+//   gicp_kernel        one workgroup per pose: per-thread sequential partial sums of J^T M J / J^T M e,
+//                      wave shuffle-down tree, 4 wave partials in order, one-lane 6x6 LDLT and update,
+//                      target segment staged in LDS, then concatenate_transforms (renderer.cu:1412-1429).
+#include "pcore_internal.h"
+
+#include <climits>
+#include <cfloat>
+
+#pragma clang fp contract(off)
+
+namespace pcore {
+
+namespace {
+
+constexpr int kGThreads = 256;
+constexpr int kGWaves = kGThreads / 64;
+constexpr int kMaxK = 16;
+constexpr double kPlaneScale = 1.0 - 1e-3;
+
+__device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
+    const float dx = ax - bx, dy = ay - by, dz = az - bz;
+    return dx * dx + dy * dy + dz * dz;
+}
+
+// Jacobi (6 cyclic sweeps) + PLANE regularisation, same operation order as orc plane_regularize.
+__device__ void plane_regularize(const double c[6], double out[6]) {
+    double A[3][3] = {{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}};
+    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+#pragma unroll 1
+    for (int sweep = 0; sweep < 6; sweep++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const int p = r < 2 ? 0 : 1, q = r == 0 ? 1 : 2, o = 3 - p - q;
+            const double apq = A[p][q];
+            if (apq == 0.0) continue;
+            const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+            if (theta < 0.0) t = -t;
+            const double cc = 1.0 / sqrt(t * t + 1.0);
+            const double ss = t * cc;
+            const double app = A[p][p], aqq = A[q][q];
+            A[p][p] = app - t * apq;
+            A[q][q] = aqq + t * apq;
+            A[p][q] = 0.0;
+            A[q][p] = 0.0;
+            const double aop = A[o][p], aoq = A[o][q];
+            A[o][p] = cc * aop - ss * aoq;
+            A[p][o] = A[o][p];
+            A[o][q] = ss * aop + cc * aoq;
+            A[q][o] = A[o][q];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const double vkp = V[k][p], vkq = V[k][q];
+                V[k][p] = cc * vkp - ss * vkq;
+                V[k][q] = ss * vkp + cc * vkq;
+            }
+        }
+    int m = 0;
+    if (A[1][1] < A[m][m]) m = 1;
+    if (A[2][2] < A[m][m]) m = 2;
+    const double n0 = V[0][m], n1 = V[1][m], n2 = V[2][m];
+    out[0] = 1.0 - kPlaneScale * (n0 * n0);
+    out[1] = 0.0 - kPlaneScale * (n0 * n1);
+    out[2] = 0.0 - kPlaneScale * (n0 * n2);
+    out[3] = 1.0 - kPlaneScale * (n1 * n1);
+    out[4] = 0.0 - kPlaneScale * (n1 * n2);
+    out[5] = 1.0 - kPlaneScale * (n2 * n2);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// covariances
+// ------------------------------------------------------------------------------------------------
+template <int KMAX>
+__global__ void __launch_bounds__(kGThreads) covariance_kernel(const float4* pts, const int32_t* seg_off,
+                                                               const int32_t* seg_cnt, int seg_stride, int k,
+                                                               double* cov_out) {
+    const int sg = blockIdx.x;
+    const int off = seg_off ? seg_off[sg] : sg * seg_stride;
+    const int n = seg_cnt[sg];
+    const float4* P = pts + off;
+    double* C = cov_out + (size_t)6 * off;
+    for (int i = threadIdx.x; i < n; i += kGThreads) {
+        const float4 xi = P[i];
+        float nd[KMAX];
+        int nb[KMAX];
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) { nd[q] = 0.0f; nb[q] = 0; }
+        int cnt = 0;
+        for (int j = 0; j < n; j++) {
+            const float4 xj = P[j];
+            const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
+            // insertion identical to orc knn_self: new element starts at pos and bubbles down past
+            // entries with a strictly larger distance
+            int pos;
+            if (cnt < k) pos = cnt;
+            else if (d < nd[k - 1]) pos = k - 1;
+            else continue;
+            int c = 0;
+#pragma unroll
+            for (int q = 0; q < KMAX; q++) c += (q < pos && nd[q] > d) ? 1 : 0;
+            const int fin = pos - c;
+#pragma unroll
+            for (int q = KMAX - 1; q >= 1; q--)
+                if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
+#pragma unroll
+            for (int q = 0; q < KMAX; q++)
+                if (q == fin) { nd[q] = d; nb[q] = j; }
+            if (cnt < k) cnt++;
+        }
+        double mx = 0.0, my = 0.0, mz = 0.0;
+#pragma unroll
+        for (int q = 0; q < KMAX; q++)
+            if (q < cnt) {
+                const float4 p = P[nb[q]];
+                mx += (double)p.x; my += (double)p.y; mz += (double)p.z;
+            }
+        const double kd = (double)cnt;
+        mx = mx / kd; my = my / kd; mz = mz / kd;
+        double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < KMAX; q++)
+            if (q < cnt) {
+                const float4 p = P[nb[q]];
+                const double dx = (double)p.x - mx, dy = (double)p.y - my, dz = (double)p.z - mz;
+                c6[0] += dx * dx; c6[1] += dx * dy; c6[2] += dx * dz;
+                c6[3] += dy * dy; c6[4] += dy * dz; c6[5] += dz * dz;
+            }
+#pragma unroll
+        for (int e = 0; e < 6; e++) c6[e] = c6[e] / kd;
+        double r6[6];
+        plane_regularize(c6, r6);
+#pragma unroll
+        for (int e = 0; e < 6; e++) C[(size_t)6 * i + e] = r6[e];
+    }
+}
+
+hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const int32_t* seg_cnt, int seg_stride,
+                              int num_segs, int k, double* cov_out, hipStream_t s) {
+    if (num_segs <= 0) return hipSuccess;
+    if (k <= 0 || k > kMaxK) return hipErrorInvalidValue;
+    if (k <= 10)
+        hipLaunchKernelGGL(covariance_kernel<10>, dim3(num_segs), dim3(kGThreads), 0, s, pts, seg_off, seg_cnt,
+                           seg_stride, k, cov_out);
+    else
+        hipLaunchKernelGGL(covariance_kernel<kMaxK>, dim3(num_segs), dim3(kGThreads), 0, s, pts, seg_off, seg_cnt,
+                           seg_stride, k, cov_out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// GICP
+// ------------------------------------------------------------------------------------------------
+
+// One point's Gauss-Newton contribution (orc gicp_contrib): acc[0..20] upper(H), [21..26] b, [27] error.
+__device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&t)[3], float4 s,
+                                             const double* cs, const float4* tgt, const double* tcov, int nt,
+                                             double (&acc)[28]) {
+    const double s0 = (double)s.x, s1 = (double)s.y, s2 = (double)s.z;
+    double q[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
+    const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
+    int j = -1;
+    float best = INFINITY;
+    for (int o = 0; o < nt; o++) {
+        const float4 p = tgt[o];
+        const float d = sqdist3(qx, qy, qz, p.x, p.y, p.z);
+        if (d < best) { best = d; j = o; }
+    }
+    if (j < 0) return;
+    const double* ct = tcov + (size_t)6 * j;
+    const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
+    const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
+    double RC[3][3], A[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) RC[r][c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) A[r][c] = Ct[r][c] + (RC[r][0] * R[c][0] + RC[r][1] * R[c][1] + RC[r][2] * R[c][2]);
+    double m[3][3];
+    m[0][0] = A[1][1] * A[2][2] - A[1][2] * A[2][1];
+    m[0][1] = A[0][2] * A[2][1] - A[0][1] * A[2][2];
+    m[0][2] = A[0][1] * A[1][2] - A[0][2] * A[1][1];
+    m[1][0] = A[1][2] * A[2][0] - A[1][0] * A[2][2];
+    m[1][1] = A[0][0] * A[2][2] - A[0][2] * A[2][0];
+    m[1][2] = A[0][2] * A[1][0] - A[0][0] * A[1][2];
+    m[2][0] = A[1][0] * A[2][1] - A[1][1] * A[2][0];
+    m[2][1] = A[0][1] * A[2][0] - A[0][0] * A[2][1];
+    m[2][2] = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+    const double det = A[0][0] * m[0][0] + A[0][1] * m[1][0] + A[0][2] * m[2][0];
+    const double inv = 1.0 / det;
+    double M[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
+    const float4 tj = tgt[j];
+    const double e[3] = {(double)tj.x - q[0], (double)tj.y - q[1], (double)tj.z - q[2]};
+    const double J[3][6] = {{0.0, -q[2], q[1], -1.0, 0.0, 0.0},
+                            {q[2], 0.0, -q[0], 0.0, -1.0, 0.0},
+                            {-q[1], q[0], 0.0, 0.0, 0.0, -1.0}};
+    double MJ[3][6];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 6; c++) MJ[r][c] = M[r][0] * J[0][c] + M[r][1] * J[1][c] + M[r][2] * J[2][c];
+    int h = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+        for (int b = a; b < 6; b++) { acc[h] += J[0][a] * MJ[0][b] + J[1][a] * MJ[1][b] + J[2][a] * MJ[2][b]; h++; }
+    double Me[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) Me[r] = M[r][0] * e[0] + M[r][1] * e[1] + M[r][2] * e[2];
+#pragma unroll
+    for (int a = 0; a < 6; a++) acc[21 + a] += J[0][a] * Me[0] + J[1][a] * Me[1] + J[2][a] * Me[2];
+    acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+}
+
+// 6x6 LDLT without pivoting (orc ldlt_solve6).  Single lane.
+__device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
+    double H[6][6];
+    int h = 0;
+    for (int a = 0; a < 6; a++)
+        for (int c = a; c < 6; c++) { H[a][c] = Hu[h]; H[c][a] = Hu[h]; h++; }
+    double L[6][6], D[6];
+    for (int a = 0; a < 6; a++)
+        for (int c = 0; c < 6; c++) L[a][c] = 0.0;
+    for (int j = 0; j < 6; j++) {
+        double v = H[j][j];
+        for (int k = 0; k < j; k++) v = v - L[j][k] * L[j][k] * D[k];
+        if (!(v > 0.0) || !isfinite(v)) return false;
+        D[j] = v;
+        for (int i = j + 1; i < 6; i++) {
+            double w = H[i][j];
+            for (int k = 0; k < j; k++) w = w - L[i][k] * L[j][k] * D[k];
+            L[i][j] = w / D[j];
+        }
+    }
+    double y[6];
+    for (int i = 0; i < 6; i++) {
+        double v = -b[i];
+        for (int k = 0; k < i; k++) v = v - L[i][k] * y[k];
+        y[i] = v;
+    }
+    for (int i = 5; i >= 0; i--) {
+        double v = y[i] / D[i];
+        for (int k = i + 1; k < 6; k++) v = v - L[k][i] * d[k];
+        d[i] = v;
+    }
+    for (int i = 0; i < 6; i++)
+        if (!isfinite(d[i])) return false;
+    return true;
+}
+
+__global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_g[];
+    __shared__ double sR[9], sT[3];
+    __shared__ double wpart[kGWaves][28];
+    __shared__ int s_done, s_iters;
+    const int pose = blockIdx.x;  // chunk-local
+    const int gp = g.pose_base + pose;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int ns = g.src_count[pose];
+    const float4* src = g.src + (size_t)pose * g.src_cap;
+    const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
+    int seg = g.whole_seg;
+    if (g.pose_label) {
+        const int pl = g.pose_label[gp];
+        seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
+    }
+    const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
+    const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
+    const double* tcov = g.tgt_cov + (size_t)6 * lo;
+    const float4* tgt = g.tgt + lo;
+    if (nt <= g.tgt_lds_cap) {  // stage the target segment in LDS (broadcast reads in the NN loop)
+        float4* tl = reinterpret_cast<float4*>(smem_g);
+        for (int i = tid; i < nt; i += kGThreads) tl[i] = tgt[i];
+        tgt = tl;
+    }
+    if (tid == 0) {
+        for (int i = 0; i < 9; i++) sR[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        sT[0] = sT[1] = sT[2] = 0.0;
+        s_done = (ns <= 0 || nt <= 0) ? 1 : 0;
+        s_iters = 0;
+    }
+    __syncthreads();
+    for (int it = 0; it < g.max_iter; it++) {
+        if (s_done) break;
+        double R[3][3], t[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) R[r][c] = sR[3 * r + c];
+            t[r] = sT[r];
+        }
+        double acc[28];
+#pragma unroll
+        for (int v = 0; v < 28; v++) acc[v] = 0.0;
+        for (int i = tid; i < ns; i += kGThreads) gicp_contrib(R, t, src[i], scov + (size_t)6 * i, tgt, tcov, nt, acc);
+        // fixed-order reduction: shuffle-down tree to lane 0 of each wave
+#pragma unroll
+        for (int v = 0; v < 28; v++) {
+            double x = acc[v];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
+            if (lane == 0) wpart[wave][v] = x;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double tot[28];
+            for (int v = 0; v < 28; v++) {
+                double sum = wpart[0][v];
+                for (int w = 1; w < kGWaves; w++) sum = sum + wpart[w][v];
+                tot[v] = sum;
+            }
+            double d[6];
+            if (!ldlt_solve6(tot, tot + 21, d)) {
+                s_done = 1;
+            } else {
+                s_iters = s_iters + 1;
+                double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
+                const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+                const double inv = 1.0 / nrm;
+                qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
+                const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
+                const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
+                const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
+                                         {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
+                                         {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
+                double Rn[3][3], tn[3];
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++)
+                        Rn[r][c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
+                    tn[r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
+                }
+                double dr = 0.0, dt = 0.0;
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++) {
+                        const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
+                        dr = v > dr ? v : dr;
+                    }
+                    const double v = fabs(d[3 + r]);
+                    dt = v > dt ? v : dt;
+                }
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++) sR[3 * r + c] = Rn[r][c];
+                    sT[r] = tn[r];
+                }
+                if (dr < g.rot_eps && dt < g.trans_eps) s_done = 1;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        // concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
+        const float* pin = g.poses_in + (size_t)16 * gp;
+        float A[4][4], Tf[4][4];
+        for (int r = 0; r < 4; r++)
+            for (int c = 0; c < 4; c++) {
+                A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
+                Tf[r][c] = r < 3 ? (float)(c < 3 ? sR[3 * r + c] : sT[r]) : (c == 3 ? 1.0f : 0.0f);
+            }
+        float* pout = g.poses_out + (size_t)16 * gp;
+        for (int r = 0; r < 4; r++)
+            for (int c = 0; c < 4; c++) {
+                const float p = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
+                pout[4 * r + c] = r < 3 ? (float)((double)p * 100) : p;
+            }
+        if (g.iters_out) g.iters_out[gp] = s_iters;
+    }
+}
+
+hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
+    if (num_poses <= 0) return hipSuccess;
+    const size_t lds = (size_t)g.tgt_lds_cap * sizeof(float4);
+    hipLaunchKernelGGL(gicp_kernel, dim3(num_poses), dim3(kGThreads), lds, s, g);
+    return hipGetLastError();
+}
+
+}  // namespace pcore

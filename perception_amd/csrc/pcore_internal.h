@@ -64,9 +64,39 @@ struct FusedArgs {
     float* out_oc;
     float* out_diff;
     int32_t* dbg_zs;
+    // stage CLOUD-into-scratch (GICP input): per-pose slots of `cloud_cap` points
+    float4* cloud_out;
+    int32_t* cloud_count;
+    int32_t cloud_cap;
+};
+
+// GICP over a chunk of poses (pcore_kernels.hip, gicp_kernel)
+struct GicpArgs {
+    const float4* src;        // chunk-local per-pose slots: src + pose * src_cap
+    const int32_t* src_count;
+    const double* src_cov;    // 6 per source point, same slots
+    int32_t src_cap;
+    const float4* tgt;        // observed points, label-sorted
+    const double* tgt_cov;    // 6 per target point (covariances within the segment)
+    const int32_t* seg_lo;    // num_segs entries
+    const int32_t* seg_hi;
+    int32_t num_segs;
+    int32_t whole_seg;        // segment used when pose_label == nullptr (3-DoF)
+    const int32_t* pose_label;  // batch-global, nullable
+    const float* poses_in;    // batch-global N x 16
+    float* poses_out;         // batch-global N x 16
+    int32_t* iters_out;       // batch-global, nullable
+    int32_t pose_base;        // first batch index of this chunk
+    int32_t max_iter;
+    double rot_eps, trans_eps;
+    int32_t tgt_lds_cap;      // targets staged in LDS when the segment has <= this many points
 };
 
 // launchers (pcore_kernels.hip)
+hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s);
+hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const int32_t* seg_cnt, int seg_stride,
+                              int num_segs, int k, double* cov_out, hipStream_t s);
+hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s);
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
 size_t fused_lds_bytes(int ws, int hs, int bitmap_words);
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,

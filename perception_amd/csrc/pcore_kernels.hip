@@ -197,41 +197,34 @@ size_t fused_lds_bytes(int ws, int hs, int bitmap_words) {
     return b;
 }
 
+__device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsamp, int bitmap_words) {
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    FusedSmem sm;
+    unsigned char* p = smem_raw;
+    sm.zbuf = (int32_t*)p; p += al((size_t)nsamp * 4);
+    sm.vx = (float*)p; p += al((size_t)kWaves * kWave * 4);
+    sm.vy = (float*)p; p += al((size_t)kWaves * kWave * 4);
+    sm.vz = (float*)p; p += al((size_t)kWaves * kWave * 4);
+    sm.ring = (TriRec*)p; p += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+    sm.bitmap = (uint32_t*)p; p += al((size_t)bitmap_words * 4);
+    sm.counters = (int32_t*)p;
+    return sm;
+}
+
 template <int STRIDE>
-__global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int pose = blockIdx.x;
+__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose) {
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
+    (void)tid;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
-    const int W = a.width, H = a.height, ws = a.ws, hs = a.hs;
-    const int nsamp = ws * hs;
-
-    FusedSmem sm;
-    {
-        auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-        unsigned char* p = smem_raw;
-        sm.zbuf = (int32_t*)p; p += al((size_t)nsamp * 4);
-        sm.vx = (float*)p; p += al((size_t)kWaves * kWave * 4);
-        sm.vy = (float*)p; p += al((size_t)kWaves * kWave * 4);
-        sm.vz = (float*)p; p += al((size_t)kWaves * kWave * 4);
-        sm.ring = (TriRec*)p; p += al((size_t)kWaves * kRecCap * sizeof(TriRec));
-        sm.bitmap = (uint32_t*)p; p += al((size_t)a.bitmap_words * 4);
-        sm.counters = (int32_t*)p;
-    }
-    for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
-    for (int i = tid; i < a.bitmap_words; i += kThreads) sm.bitmap[i] = 0u;
-    if (tid < 4) sm.counters[tid] = 0;
-
+    const int W = a.width, H = a.height, ws = a.ws;
     // pose (wave-uniform -> scalar loads)
     const float* P = a.poses + (size_t)16 * pose;
     const float m00 = P[0], m01 = P[1], m02 = P[2], m03 = P[3];
     const float m10 = P[4], m11 = P[5], m12 = P[6], m13 = P[7];
     const float m20 = P[8], m21 = P[9], m22 = P[10], m23 = P[11];
     const int model = a.pose_model[pose];
-    const bool use_seg = a.pose_label != nullptr;
-    const int32_t pl = use_seg ? a.pose_label[pose] : 0;
     __syncthreads();
 
     // ---------------- phase 1: raster of the sampled pixels ----------------
@@ -342,6 +335,27 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
         if (rec_count > 0) flush(rec_count);
     }
     __syncthreads();
+}
+
+template <int STRIDE>
+__global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int pose = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    const int s = STRIDE > 0 ? STRIDE : a.stride;
+    const int W = a.width, H = a.height, ws = a.ws, hs = a.hs;
+    const int nsamp = ws * hs;
+
+    const FusedSmem sm = carve_smem(smem_raw, nsamp, a.bitmap_words);
+    for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
+    for (int i = tid; i < a.bitmap_words; i += kThreads) sm.bitmap[i] = 0u;
+    if (tid < 4) sm.counters[tid] = 0;
+
+    const bool use_seg = a.pose_label != nullptr;
+    const int32_t pl = use_seg ? a.pose_label[pose] : 0;
+    raster_phase<STRIDE>(a, sm, pose);
 
     // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
     int32_t* queue = reinterpret_cast<int32_t*>(sm.ring) + wave * (kRecCap * (int)sizeof(TriRec) / 4);
@@ -459,6 +473,65 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
             if (a.out_diff) a.out_diff[pose] = 0.0f;
         }
     }
+}
+
+// Stage CLOUD into per-pose scratch slots (the GICP source clouds): sampled raster, source occlusion,
+// then the reference's compaction order (row-major samples, compute_point_clouds.cuh:290-346).
+template <int STRIDE>
+__global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    __shared__ int wsum[kWaves];
+    __shared__ int carry_s;
+    const int pose = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int s = STRIDE > 0 ? STRIDE : a.stride;
+    const int ws = a.ws, nsamp = a.ws * a.hs;
+    const FusedSmem sm = carve_smem(smem_raw, nsamp, 0);
+    for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
+    if (tid == 0) carry_s = 0;
+    const bool use_seg = a.pose_label != nullptr;
+    const int32_t pl = use_seg ? a.pose_label[pose] : 0;
+    raster_phase<STRIDE>(a, sm, pose);
+    float4* out = a.cloud_out + (size_t)pose * a.cloud_cap;
+    for (int base = 0; base < nsamp; base += kThreads) {
+        const int k = base + tid;
+        int32_t zf = 0;
+        if (k < nsamp)
+            zf = occlusion_rule(sm.zbuf[k], a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg, pl,
+                                a.occlusion_threshold);
+        const bool valid = zf > 0;
+        const uint64_t b = __ballot(valid);
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int woff = 0, tot = 0;
+        for (int w = 0; w < kWaves; w++) {
+            if (w < wave) woff += wsum[w];
+            tot += wsum[w];
+        }
+        const int carry = carry_s;
+        if (valid) {
+            const int o = carry + woff + mbcnt64(b);
+            const int ky = k / ws, kx = k - ky * ws;
+            const float zp = (float)zf / a.depth_factor;
+            const float xp = ((float)(kx * s) - a.cx) / a.fx * zp;
+            const float yp = ((float)(ky * s) - a.cy) / a.fy * zp;
+            if (o < a.cloud_cap) out[o] = make_float4(xp, yp, zp, 0.0f);
+        }
+        __syncthreads();
+        if (tid == 0) carry_s = carry + tot;
+        __syncthreads();
+    }
+    if (tid == 0) a.cloud_count[pose] = carry_s < a.cloud_cap ? carry_s : a.cloud_cap;
+}
+
+hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
+    const size_t lds = fused_lds_bytes(a.ws, a.hs, 0);
+    if (a.num_poses <= 0) return hipSuccess;
+    if (a.stride == 8)
+        hipLaunchKernelGGL(render_cloud_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL(render_cloud_kernel<0>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s) {

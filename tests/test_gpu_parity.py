@@ -238,3 +238,54 @@ def test_gpu_reproduces_committed_fixture(name):
     assert _bits_equal(df.cpu().numpy(), g["diff"])
     cost, idx = decode_keys(core.select(rc, oc, pm, K))
     assert np.array_equal(cost, g["best_cost"]) and np.array_equal(idx, g["best_index"])
+
+
+def _label_covs(case, six=True):
+    cov = np.zeros((len(case.obs_xyz), 6))
+    if six:
+        for L in range(len(case.label_start)):
+            a, b = case.label_start[L], case.label_end[L]
+            if b > a:
+                cov[a:b] = oracle.covariances(case.obs_xyz[a:b])
+    else:
+        cov = oracle.covariances(case.obs_xyz)
+    return cov
+
+
+@pytest.mark.parametrize("fixture", ["one_object", "three_objects"])
+def test_evaluate_icp_matches_oracle(fixture, request):
+    case, core, t = request.getfixturevalue(fixture)
+    sc = case.scene
+    n = min(48, len(case.poses))
+    adj, iters, rc, oc, df = core.evaluate_icp(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n],
+                                               cost_type=2, stride=case.stride)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n], case.pose_label[:n],
+        sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy,
+        100.0, case.obs_xyz, _label_covs(case), case.label_start, case.label_end, case.pose_obs_total[:n], 2, True,
+        0.01)
+    adj = adj.cpu().numpy()
+    # GICP transform within 1e-4 (north_star); the build-owned spec is in fact bit-reproducible
+    assert np.abs(adj - oadj).max() <= 1e-4 * 100, np.abs(adj - oadj).max()
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj, oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+
+
+def test_evaluate_icp_3dof_matches_oracle(one_object):
+    case, core, t = one_object
+    sc = case.scene
+    n = 24
+    tot = np.full(n, len(case.obs_xyz), np.float32)
+    adj, iters, rc, oc, df = core.evaluate_icp(t["poses"][:n], t["pm"][:n], None,
+                                               torch.from_numpy(tot).to(t["poses"].device), cost_type=0,
+                                               stride=case.stride)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n], None, sc.width, sc.height,
+        sc.proj, sc.src_depth_cm, None, 1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz,
+        _label_covs(case, six=False), None, None, tot, 0, True, 0.01)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
