@@ -1,0 +1,346 @@
+"""Host orchestration of the GPU greedy-render search: the ObjectRecognizer / EnvObjectRecognition path
+that the reference drives through perch_fat (SURVEY.md 8b "secondary seams", build plan step 7).
+
+Mirrors, on top of PoseCore (the C ABI):
+  ObjectRecognizer::SetStaticInput / LocalizeObjectsGreedyRender   object_recognizer.cpp:285-342
+  EnvObjectRecognition::SetInput (6-DoF images)                     search_env.cpp:5862-6060
+  EnvObjectRecognition::ComputeGreedyRenderPoses                    search_env.cpp:2462-2651
+  EnvObjectRecognition::GenerateSuccessorStates (pose lists)        search_env.cpp:7056-7254, IsValidPose 309-528
+  EnvObjectRecognition::ComputeGreedyCostsInParallelGPU             search_env.cpp:1782-2052
+  EnvObjectRecognition::GetStateImagesUnifiedGPU (pose building)    search_env.cpp:1505-1717
+and writes perch_fat's output_poses.txt / output_stats.txt (perch_fat.cpp:302-323).
+
+Multi-GPU: with torch.distributed initialised, every rank evaluates a contiguous shard of the candidate
+list; the per-model selection keys meet in ONE all-reduce(MIN) and the winning adjusted poses in one
+all-reduce(SUM) of a num_models x 16 tensor that only the owning ranks fill.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from . import io as pio
+from ._native import COST_DEPTH_6DOF, ICP_K, ICP_MAX_ITER, ICP_ROT_EPS, ICP_TRANS_EPS, PCORE_KEY_NONE
+from .core import PoseCore, decode_keys
+from .distributed import allreduce_min_keys, shard_range
+from .model import Model, compute_proj, init_from_eigen_batch, matrix_to_quat_xyzw, pose_matrix, to_eigen
+
+# cam_to_body (search_env.cpp:1536-1539)
+CAM_TO_BODY = np.array([[0, 0, 1, 0], [-1, 0, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1]], np.float64)
+K_MESH_ADDITIVE_INFLATION = 0.01  # object_model.cpp:43
+
+
+@dataclass
+class PerchParams:
+    """perch_params of sbpl_perception/config/pr3_env_config.yaml (6-DoF GPU settings) + defaults of
+    search_env.cpp:153-188."""
+    icp_type: int = 3                        # 3 = GICP inside the GPU flow
+    sensor_resolution: float = 0.01          # sensor_resolution_radius (m)
+    min_neighbor_points_for_valid_pose: int = 30
+    gpu_batch_size: int = 700
+    gpu_stride: int = 8
+    gpu_occlusion_threshold: float = 1.0     # cm (search_env.cpp:185)
+    gpu_depth_factor: int = 100              # search_env.h:411
+    use_color_cost: bool = False
+    color_distance_threshold: float = 15.0
+    # fast_gicp settings hard-coded at renderer.cu:1696-1699
+    icp_k: int = ICP_K
+    icp_max_iterations: int = ICP_MAX_ITER
+    icp_rotation_epsilon: float = ICP_ROT_EPS
+    icp_transformation_epsilon: float = ICP_TRANS_EPS
+
+
+@dataclass
+class CameraIntrinsics:
+    width: int
+    height: int
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+
+
+@dataclass
+class ModelMetaData:
+    """utils.h:82-103 (name, file, flipped, symmetric, ...); `model` may be given instead of `file`."""
+    name: str
+    file: Optional[str] = None
+    model: Optional[Model] = None
+    flipped: bool = False
+    symmetric: bool = False
+    mesh_in_mm: bool = False
+    mesh_scaling_factor: float = 1.0
+
+
+@dataclass
+class RecognitionInput:
+    """utils.h:43-80, the fields the 6-DoF GPU path reads."""
+    model_names: List[str]
+    input_depth_image: Union[str, np.ndarray]          # 16-bit depth (path or (H,W) array)
+    predicted_mask_image: Union[str, np.ndarray]       # labels 1..K in model_names order, 0 = background
+    depth_factor: float = 10000.0
+    camera_pose: np.ndarray = field(default_factory=lambda: np.linalg.inv(CAM_TO_BODY))
+    rendered_root_dir: Optional[str] = None             # <root>/<model>/poses.txt
+    pose_lists: Optional[Dict[str, np.ndarray]] = None  # alternative: name -> (N, 7) x y z qx qy qz qw
+    use_external_pose_list: int = 1
+    use_icp: int = 1
+
+
+@dataclass
+class EnvStats:
+    """utils.h:114-120."""
+    scenes_rendered: int = 0
+    scenes_valid: int = 0
+    time: float = 0.0
+    icp_time: float = 0.0
+    peak_gpu_mem: float = 0.0
+
+
+@dataclass
+class LocalizationResult:
+    object_transforms: List[np.ndarray]
+    preprocessing_transforms: List[np.ndarray]
+    detected_poses: List[np.ndarray]     # (7,) x y z qx qy qz qw (ContPose)
+    model_names: List[str]
+    costs: List[int]
+    indices: List[int]
+    stats: EnvStats
+
+
+def preprocessing_transform(model: Model, flipped: bool = False, mesh_in_mm: bool = False,
+                            scale: float = 1.0, six_dof: bool = True) -> np.ndarray:
+    """PreprocessModel (object_model.cpp:49-132): translate by -centroid (z: centroid for 6-DoF, min z
+    otherwise) of the mesh vertices, optional scale and z flip; returns the 4x4 (float32 precision)."""
+    v = model.vertices().astype(np.float64)
+    c = v.mean(0) if len(v) else np.zeros(3)
+    flip = np.eye(4)
+    if flipped:
+        flip[2, 2] = -1
+        v = v * np.array([1, 1, -1])
+    z = c[2] if six_dof else (v[:, 2].min() if len(v) else 0.0)
+    s = scale if mesh_in_mm else 1.0
+    T = np.eye(4)
+    T[:3, :3] *= s
+    T[:3, 3] = -np.array([c[0] * s, c[1] * s, z * s])
+    return (T @ flip).astype(np.float32).astype(np.float64)
+
+
+def _dims(model: Model):
+    v = model.vertices()
+    if len(v) == 0:
+        return np.zeros(3)
+    return v.max(0) - v.min(0)
+
+
+class ObjectRecognizer:
+    """ObjectRecognizer + EnvObjectRecognition for the greedy GPU search, driven by PoseCore."""
+
+    def __init__(self, model_bank: Dict[str, ModelMetaData], camera: CameraIntrinsics,
+                 params: Optional[PerchParams] = None, device: int = 0):
+        self.bank = model_bank
+        self.cam = camera
+        self.params = params or PerchParams()
+        self.device = torch.device("cuda", device)
+        self.core = PoseCore(device)
+        self.proj = compute_proj(camera.fx, camera.fy, camera.cx, camera.cy, camera.width, camera.height)
+        self.core.set_camera(camera.width, camera.height, camera.fx, camera.fy, camera.cx, camera.cy, self.proj)
+        self.models: List[Model] = []
+        self.model_names: List[str] = []
+        self.preprocess: List[np.ndarray] = []
+        self.last_stats = EnvStats()
+
+    # -- ObjectRecognizer::SetStaticInput -> LoadObjFiles (search_env.cpp:253-307) -----------------
+    def set_static_input(self, model_names: Sequence[str], six_dof: bool = True):
+        self.models, self.preprocess, self.model_names = [], [], list(model_names)
+        for name in model_names:
+            meta = self.bank[name]
+            m = meta.model if meta.model is not None else pio.load_ply(meta.file, name)
+            self.models.append(m)
+            self.preprocess.append(preprocessing_transform(m, meta.flipped, meta.mesh_in_mm,
+                                                           meta.mesh_scaling_factor, six_dof))
+        tris = np.concatenate([m.tris for m in self.models])
+        colors = np.concatenate([m.colors for m in self.models])
+        self.core.upload_meshes(tris, [m.num_tris for m in self.models], colors)
+
+    # -- SetInput (search_env.cpp:5862-6060), 6-DoF images ------------------------------------------
+    def set_input(self, inp: RecognitionInput):
+        depth = inp.input_depth_image
+        depth = pio.load_depth_png(depth) if isinstance(depth, str) else np.asarray(depth, np.int32)
+        mask = inp.predicted_mask_image
+        mask = pio.load_mask_png(mask) if isinstance(mask, str) else np.asarray(mask, np.uint8)
+        if depth.shape != (self.cam.height, self.cam.width) or mask.shape != depth.shape:
+            raise ValueError("depth / mask size does not match the camera")
+        p = self.params
+        self.camera_pose = np.asarray(inp.camera_pose, np.float64)
+        d_depth = torch.from_numpy(np.ascontiguousarray(depth, np.int32)).to(self.device)
+        d_mask = torch.from_numpy(np.ascontiguousarray(mask)).to(self.device)
+        # depth2cloud_global with the label mask (search_env.cpp:5993-6017)
+        self.obs_xyz, self.obs_label = self.core.observed_cloud(d_depth, d_mask, p.gpu_stride, inp.depth_factor)
+        lab = self.obs_label.cpu().numpy()
+        self.obs_xyz_host = self.obs_xyz.cpu().numpy()
+        self.obs_label_host = lab
+        K = len(inp.model_names)
+        # segmented_observed_point_count (search_env.cpp:6024-6059)
+        self.segmented_count = np.bincount(lab[lab >= 0], minlength=K).astype(np.float32)[:max(K, 1)]
+        # source depth in gpu cm units: int32 /= (depth_factor / gpu_depth_factor) (search_env.cpp:2487-2498)
+        div = np.float32(inp.depth_factor) / np.float32(p.gpu_depth_factor)
+        src_cm = (depth.astype(np.float32) / div).astype(np.int32)
+        self.core.set_observation(torch.from_numpy(src_cm).to(self.device), d_mask, self.obs_xyz, self.obs_label,
+                                  p.sensor_resolution)
+        self.segmented_object_names = list(inp.model_names)
+
+    # -- GenerateSuccessorStates (search_env.cpp:7056-7254) ----------------------------------------
+    def _valid_pose_mask(self, model_id: int, translations: np.ndarray, required_object_id: int) -> np.ndarray:
+        """IsValidPose (search_env.cpp:309-410), 6-DoF branch: at least min_neighbor_points_for_valid_pose
+        points of the object's segmented observed cloud within inflation * circumscribed_radius_3d."""
+        dims = _dims(self.models[model_id])
+        circ3d = float(max(dims)) / 2.0  # GetCircumscribedRadius3D, object_model.cpp:464-466
+        inscribed = float(min(dims[0], dims[1])) / 2.0
+        infl = 1.0 + K_MESH_ADDITIVE_INFLATION / inscribed if inscribed > 0 else 1.0  # object_model.cpp:381-383
+        rad = infl * circ3d
+        seg = self.obs_xyz_host[self.obs_label_host == required_object_id].astype(np.float64)
+        need = self.params.min_neighbor_points_for_valid_pose
+        if len(seg) < need:
+            return np.zeros(len(translations), bool)
+        out = np.zeros(len(translations), bool)
+        for a in range(0, len(translations), 4096):
+            t = translations[a:a + 4096]
+            d2 = ((t[:, None, :] - seg[None, :, :]) ** 2).sum(-1)
+            out[a:a + 4096] = (d2 <= rad * rad).sum(1) >= need
+        return out
+
+    def generate_successor_states(self, inp: RecognitionInput):
+        states = []  # (model_id, required_object_id, (7,) pose)
+        for ii, name in enumerate(self.model_names):
+            if inp.pose_lists is not None and name in inp.pose_lists:
+                P = np.asarray(inp.pose_lists[name], np.float64).reshape(-1, 7)
+            elif inp.rendered_root_dir is not None:
+                path = os.path.join(inp.rendered_root_dir, name, "poses.txt")
+                P = pio.read_poses_txt(path) if os.path.exists(path) else np.zeros((0, 7))
+            else:
+                P = np.zeros((0, 7))
+            req = self.segmented_object_names.index(name) if name in self.segmented_object_names else \
+                len(self.segmented_object_names)
+            ok = self._valid_pose_mask(ii, P[:, :3], req) if len(P) else np.zeros(0, bool)
+            for p in P[ok]:
+                states.append((ii, req, p))
+        return states
+
+    def _pose_in_cam(self, states) -> np.ndarray:
+        """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576)."""
+        cam_z_front = self.camera_pose @ CAM_TO_BODY
+        cam_matrix = np.linalg.inv(cam_z_front)
+        mats = np.empty((len(states), 4, 4))
+        for i, (mid, _, p) in enumerate(states):
+            mats[i] = cam_matrix @ pose_matrix(p[:3], p[3:7]) @ self.preprocess[mid]
+        return init_from_eigen_batch(mats, 100)
+
+    # -- ComputeGreedyRenderPoses (search_env.cpp:2462-2651) ----------------------------------------
+    def compute_greedy_render_poses(self, inp: RecognitionInput):
+        t0 = time.perf_counter()
+        p = self.params
+        states = self.generate_successor_states(inp)
+        n_total = len(states)
+        K = len(self.models)
+        world, rank = 1, 0
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
+        lo, hi = shard_range(n_total, rank, world)
+        mine = states[lo:hi]
+        keys = torch.full((K,), PCORE_KEY_NONE, dtype=torch.int64, device=self.device)
+        adj_all = None
+        icp_time = 0.0
+        if mine:
+            poses = torch.from_numpy(self._pose_in_cam(mine)).to(self.device)
+            pm = torch.tensor([s[0] for s in mine], dtype=torch.int32, device=self.device)
+            pl = torch.tensor([s[1] for s in mine], dtype=torch.int32, device=self.device)
+            seg = np.append(self.segmented_count, 0.0)
+            tot = torch.from_numpy(np.array([seg[min(s[1], len(seg) - 1)] for s in mine], np.float32)).to(self.device)
+            n = len(mine)
+            rc = torch.empty(n, dtype=torch.float32, device=self.device)
+            oc = torch.empty_like(rc)
+            df = torch.empty_like(rc)
+            adj_all = poses.clone()
+            iters = torch.zeros(n, dtype=torch.int32, device=self.device)
+            # the reference's gpu_batch_size loop (search_env.cpp:2504-2525); batches only bound memory here
+            bs = max(1, p.gpu_batch_size)
+            ti = time.perf_counter()
+            for b0 in range(0, n, bs):
+                b1 = min(n, b0 + bs)
+                sl = slice(b0, b1)
+                if p.icp_type == 3 and inp.use_icp:
+                    self.core.evaluate_icp(poses[sl], pm[sl], pl[sl], tot[sl], cost_type=COST_DEPTH_6DOF,
+                                           stride=p.gpu_stride, depth_factor=p.gpu_depth_factor,
+                                           sensor_resolution=p.sensor_resolution,
+                                           occlusion_threshold=p.gpu_occlusion_threshold, k=p.icp_k,
+                                           max_iterations=p.icp_max_iterations,
+                                           rotation_epsilon=p.icp_rotation_epsilon,
+                                           transformation_epsilon=p.icp_transformation_epsilon,
+                                           out=(adj_all[sl], iters[sl], rc[sl], oc[sl], df[sl]))
+                else:
+                    self.core.evaluate(poses[sl], pm[sl], pl[sl], tot[sl], cost_type=COST_DEPTH_6DOF,
+                                       stride=p.gpu_stride, depth_factor=p.gpu_depth_factor,
+                                       sensor_resolution=p.sensor_resolution,
+                                       occlusion_threshold=p.gpu_occlusion_threshold, out=(rc[sl], oc[sl], df[sl]))
+                self.core.select(rc[sl], oc[sl], pm[sl], K, index_base=lo + b0, keys=keys)
+            torch.cuda.synchronize(self.device)
+            icp_time = time.perf_counter() - ti if (p.icp_type == 3 and inp.use_icp) else 0.0
+            self._last_costs = (rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy())
+        allreduce_min_keys(keys)
+        cost, idx = decode_keys(keys)
+        # winning adjusted poses: the owning rank contributes, the others add zeros
+        win = torch.zeros((K, 16), dtype=torch.float32, device=self.device)
+        for m in range(K):
+            if idx[m] >= 0 and lo <= idx[m] < hi:
+                win[m] = adj_all[int(idx[m]) - lo]
+        if world > 1:
+            torch.distributed.all_reduce(win, op=torch.distributed.ReduceOp.SUM)
+        win = win.cpu().numpy()
+        results = []
+        for m in range(K):
+            if idx[m] < 0:
+                continue
+            # search_env.cpp:1996-2019: GPU-adjusted mat4x4 -> to_eigen(100) -> ContPose (6-DoF keeps the frame)
+            Tm = to_eigen(win[m], 100).astype(np.float64)
+            if inp.use_external_pose_list != 1:
+                Tm = (self.camera_pose @ CAM_TO_BODY) @ Tm @ np.linalg.inv(self.preprocess[m])
+            q = matrix_to_quat_xyzw(Tm[:3, :3])
+            cont = np.concatenate([Tm[:3, 3], q])
+            results.append((m, int(cost[m]), int(idx[m]), cont))
+        self.last_stats = EnvStats(scenes_rendered=n_total, scenes_valid=0, time=time.perf_counter() - t0,
+                                   icp_time=icp_time, peak_gpu_mem=float(torch.cuda.max_memory_allocated(self.device)))
+        return results
+
+    # -- ObjectRecognizer::LocalizeObjectsGreedyRender (object_recognizer.cpp:290-342) -------------
+    def localize_objects_greedy_render(self, inp: RecognitionInput) -> LocalizationResult:
+        if not self.models or self.model_names != list(inp.model_names):
+            self.set_static_input(inp.model_names, six_dof=inp.use_external_pose_list == 1)
+        self.set_input(inp)
+        res = self.compute_greedy_render_poses(inp)
+        out = LocalizationResult([], [], [], [], [], [], self.last_stats)
+        for m, cost, idx, cont in res:
+            # GetRawModelToSceneTransform (object_model.cpp:502-510): ContPose transform * preprocessing
+            T = pose_matrix(cont[:3], cont[3:7]).astype(np.float32).astype(np.float64) @ self.preprocess[m]
+            out.object_transforms.append(T)
+            out.preprocessing_transforms.append(self.preprocess[m])
+            out.detected_poses.append(cont)
+            out.model_names.append(self.model_names[m])
+            out.costs.append(cost)
+            out.indices.append(idx)
+        return out
+
+    def write_outputs(self, result: LocalizationResult, out_dir: str):
+        """perch_fat.cpp:302-323 output_poses.txt + output_stats.txt."""
+        os.makedirs(out_dir, exist_ok=True)
+        objs = [pio.DetectedObject(n, c[:3], c[3:7], T, P) for n, c, T, P in
+                zip(result.model_names, result.detected_poses, result.object_transforms,
+                    result.preprocessing_transforms)]
+        pio.write_output_poses(os.path.join(out_dir, "output_poses.txt"), objs)
+        s = result.stats
+        pio.write_output_stats(os.path.join(out_dir, "output_stats.txt"), s.scenes_rendered, s.scenes_valid, 0,
+                               s.time, 0, s.icp_time, s.peak_gpu_mem)

@@ -35,6 +35,21 @@ class Workload:
     gt_index: Sequence[int]
 
 
+def object_centers(K: int):
+    """K object centres on a grid in front of the camera (0.7-1.2 m), well inside the 640x480 view."""
+    if K == 1:
+        return [(0.03, -0.02, 0.80)]
+    cols = int(np.ceil(np.sqrt(K)))
+    rows = int(np.ceil(K / cols))
+    out = []
+    for i in range(K):
+        r, c = divmod(i, cols)
+        x = -0.30 + 0.60 * (c / max(cols - 1, 1))
+        y = -0.20 + 0.40 * (r / max(rows - 1, 1))
+        out.append((x, y, 0.75 + 0.45 * (i % 3) / 2))
+    return out
+
+
 def gpu_render_fn(core: PoseCore, device):
     def fn(tris, cnt, p16, pm, W, H, proj):
         poses = torch.from_numpy(np.ascontiguousarray(p16)).to(device)
@@ -58,7 +73,7 @@ def build(names: Sequence[str] = ("003_cracker_box",), poses_per_model: int = 10
     W, H = cam["width"], cam["height"]
     zero = torch.zeros((H, W), dtype=torch.int32, device=dev)
     core.set_observation(zero, None, torch.zeros((0, 3), dtype=torch.float32, device=dev), None, 0.01)
-    centers = [(0.03 + 0.12 * (i - (K - 1) / 2), -0.02, 0.80 + 0.05 * i) for i in range(K)]
+    centers = object_centers(K)
     gts = np.stack([syn.default_gt_pose(rng, c) for c in centers])
     scene = syn.make_scene(list(names), gts, gpu_render_fn(core, dev), cam=cam, rng=rng, k=k)
     raw = torch.from_numpy(scene.depth_raw).to(dev)

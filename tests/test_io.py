@@ -1,0 +1,92 @@
+"""File formats around the hot path (f2): PLY meshes, poses.txt, output_poses.txt / output_stats.txt,
+16-bit depth PNGs (the reference's own demo_depth.png, copied as a data fixture)."""
+import os
+
+import numpy as np
+
+import oracle
+from perception_amd import io, synthetic as syn
+from perception_amd.model import Model
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _per_vertex_colored(model):
+    v = model.tris.reshape(-1, 3)
+    key = (np.abs(v * 1000).astype(np.int64) % 256)
+    model.colors = key.reshape(-1, 3, 3)[:, 0, :].astype(np.uint8)
+    return model
+
+
+def test_ply_roundtrip_binary_and_ascii(tmp_path):
+    m = _per_vertex_colored(syn.ycb_proxy("005_tomato_soup_can"))
+    for binary in (True, False):
+        p = str(tmp_path / f"m{int(binary)}.ply")
+        io.save_ply(p, m, binary=binary)
+        m2 = io.load_ply(p)
+        assert np.array_equal(m2.tris, m.tris)
+        assert np.array_equal(m2.colors, m.colors)
+
+
+def test_ply_polygons_are_fan_triangulated_and_float_colors_rounded(tmp_path):
+    p = str(tmp_path / "quad.ply")
+    with open(p, "w") as f:
+        f.write("ply\nformat ascii 1.0\ncomment test\nelement vertex 4\nproperty float x\nproperty float y\n"
+                "property float z\nproperty float red\nproperty float green\nproperty float blue\n"
+                "element face 2\nproperty list uchar int vertex_indices\nend_header\n"
+                "0 0 0 1 0.5 0\n1 0 0 0 0 0\n1 1 0 0 0 0\n0 1 0 0 0 0\n4 0 1 2 3\n2 0 1\n")
+    m = io.load_ply(p)
+    assert m.tris.shape == (2, 9)  # quad -> 2 triangles, 2-index face skipped (model.cpp:76)
+    assert np.array_equal(m.tris[1], np.array([0, 0, 0, 1, 1, 0, 0, 1, 0], np.float32))
+    assert list(m.colors[0]) == [255, 128, 0]
+
+
+def test_default_color_is_128(tmp_path):
+    p = str(tmp_path / "t.ply")
+    with open(p, "w") as f:
+        f.write("ply\nformat ascii 1.0\nelement vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+                "element face 1\nproperty list uchar int vertex_indices\nend_header\n0 0 0\n1 0 0\n0 1 0\n3 0 1 2\n")
+    m = io.load_ply(p)
+    assert (m.colors == 128).all()
+
+
+def test_poses_txt_roundtrip(tmp_path):
+    rng = np.random.default_rng(0)
+    P = np.concatenate([rng.uniform(-1, 1, (50, 3)), rng.normal(size=(50, 4))], 1)
+    p = str(tmp_path / "poses.txt")
+    io.write_poses_txt(p, P)
+    Q = io.read_poses_txt(p)
+    assert Q.shape == (50, 7)
+    assert np.allclose(Q, P, atol=5e-5)
+
+
+def test_output_poses_and_stats_roundtrip(tmp_path):
+    objs = []
+    for i, name in enumerate(["003_cracker_box", "005_tomato_soup_can"]):
+        T = np.eye(4)
+        T[:3, 3] = (0.1 * i, -0.2, 0.8)
+        P = np.eye(4)
+        P[:3, 3] = (0, 0, -0.01 * i)
+        objs.append(io.DetectedObject(name, T[:3, 3], np.array([0, 0, 0.3, 0.95]), T, P))
+    p = str(tmp_path / "output_poses.txt")
+    io.write_output_poses(p, objs)
+    with open(p) as f:
+        assert len(f.readlines()) == 26
+    back = io.read_output_poses(p)
+    assert [o.name for o in back] == ["003_cracker_box", "005_tomato_soup_can"]
+    for a, b in zip(objs, back):
+        assert np.allclose(a.transform, b.transform) and np.allclose(a.preprocessing, b.preprocessing)
+        assert np.allclose(a.translation, b.translation) and np.allclose(a.quaternion_xyzw, b.quaternion_xyzw)
+    s = str(tmp_path / "output_stats.txt")
+    io.write_output_stats(s, 10000, 0, 0, 1.5, 0, 0.7, 1e9)
+    st = io.read_output_stats(s)
+    assert st["rendered"] == 10000 and st["runtime"] == 1.5 and st["icp_runtime"] == 0.7
+
+
+def test_reference_demo_depth_png_unprojects():
+    d = io.load_depth_png(os.path.join(G, "demo_depth.png"))
+    assert d.shape == (480, 640) and d.max() == 51320
+    xyz, pose, lab = oracle.depth_to_cloud(d, 8, 321.06398107, 242.97676897, 576.09757860, 576.09757860, 10000.0)
+    sub = d[::8, ::8]
+    assert len(xyz) == int((sub > 0).sum())
+    assert np.allclose(np.sort(xyz[:, 2]), np.sort(sub[sub > 0].astype(np.float32) / np.float32(10000.0)))

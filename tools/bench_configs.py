@@ -1,0 +1,97 @@
+#!/usr/bin/env python
+"""Time the BASELINE.json configs other than the headline one on ONE GPU (per-GPU shares of the
+multi-GPU configs).  Prints one JSON line per config.  Not the driver's bench (bench.py is).
+
+  C2  1 mesh, 10k poses, render + score, 640x480
+  C3  5 objects, 50k poses, render + GICP + re-render + score, 640x480 (+ argmin vs GT)
+  C4  21 objects, 200k poses over 8 GPUs -> 25k poses per GPU, render + score
+  C5  1 mesh, 1M poses at 1280x720 over 8 GPUs -> 125k poses per GPU, render + score
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from perception_amd import synthetic as syn  # noqa: E402
+from perception_amd import workloads  # noqa: E402
+from perception_amd._native import PCORE_KEY_NONE  # noqa: E402
+from perception_amd.core import decode_keys  # noqa: E402
+
+C3_NAMES = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def run(name, names, per_model, cam, icp, steps, warmup):
+    w = workloads.build(names=names, poses_per_model=per_model, cam=cam)
+    n = int(w.poses.shape[0])
+    dev = w.poses.device
+    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev)
+    if icp:
+        out = (torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+               *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)))
+
+        def step():
+            keys.fill_(PCORE_KEY_NONE)
+            adj, it, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                      stride=w.stride, out=out)
+            w.core.select(rc, oc, w.pose_model, w.num_models, keys=keys)
+    else:
+        out = tuple(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3))
+
+        def step():
+            keys.fill_(PCORE_KEY_NONE)
+            workloads.step(w, out, keys)
+    dt = timed(step, steps, warmup)
+    cost, idx = decode_keys(keys)
+    res = {"config": name, "poses": n, "models": w.num_models, "width": w.scene.width, "height": w.scene.height,
+           "icp": icp, "s_per_step": dt, "poses_per_s": n / dt,
+           "argmin_index": [int(i) for i in idx], "gt_index": [int(i) for i in w.gt_index],
+           "argmin_cost": [int(c) for c in cost]}
+    if icp:
+        it = out[1].float()
+        res["gicp_iters_mean"] = float(it.mean().item())
+        res["gicp_iters_max"] = int(it.max().item())
+    print(json.dumps(res), flush=True)
+    del w
+    torch.cuda.empty_cache()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2,C3,C4,C5")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the per-GPU pose count")
+    a = ap.parse_args()
+    sel = a.configs.split(",")
+    sc = a.scale
+    if "C2" in sel:
+        run("C2", ["003_cracker_box"], int(10000 * sc), syn.CAM_640, False, a.steps, a.warmup)
+    if "C3" in sel:
+        run("C3", C3_NAMES, int(10000 * sc), syn.CAM_640, True, a.steps, a.warmup)
+    if "C4" in sel:
+        run("C4/8", list(syn.YCB_PROXIES), int(25000 / 21 * sc), syn.CAM_640, False, a.steps, a.warmup)
+    if "C5" in sel:
+        run("C5/8", ["003_cracker_box"], int(125000 * sc), syn.CAM_1280, False, a.steps, a.warmup)
+
+
+if __name__ == "__main__":
+    main()
