@@ -71,6 +71,9 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    override = os.environ.get("PCORE_LIB")  # A/B profiling of alternative builds of the same sources
+    if override:
+        auto_build = False
     if auto_build:
         try:
             if _build.needs_build():
@@ -78,9 +81,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         except (RuntimeError, OSError) as e:  # no hipcc on this machine: fall through to the prebuilt .so
             if not os.path.exists(_build.LIB):
                 raise RuntimeError(f"libpcore.so is missing and cannot be built: {e}") from e
-    if not os.path.exists(_build.LIB):
-        raise RuntimeError(f"libpcore.so not found at {_build.LIB}; run `python -m perception_amd.build`")
-    L = ctypes.CDLL(_build.LIB)
+    path = override or _build.LIB
+    if not os.path.exists(path):
+        raise RuntimeError(f"libpcore.so not found at {path}; run `python -m perception_amd.build`")
+    L = ctypes.CDLL(path)
     vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
     L.pcore_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.pcore_destroy.argtypes = [vp]

@@ -9,6 +9,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -560,6 +561,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.out_oc = d_out_oc;
     a.out_diff = d_out_diff;
     a.dbg_zs = d_dbg_zs;
+    if (const char* e = getenv("PCORE_DEBUG_SKIP")) a.dbg_skip = atoi(e);
     HIPC(c, launch_fused_cost(a, s));
     return PCORE_OK;
 }

@@ -68,6 +68,9 @@ struct FusedArgs {
     float4* cloud_out;
     int32_t* cloud_count;
     int32_t cloud_cap;
+    // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
+    // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
+    int32_t dbg_skip;
 };
 
 // GICP over a chunk of poses (pcore_kernels.hip, gicp_kernel)

@@ -27,7 +27,7 @@ namespace pcore {
 constexpr int kWave = 64;
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kRecCap = 128;  // per-wave ring of queued triangle records
+constexpr int kRecCap = 96;   // per-wave ring of queued triangle records (flush above kRecCap - 64)
 constexpr int64_t PCORE_KEY_NONE_DEV = 0x7fffffffffffffffLL;
 constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queued; larger ones are
                               // processed cooperatively by the whole wave
@@ -171,9 +171,10 @@ __device__ __forceinline__ int sample_window(const float (&bmin)[2], const float
 
 struct FusedSmem {
     int32_t* zbuf;  // hs * ws
-    float* vx;      // kWaves * 64
+    float* vx;      // kWaves * 64: screen x of the wave's meshlet vertices
     float* vy;
-    float* vz;
+    float* vz;      // camera z (cm)
+    uint2* vwin;    // kWaves * 64: packed int16 sample-window bounds per vertex (see vertex_window)
     TriRec* ring;   // kWaves * kRecCap (phase 1); reused as int32 point queues in phase 2
     uint32_t* bitmap;
     int32_t* counters;  // [0] bad, [1] explained, [2] points
@@ -191,6 +192,7 @@ size_t fused_lds_bytes(int ws, int hs, int bitmap_words) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
     size_t b = al((size_t)ws * hs * 4);
     b += al((size_t)kWaves * kWave * 4) * 3;
+    b += al((size_t)kWaves * kWave * 8);
     b += al((size_t)kWaves * kRecCap * sizeof(TriRec));
     b += al((size_t)bitmap_words * 4);
     b += 16;
@@ -205,6 +207,7 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
     sm.vx = (float*)p; p += al((size_t)kWaves * kWave * 4);
     sm.vy = (float*)p; p += al((size_t)kWaves * kWave * 4);
     sm.vz = (float*)p; p += al((size_t)kWaves * kWave * 4);
+    sm.vwin = (uint2*)p; p += al((size_t)kWaves * kWave * 8);
     sm.ring = (TriRec*)p; p += al((size_t)kWaves * kRecCap * sizeof(TriRec));
     sm.bitmap = (uint32_t*)p; p += al((size_t)bitmap_words * 4);
     sm.counters = (int32_t*)p;
@@ -212,11 +215,43 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
 }
 
 template <int STRIDE>
+__device__ __forceinline__ int floor_div(int v, int s) {
+    if constexpr (STRIDE == 8) return v >> 3;  // arithmetic shift == floor division by 8
+    else {
+        const int q = v / s;
+        return (v % s != 0 && v < 0) ? q - 1 : q;
+    }
+}
+
+// Per-vertex contribution to the sample window of every triangle that uses the vertex.  For finite
+// screen coordinates the window of sample_window() (reference bbox + loop bounds) decomposes over the
+// three vertices because every step is monotone: trunc(max(0, min p) + 0.5) = max(0, min trunc(p + 0.5)),
+// floor(min(W-1, max p)) = min(W-1, max floor p), and ceil/floor division by s are monotone.  Clamping
+// p to +-65536 first changes no window of a <= 16384-pixel image and keeps every bound in int16.
+//   lo = (ceil(trunc(sx+0.5)/s), ceil((H-1-floor(sy))/s)),  hi = (floor(floor(sx)/s), floor((H-1-trunc(sy+0.5))/s))
+// A triangle's window is kx in [max(0, min lo.x), min(ws-1, max hi.x)] (same for y).
+template <int STRIDE>
+__device__ __forceinline__ uint2 vertex_window(float sx, float sy, int s, int H) {
+    const float cx = fminf(fmaxf(sx, -65536.0f), 65536.0f);
+    const float cy = fminf(fmaxf(sy, -65536.0f), 65536.0f);
+    const int tx = (int)(cx + 0.5f), fx = (int)floorf(cx);
+    const int ty = (int)(cy + 0.5f), fy = (int)floorf(cy);
+    const int lox = -floor_div<STRIDE>(-tx, s);
+    const int loy = -floor_div<STRIDE>(fy - (H - 1), s);
+    const int hix = floor_div<STRIDE>(fx, s);
+    const int hiy = floor_div<STRIDE>(H - 1 - ty, s);
+    return make_uint2(((uint32_t)lox & 0xffffu) | ((uint32_t)loy << 16), ((uint32_t)hix & 0xffffu) | ((uint32_t)hiy << 16));
+}
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
+
+template <int STRIDE>
 __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose) {
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
-    (void)tid;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int W = a.width, H = a.height, ws = a.ws;
     // pose (wave-uniform -> scalar loads)
@@ -233,11 +268,16 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     float* vx = sm.vx + wave * kWave;
     float* vy = sm.vy + wave * kWave;
     float* vz = sm.vz + wave * kWave;
+    uint2* vwin = sm.vwin + wave * kWave;
     TriRec* ring = sm.ring + wave * kRecCap;
+    const short2v wzero = {0, 0};
+    const short2v wlim = {(short)(ws - 1), (short)(a.hs - 1)};
     int rec_count = 0;  // wave-uniform
 
+    const int dbg = a.dbg_skip;
     auto flush = [&](int count) {
         wave_sync();
+        if (dbg & 1) return;
         for (int base = 0; base < count; base += kWave) {
             const int j = base + lane;
             if (j < count) {
@@ -251,90 +291,121 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         wave_sync();
     };
 
-    if (model >= 0 && model < a.num_models) {
-        const int ml_lo = a.model_ml_lo[model], ml_hi = a.model_ml_hi[model];
-        for (int m = ml_lo + wave; m < ml_hi; m += kWaves) {
-            const Meshlet ml = a.meshlets[m];
-            // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
-            // (image_renderer.cuh:296-305, 82-84)
-            bool bad_vertex = false;
-            if (lane < ml.nv) {
-                const float4 v = a.mverts[ml.vbase + lane];
-                const float lx = row4(m00, m01, m02, m03, v.x, v.y, v.z);
-                const float ly = row4(m10, m11, m12, m13, v.x, v.y, v.z);
-                const float lz = row4(m20, m21, m22, m23, v.x, v.y, v.z);
-                const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
-                const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
-                const float sx = px / lz * Wf / 2.0f + Wf / 2.0f;
-                const float sy = py / lz * Hf / 2.0f + Hf / 2.0f;
-                vx[lane] = sx;
-                vy[lane] = sy;
-                vz[lane] = lz;
-                bad_vertex = !(sx == sx) || !(sy == sy);
-            }
-            const uint64_t nanmask = __ballot(bad_vertex);
-            wave_sync();
-            for (int t0 = 0; t0 < ml.nt; t0 += kWave) {
-                const int t = t0 + lane;
-                int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
-                TriRec r;
-                if (t < ml.nt) {
-                    const uint32_t pk = a.mtris[ml.tbase + t];
-                    const int i0 = pk & 0xff, i1 = (pk >> 8) & 0xff, i2 = (pk >> 16) & 0xff;
-                    r.a0 = vx[i0]; r.a1 = vy[i0];
-                    r.b0 = vx[i1]; r.b1 = vy[i1];
-                    r.c0 = vx[i2]; r.c1 = vy[i2];
-                    float bmin[2], bmax[2];
-                    const bool nan_tri = nanmask != 0 && (((nanmask >> i0) | (nanmask >> i1) | (nanmask >> i2)) & 1ull);
-                    if (!nan_tri) {
-                        // finite (or +-inf) coordinates: min/max form equals the reference's iterative clamp
-                        bmin[0] = fmaxf(0.0f, fminf(fminf(r.a0, r.b0), r.c0));
-                        bmin[1] = fmaxf(0.0f, fminf(fminf(r.a1, r.b1), r.c1));
-                        bmax[0] = fminf(cmax0, fmaxf(fmaxf(r.a0, r.b0), r.c0));
-                        bmax[1] = fminf(cmax1, fmaxf(fmaxf(r.a1, r.b1), r.c1));
-                    } else {
-                        const float p[3][2] = {{r.a0, r.a1}, {r.b0, r.b1}, {r.c0, r.c1}};
-                        bbox_ref(p, cmax0, cmax1, bmin, bmax);
-                    }
-                    nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
-                    if (nk > 0) {
-                        r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
-                    }
-                }
-                // large triangles: whole-wave cooperative
-                uint64_t big = __ballot(nk > kSmallK);
-                while (big) {
-                    const int j = __ffsll((unsigned long long)big) - 1;
-                    big &= big - 1;
-                    TriRec rb;
-                    rb.a0 = __shfl(r.a0, j); rb.a1 = __shfl(r.a1, j);
-                    rb.b0 = __shfl(r.b0, j); rb.b1 = __shfl(r.b1, j);
-                    rb.c0 = __shfl(r.c0, j); rb.c1 = __shfl(r.c1, j);
-                    rb.z0 = __shfl(r.z0, j); rb.z1 = __shfl(r.z1, j); rb.z2 = __shfl(r.z2, j);
-                    const int bkx0 = __shfl(kx0, j), bky0 = __shfl(ky0, j), bnx = __shfl(nx, j), bnk = __shfl(nk, j);
-                    for (int q = lane; q < bnk; q += kWave) {
-                        const int iy = q / bnx, ix = q - iy * bnx;
-                        raster_sample(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf);
-                    }
-                }
-                // small triangles: queue into the wave's ring
-                const bool qd = nk > 0 && nk <= kSmallK;
-                const uint64_t bq = __ballot(qd);
-                if (qd) {
-                    r.meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) | ((uint32_t)(ny - 1) << 28);
-                    ring[rec_count + mbcnt64(bq)] = r;
-                }
-                rec_count += __popcll(bq);
-                if (rec_count > kRecCap - kWave) {
-                    flush(rec_count);
-                    rec_count = 0;
-                }
-            }
-            wave_sync();  // vertex slots are rewritten by the next meshlet
-        }
-        if (rec_count > 0) flush(rec_count);
+    if (model < 0 || model >= a.num_models) return;
+    const int ml_lo = a.model_ml_lo[model], ml_hi = a.model_ml_hi[model];
+    int m = ml_lo + wave;
+    Meshlet ml = {0, 0, 0, 0};
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t pk0 = 0, pk1 = 0;
+    if (m < ml_hi) {
+        ml = a.meshlets[m];
+        if (lane < ml.nv) v = a.mverts[ml.vbase + lane];
+        if (lane < ml.nt) pk0 = a.mtris[ml.tbase + lane];
+        if (kWave + lane < ml.nt) pk1 = a.mtris[ml.tbase + kWave + lane];
     }
-    __syncthreads();
+    for (; m < ml_hi; m += kWaves) {
+        // prefetch the next meshlet of this wave while this one is processed
+        const int mn = m + kWaves;
+        Meshlet mln = {0, 0, 0, 0};
+        float4 vn = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t pn0 = 0, pn1 = 0;
+        if (mn < ml_hi) {
+            mln = a.meshlets[mn];
+            if (lane < mln.nv) vn = a.mverts[mln.vbase + lane];
+            if (lane < mln.nt) pn0 = a.mtris[mln.tbase + lane];
+            if (kWave + lane < mln.nt) pn1 = a.mtris[mln.tbase + kWave + lane];
+        }
+        // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
+        // (image_renderer.cuh:296-305, 82-84)
+        bool bad_vertex = false;
+        if (lane < ml.nv && !(dbg & 8)) {
+            const float lx = row4(m00, m01, m02, m03, v.x, v.y, v.z);
+            const float ly = row4(m10, m11, m12, m13, v.x, v.y, v.z);
+            const float lz = row4(m20, m21, m22, m23, v.x, v.y, v.z);
+            const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
+            const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
+            const float sx = px / lz * Wf / 2.0f + Wf / 2.0f;
+            const float sy = py / lz * Hf / 2.0f + Hf / 2.0f;
+            vx[lane] = sx;
+            vy[lane] = sy;
+            vz[lane] = lz;
+            vwin[lane] = vertex_window<STRIDE>(sx, sy, s, H);
+            bad_vertex = !(sx == sx) || !(sy == sy);
+        }
+        const uint64_t nanmask = __ballot(bad_vertex);
+        wave_sync();
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const int t0 = half * kWave;
+            if (t0 >= ml.nt || (dbg & 2)) break;
+            const int t = t0 + lane;
+            const uint32_t pk = half == 0 ? pk0 : pk1;
+            int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
+            int i0 = 0, i1 = 0, i2 = 0;
+            if (t < ml.nt) {
+                i0 = pk & 0xff; i1 = (pk >> 8) & 0xff; i2 = (pk >> 16) & 0xff;
+                const bool nan_tri = nanmask != 0 && (((nanmask >> i0) | (nanmask >> i1) | (nanmask >> i2)) & 1ull);
+                if (!nan_tri) {
+                    const uint2 w0 = vwin[i0], w1 = vwin[i1], w2 = vwin[i2];
+                    short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
+                    short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
+                    lo = __builtin_elementwise_max(lo, wzero);
+                    hi = __builtin_elementwise_min(hi, wlim);
+                    kx0 = lo.x; ky0 = lo.y;
+                    nx = (int)hi.x - (int)lo.x + 1;
+                    ny = (int)hi.y - (int)lo.y + 1;
+                    nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+                } else {
+                    // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
+                    const float p[3][2] = {{vx[i0], vy[i0]}, {vx[i1], vy[i1]}, {vx[i2], vy[i2]}};
+                    float bmin[2], bmax[2];
+                    bbox_ref(p, cmax0, cmax1, bmin, bmax);
+                    nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
+                }
+            }
+            TriRec r;
+            if (nk > 0) {
+                r.a0 = vx[i0]; r.a1 = vy[i0];
+                r.b0 = vx[i1]; r.b1 = vy[i1];
+                r.c0 = vx[i2]; r.c1 = vy[i2];
+                r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
+            }
+            // large triangles: whole-wave cooperative
+            uint64_t big = __ballot(nk > kSmallK);
+            while (big) {
+                const int j = __ffsll((unsigned long long)big) - 1;
+                big &= big - 1;
+                TriRec rb;
+                rb.a0 = __shfl(r.a0, j); rb.a1 = __shfl(r.a1, j);
+                rb.b0 = __shfl(r.b0, j); rb.b1 = __shfl(r.b1, j);
+                rb.c0 = __shfl(r.c0, j); rb.c1 = __shfl(r.c1, j);
+                rb.z0 = __shfl(r.z0, j); rb.z1 = __shfl(r.z1, j); rb.z2 = __shfl(r.z2, j);
+                const int bkx0 = __shfl(kx0, j), bky0 = __shfl(ky0, j), bnx = __shfl(nx, j), bnk = __shfl(nk, j);
+                for (int q = lane; q < bnk; q += kWave) {
+                    const int iy = q / bnx, ix = q - iy * bnx;
+                    raster_sample(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf);
+                }
+            }
+            // small triangles: queue into the wave's ring
+            const bool qd = nk > 0 && nk <= kSmallK;
+            const uint64_t bq = __ballot(qd);
+            if (qd) {
+                r.meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) | ((uint32_t)(ny - 1) << 28);
+                ring[rec_count + mbcnt64(bq)] = r;
+            }
+            rec_count += __popcll(bq);
+            if (rec_count > kRecCap - kWave) {
+                flush(rec_count);
+                rec_count = 0;
+            }
+        }
+        wave_sync();  // vertex slots are rewritten by the next meshlet
+        ml = mln;
+        v = vn;
+        pk0 = pn0;
+        pk1 = pn1;
+    }
+    if (rec_count > 0) flush(rec_count);
 }
 
 template <int STRIDE>
@@ -345,7 +416,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     const int wave = tid >> 6;
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
-    const int W = a.width, H = a.height, ws = a.ws, hs = a.hs;
+    const int ws = a.ws, hs = a.hs;
     const int nsamp = ws * hs;
 
     const FusedSmem sm = carve_smem(smem_raw, nsamp, a.bitmap_words);
@@ -356,6 +427,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
     raster_phase<STRIDE>(a, sm, pose);
+    __syncthreads();
 
     // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
     int32_t* queue = reinterpret_cast<int32_t*>(sm.ring) + wave * (kRecCap * (int)sizeof(TriRec) / 4);
@@ -417,7 +489,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     for (int base = wave * kWave; base < nsamp; base += kThreads) {
         const int k = base + lane;
         bool valid = false;
-        if (k < nsamp) {
+        if (k < nsamp && !(a.dbg_skip & 4)) {
             const int32_t z = sm.zbuf[k];
             const int32_t zf = occlusion_rule(z, a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg, pl,
                                               a.occlusion_threshold);
@@ -492,6 +564,7 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
     raster_phase<STRIDE>(a, sm, pose);
+    __syncthreads();
     float4* out = a.cloud_out + (size_t)pose * a.cloud_cap;
     for (int base = 0; base < nsamp; base += kThreads) {
         const int k = base + tid;

@@ -1,0 +1,33 @@
+#!/usr/bin/env python
+"""Run the C2 workload's fused kernel a few times (for rocprofv3 counter / trace collection)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from perception_amd import workloads  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--poses", type=int, default=10000)
+    ap.add_argument("--icp", action="store_true")
+    a = ap.parse_args()
+    w = workloads.build(poses_per_model=a.poses)
+    n = int(w.poses.shape[0])
+    for _ in range(a.iters):
+        if a.icp:
+            w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+        else:
+            w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+    torch.cuda.synchronize()
+    print("done", n)
+
+
+if __name__ == "__main__":
+    main()
