@@ -364,7 +364,7 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
 // ==================================================================================================
 namespace {
 
-constexpr int kGicpThreads = 256;  // GPU workgroup size whose reduction order the oracle mirrors
+constexpr int kGicpThreads = 64;  // one GPU wave per pose: its reduction order is mirrored here
 constexpr int kMaxK = 16;
 constexpr double kPlaneScale = 1.0 - 1e-3;  // I - (1 - 1e-3) n n^T == U diag(1, 1, 1e-3) U^T
 

@@ -90,7 +90,7 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
  *    regularisation C = U diag(1, 1, 1e-3) U^T from 6 cyclic Jacobi sweeps (double, sqrt/div only);
  *  - Gauss-Newton on SE(3): correspondences = float 1-NN of (float)(R s + t) in the target segment,
  *    Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I], H / b reduced in the GPU's fixed order
- *    (256 per-thread sequential partials, wave shuffle-down tree, 4 wave partials in order), 6x6 LDLT
+ *    (64 per-lane sequential partials, then the wave shuffle-down tree), 6x6 LDLT
  *    without pivoting, left update T <- [R(q(w)) | rho] T with q = normalise(1, w/2), stop when
  *    max|dR - I| < rot_eps and max|dt| < trans_eps or after max_iter iterations.
  * Covariances: double[6] (xx, xy, xz, yy, yz, zz) per point. */

@@ -642,7 +642,10 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         c->cov_k_all = k;
     }
     const int nsamp = ws * hs;
-    const int chunk = std::min(num_poses, 2048);
+    // equal chunks of <= 8192 poses (8192 x 4800 slots: 0.5 GB clouds + 1.9 GB covariances), so no chunk
+    // is a short tail that leaves most of the chip idle
+    const int nchunks = (num_poses + 8191) / 8192;
+    const int chunk = (num_poses + nchunks - 1) / nchunks;
     HIPC(c, dev_reserve(c->icp_cloud, (size_t)chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_count, (size_t)chunk));
     HIPC(c, dev_reserve(c->icp_cov, (size_t)6 * chunk * nsamp));
@@ -666,7 +669,6 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.max_iter = ip->max_iterations;
     g.rot_eps = ip->rotation_epsilon;
     g.trans_eps = ip->transformation_epsilon;
-    g.tgt_lds_cap = std::min(c->max_seg, 4096);
     for (int base = 0; base < num_poses; base += chunk) {
         const int n = std::min(chunk, num_poses - base);
         a.poses = d_poses + (size_t)16 * base;

@@ -11,9 +11,9 @@
 //   covariance_kernel  one workgroup per segment (a pose's rendered cloud or an observed label):
 //                      brute-force k-NN of every point inside its segment (broadcast reads), double
 //                      mean / covariance, 6-sweep Jacobi, PLANE regularisation.
-//   gicp_kernel        one workgroup per pose: per-thread sequential partial sums of J^T M J / J^T M e,
-//                      wave shuffle-down tree, 4 wave partials in order, one-lane 6x6 LDLT and update,
-//                      target segment staged in LDS, then concatenate_transforms (renderer.cu:1412-1429).
+//   gicp_kernel        one wave per pose (4 per workgroup): per-lane sequential partial sums of J^T M J /
+//                      J^T M e, wave shuffle-down tree, one-lane 6x6 LDLT and update, then
+//                      concatenate_transforms (renderer.cu:1412-1429).
 #include "pcore_internal.h"
 
 #include <climits>
@@ -28,7 +28,22 @@ namespace {
 constexpr int kGThreads = 256;
 constexpr int kGWaves = kGThreads / 64;
 constexpr int kMaxK = 16;
+constexpr int kTgtTile = 512;  // targets staged per wave in LDS, SoA (6 KiB)
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+struct TgtTile {
+    float x[kTgtTile], y[kTgtTile], z[kTgtTile];
+};
 constexpr double kPlaneScale = 1.0 - 1e-3;
+
+// LDS writes by some lanes of a wave visible to all its lanes (no block barrier: waves are independent)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
     const float dx = ax - bx, dy = ay - by, dz = az - bz;
@@ -166,24 +181,50 @@ hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const i
 // GICP
 // ------------------------------------------------------------------------------------------------
 
-// One point's Gauss-Newton contribution (orc gicp_contrib): acc[0..20] upper(H), [21..26] b, [27] error.
-__device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&t)[3], float4 s,
-                                             const double* cs, const float4* tgt, const double* tcov, int nt,
-                                             double (&acc)[28]) {
-    const double s0 = (double)s.x, s1 = (double)s.y, s2 = (double)s.z;
-    double q[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
-    const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
-    int j = -1;
-    float best = INFINITY;
-    for (int o = 0; o < nt; o++) {
-        const float4 p = tgt[o];
-        const float d = sqdist3(qx, qy, qz, p.x, p.y, p.z);
-        if (d < best) { best = d; j = o; }
+// Stage tn targets into a wave's SoA tile, padded to a multiple of 4 with +inf.  A non-finite target
+// (never the nearest in the oracle's scan: its distance is NaN or inf) is staged as +inf too, so no
+// distance in the packed scan is NaN for a finite query.
+__device__ __forceinline__ void stage_targets(TgtTile& T, const float4* tgt, int tn, int lane) {
+    const int tn4 = (tn + 3) & ~3;
+    for (int o = lane; o < tn4; o += 64) {
+        float4 p = o < tn ? tgt[o] : make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
+        if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) p = make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
+        T.x[o] = p.x;
+        T.y[o] = p.y;
+        T.z[o] = p.z;
     }
-    if (j < 0) return;
-    const double* ct = tcov + (size_t)6 * j;
+}
+
+// Nearest of a staged tile, four targets per step with packed f32 arithmetic (same IEEE operations,
+// per element, as sqdist3).  A 4-way tournament that prefers the later target only when strictly
+// nearer, then one strict update of (best, j): the lexicographic minimum of (distance, index), i.e.
+// the oracle's first strict minimum.
+__device__ __forceinline__ void scan_targets(const TgtTile& T, int tn, int t0, float qx, float qy, float qz,
+                                             float& best, int& j) {
+    const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+#pragma unroll 2
+    for (int o = 0; o < tn; o += 4) {
+        const f4v X = *reinterpret_cast<const f4v*>(&T.x[o]);
+        const f4v Y = *reinterpret_cast<const f4v*>(&T.y[o]);
+        const f4v Z = *reinterpret_cast<const f4v*>(&T.z[o]);
+        const f2v dxa = qx2 - X.xy, dya = qy2 - Y.xy, dza = qz2 - Z.xy;
+        const f2v dxb = qx2 - X.zw, dyb = qy2 - Y.zw, dzb = qz2 - Z.zw;
+        const f2v da = dxa * dxa + dya * dya + dza * dza;
+        const f2v db = dxb * dxb + dyb * dyb + dzb * dzb;
+        const bool c01 = da.y < da.x, c23 = db.y < db.x;
+        const float m01 = c01 ? da.y : da.x, m23 = c23 ? db.y : db.x;
+        const int i01 = c01 ? 1 : 0, i23 = c23 ? 3 : 2;
+        const bool c = m23 < m01;
+        const float m = c ? m23 : m01;
+        const int i = c ? i23 : i01;
+        if (m < best) { best = m; j = t0 + o + i; }
+    }
+}
+
+// One point's Gauss-Newton contribution (orc gicp_contrib) given its transformed position q and its
+// correspondence tj / ct: acc[0..20] upper(H), [21..26] b, [27] error.
+__device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double* cs,
+                                             float4 tj, const double* ct, double (&acc)[28]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
     double RC[3][3], A[3][3];
@@ -212,7 +253,6 @@ __device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const doub
     for (int r = 0; r < 3; r++)
 #pragma unroll
         for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
-    const float4 tj = tgt[j];
     const double e[3] = {(double)tj.x - q[0], (double)tj.y - q[1], (double)tj.z - q[2]};
     const double J[3][6] = {{0.0, -q[2], q[1], -1.0, 0.0, 0.0},
                             {q[2], 0.0, -q[0], 0.0, -1.0, 0.0},
@@ -271,14 +311,16 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
     return true;
 }
 
-__global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_g[];
-    __shared__ double sR[9], sT[3];
-    __shared__ double wpart[kGWaves][28];
-    __shared__ int s_done, s_iters;
-    const int pose = blockIdx.x;  // chunk-local
+// One wave per pose, 4 poses per workgroup: no block barriers; the wave's lanes accumulate their
+// points' contributions sequentially (point i -> lane i % 64), a shuffle-down tree reduces them to
+// lane 0, which solves and updates; other waves of the CU hide the serial solve.
+__global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g, int num_poses) {
+    __shared__ double sRT[kGWaves][12];
+    __shared__ TgtTile sT[kGWaves];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pose = __builtin_amdgcn_readfirstlane(blockIdx.x * kGWaves + wave);  // chunk-local, wave-uniform
+    if (pose >= num_poses) return;
     const int gp = g.pose_base + pose;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ns = g.src_count[pose];
     const float4* src = g.src + (size_t)pose * g.src_cap;
     const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
@@ -287,56 +329,68 @@ __global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g) {
         const int pl = g.pose_label[gp];
         seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
     }
+    seg = __builtin_amdgcn_readfirstlane(seg);
     const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
     const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
     const double* tcov = g.tgt_cov + (size_t)6 * lo;
     const float4* tgt = g.tgt + lo;
-    if (nt <= g.tgt_lds_cap) {  // stage the target segment in LDS (broadcast reads in the NN loop)
-        float4* tl = reinterpret_cast<float4*>(smem_g);
-        for (int i = tid; i < nt; i += kGThreads) tl[i] = tgt[i];
-        tgt = tl;
+    double* RT = sRT[wave];
+    TgtTile& T = sT[wave];
+    const bool resident = nt <= kTgtTile;  // the whole segment stays in LDS for all iterations
+    if (resident) stage_targets(T, tgt, min(nt, kTgtTile), lane);
+    if (lane == 0) {
+        for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
     }
-    if (tid == 0) {
-        for (int i = 0; i < 9; i++) sR[i] = (i % 4 == 0) ? 1.0 : 0.0;
-        sT[0] = sT[1] = sT[2] = 0.0;
-        s_done = (ns <= 0 || nt <= 0) ? 1 : 0;
-        s_iters = 0;
-    }
-    __syncthreads();
-    for (int it = 0; it < g.max_iter; it++) {
-        if (s_done) break;
+    int iters = 0;
+    bool done = ns <= 0 || nt <= 0;
+    for (int it = 0; it < g.max_iter && !done; it++) {
+        wave_lds_sync();
         double R[3][3], t[3];
 #pragma unroll
         for (int r = 0; r < 3; r++) {
 #pragma unroll
-            for (int c = 0; c < 3; c++) R[r][c] = sR[3 * r + c];
-            t[r] = sT[r];
+            for (int c = 0; c < 3; c++) R[r][c] = RT[3 * r + c];
+            t[r] = RT[9 + r];
         }
         double acc[28];
 #pragma unroll
         for (int v = 0; v < 28; v++) acc[v] = 0.0;
-        for (int i = tid; i < ns; i += kGThreads) gicp_contrib(R, t, src[i], scov + (size_t)6 * i, tgt, tcov, nt, acc);
-        // fixed-order reduction: shuffle-down tree to lane 0 of each wave
+        for (int i0 = 0; i0 < ns; i0 += 64) {
+            const int i = i0 + lane;
+            const bool act = i < ns;
+            const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+            double q[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
+            const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
+            // nearest target: first strict minimum of the float squared distance (orc gicp_nn)
+            int j = -1;
+            float best = INFINITY;
+            for (int t0 = 0; t0 < nt; t0 += kTgtTile) {
+                const int tn = min(kTgtTile, nt - t0);
+                if (!resident) {
+                    wave_lds_sync();
+                    stage_targets(T, tgt + t0, tn, lane);
+                    wave_lds_sync();
+                }
+                scan_targets(T, tn, t0, qx, qy, qz, best, j);
+            }
+            if (act && j >= 0) gicp_contrib(R, q, scov + (size_t)6 * i, tgt[j], tcov + (size_t)6 * j, acc);
+        }
 #pragma unroll
         for (int v = 0; v < 28; v++) {
             double x = acc[v];
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
-            if (lane == 0) wpart[wave][v] = x;
+            acc[v] = x;
         }
-        __syncthreads();
-        if (tid == 0) {
-            double tot[28];
-            for (int v = 0; v < 28; v++) {
-                double sum = wpart[0][v];
-                for (int w = 1; w < kGWaves; w++) sum = sum + wpart[w][v];
-                tot[v] = sum;
-            }
+        int flag = 0;  // 0 continue, 1 stop (no update), 2 stop after update
+        if (lane == 0) {
             double d[6];
-            if (!ldlt_solve6(tot, tot + 21, d)) {
-                s_done = 1;
+            if (!ldlt_solve6(acc, acc + 21, d)) {
+                flag = 1;
             } else {
-                s_iters = s_iters + 1;
                 double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
                 const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
                 const double inv = 1.0 / nrm;
@@ -346,38 +400,33 @@ __global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g) {
                 const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
                                          {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
                                          {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
-                double Rn[3][3], tn[3];
-                for (int r = 0; r < 3; r++) {
-                    for (int c = 0; c < 3; c++)
-                        Rn[r][c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
-                    tn[r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
-                }
                 double dr = 0.0, dt = 0.0;
                 for (int r = 0; r < 3; r++) {
                     for (int c = 0; c < 3; c++) {
+                        RT[3 * r + c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
                         const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
                         dr = v > dr ? v : dr;
                     }
+                    RT[9 + r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
                     const double v = fabs(d[3 + r]);
                     dt = v > dt ? v : dt;
                 }
-                for (int r = 0; r < 3; r++) {
-                    for (int c = 0; c < 3; c++) sR[3 * r + c] = Rn[r][c];
-                    sT[r] = tn[r];
-                }
-                if (dr < g.rot_eps && dt < g.trans_eps) s_done = 1;
+                flag = (dr < g.rot_eps && dt < g.trans_eps) ? 2 : 0;
             }
         }
-        __syncthreads();
+        flag = __shfl(flag, 0, 64);
+        if (flag != 1) iters++;
+        done = flag != 0;
     }
-    if (tid == 0) {
+    wave_lds_sync();
+    if (lane == 0) {
         // concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
         const float* pin = g.poses_in + (size_t)16 * gp;
         float A[4][4], Tf[4][4];
         for (int r = 0; r < 4; r++)
             for (int c = 0; c < 4; c++) {
                 A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
-                Tf[r][c] = r < 3 ? (float)(c < 3 ? sR[3 * r + c] : sT[r]) : (c == 3 ? 1.0f : 0.0f);
+                Tf[r][c] = r < 3 ? (float)(c < 3 ? RT[3 * r + c] : RT[9 + r]) : (c == 3 ? 1.0f : 0.0f);
             }
         float* pout = g.poses_out + (size_t)16 * gp;
         for (int r = 0; r < 4; r++)
@@ -385,14 +434,13 @@ __global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g) {
                 const float p = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
                 pout[4 * r + c] = r < 3 ? (float)((double)p * 100) : p;
             }
-        if (g.iters_out) g.iters_out[gp] = s_iters;
+        if (g.iters_out) g.iters_out[gp] = iters;
     }
 }
 
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;
-    const size_t lds = (size_t)g.tgt_lds_cap * sizeof(float4);
-    hipLaunchKernelGGL(gicp_kernel, dim3(num_poses), dim3(kGThreads), lds, s, g);
+    hipLaunchKernelGGL(gicp_kernel, dim3((num_poses + kGWaves - 1) / kGWaves), dim3(kGThreads), 0, s, g, num_poses);
     return hipGetLastError();
 }
 

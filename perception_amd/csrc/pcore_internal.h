@@ -92,7 +92,6 @@ struct GicpArgs {
     int32_t pose_base;        // first batch index of this chunk
     int32_t max_iter;
     double rot_eps, trans_eps;
-    int32_t tgt_lds_cap;      // targets staged in LDS when the segment has <= this many points
 };
 
 // launchers (pcore_kernels.hip)

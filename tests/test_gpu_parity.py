@@ -289,3 +289,38 @@ def test_evaluate_icp_3dof_matches_oracle(one_object):
     assert np.array_equal(iters.cpu().numpy(), oit)
     assert _bits_equal(adj.cpu().numpy(), oadj)
     assert _bits_equal(rc.cpu().numpy(), orc)
+
+
+def test_evaluate_icp_dense_targets_matches_oracle(one_object):
+    """Observed cloud at stride 2 (label segment of ~2k points): the GICP kernel's target tiling path."""
+    case, core, t = one_object
+    sc = case.scene
+    xyz, lab = core.observed_cloud(t["raw"], t["mask"], 2, sc.depth_factor)
+    oxyz, _, olab = oracle.depth_to_cloud(sc.depth_raw, 2, sc.cx, sc.cy, sc.fx, sc.fy, sc.depth_factor,
+                                          label_mask=sc.mask)
+    assert _bits_equal(xyz.cpu().numpy(), oxyz) and np.array_equal(lab.cpu().numpy(), olab)
+    order = np.argsort(olab, kind="stable")
+    oxyz, olab = oxyz[order], olab[order]
+    ls = np.array([np.searchsorted(olab, L, "left") for L in range(case.K)], np.int32)
+    le = np.array([np.searchsorted(olab, L, "right") for L in range(case.K)], np.int32)
+    assert (le - ls).max() > 1024
+    tot = (le - ls).astype(np.float32)[case.pose_label]
+    ocov = np.zeros((len(oxyz), 6))
+    for L in range(case.K):
+        ocov[ls[L]:le[L]] = oracle.covariances(oxyz[ls[L]:le[L]])
+    n = 16
+    try:
+        core.set_observation(t["src"], t["mask"], xyz, lab, 0.01)
+        adj, iters, rc, oc, df = core.evaluate_icp(t["poses"][:n], t["pm"][:n], t["pl"][:n],
+                                                   torch.from_numpy(tot[:n]).to(t["poses"].device),
+                                                   cost_type=2, stride=case.stride)
+    finally:
+        core.set_observation(t["src"], t["mask"], t["obs_xyz"], t["obs_lab"], 0.01)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n], case.pose_label[:n],
+        sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy,
+        100.0, oxyz, ocov, ls, le, tot[:n], 2, True, 0.01)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
