@@ -91,6 +91,19 @@ int pcore_observed_cloud(pcore_ctx* ctx, const int32_t* d_depth, const uint8_t* 
                          int32_t height, int32_t stride, float depth_factor, float* d_out_xyz,
                          int32_t* d_out_label, int32_t cap, int32_t* out_count, pcore_stream stream);
 
+/* depth2cloud_global for 3-DoF table-top scenes (renderer.cu:1936-2069 with camera_transform and
+ * observed_cloud_bounds; compute_point_clouds.cuh:14-35, 79-91, 125-157): as pcore_observed_cloud
+ * without a label mask, keeping only pixels whose point, moved to the world frame by `cam_to_world`
+ * (HOST, 4 x 4 row-major float, R p + t evaluated left to right in float), lies inside `bounds` (HOST,
+ * 6 doubles: x_max, x_min, y_max, y_min, z_max, z_min, compared as floats).  The output points stay in
+ * the CAMERA frame, as in the reference.  cam_to_world and bounds are both given or both NULL.
+ * d_rgb (nullable): H x W x 3 uint8 image; d_out_rgb (nullable, needs d_rgb) receives each kept
+ * pixel's 3 bytes in the input's channel order. */
+int pcore_observed_cloud_bounded(pcore_ctx* ctx, const int32_t* d_depth, const uint8_t* d_rgb, int32_t width,
+                                 int32_t height, int32_t stride, float depth_factor, const float* cam_to_world,
+                                 const double* bounds, float* d_out_xyz, uint8_t* d_out_rgb, int32_t cap,
+                                 int32_t* out_count, pcore_stream stream);
+
 /* Observation used by every evaluate call until replaced: the source depth in cm (H x W int32; the
  * reference's source_depth after search_env.cpp:2487-2498), the source mask label (H x W uint8, the
  * reference's source_mask_label; NULL for 3-DoF) and the observed cloud with its labels (the
@@ -156,6 +169,19 @@ int pcore_depth_to_cloud(pcore_ctx* ctx, const int32_t* d_depth, int32_t num_pos
 #define PCORE_KEY_NONE ((int64_t)0x7fffffffffffffffLL)
 int pcore_select(pcore_ctx* ctx, const float* d_rc, const float* d_oc, const int32_t* d_pose_model,
                  int32_t num_poses, int64_t index_base, int32_t num_models, int64_t* d_keys, pcore_stream stream);
+
+/* ADD / ADD-S of estimated against ground-truth poses over one model's points -- the YCB harness
+ * metric: compare_clouds (sbpl_perception/src/scripts/tools/fat_dataset/
+ * fat_pose_image.py:2020-2139) and pose_error.add / adi (fat_dataset/lib/utils/pose_error.py:72-108).
+ *   d_pts      n x 3 float model points (model frame, metres), device
+ *   d_T_gt,    num_pairs x 16 double, row-major 4x4 object-to-camera transforms, device
+ *   d_T_est
+ *   d_add      num_pairs doubles: mean_i |T_gt p_i - T_est p_i|           (nullable)
+ *   d_adds     num_pairs doubles: mean_i min_j |T_gt p_i - T_est p_j|     (nullable)
+ * f64 arithmetic; the minimum is exact (no kd-tree approximation).  Needs only a context (no meshes /
+ * camera / observation). */
+int pcore_pose_distances(pcore_ctx* ctx, const float* d_pts, int32_t n, const double* d_T_gt, const double* d_T_est,
+                         int32_t num_pairs, double* d_add, double* d_adds, pcore_stream stream);
 
 #ifdef __cplusplus
 }

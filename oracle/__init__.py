@@ -108,6 +108,27 @@ def depth_to_cloud(depth, stride, cx, cy, fx, fy, depth_factor, label_mask=None,
     return xyz[:cnt].copy(), pose[:cnt].copy(), lab[:cnt].copy()
 
 
+def depth_to_cloud_bounded(depth, stride, cx, cy, fx, fy, depth_factor, cam_to_world=None, bounds=None, rgb=None):
+    """3-DoF observed cloud: (xyz (P,3) f32 camera frame, rgb (P,3) u8 or None)."""
+    depth = _c(depth, np.int32)
+    h, w = depth.shape
+    cap = ((h + stride - 1) // stride) * ((w + stride - 1) // stride)
+    xyz = np.zeros((max(cap, 1), 3), np.float32)
+    out_rgb = np.zeros((max(cap, 1), 3), np.uint8)
+    L = lib()
+    L.orc_depth_to_cloud_bounded.restype = ctypes.c_int
+    L.orc_depth_to_cloud_bounded.argtypes = [_i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                             ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                             _opt(_f32p), _opt(np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")),
+                                             _opt(_u8p), _f32p, _u8p, ctypes.c_int]
+    cnt = L.orc_depth_to_cloud_bounded(
+        depth.reshape(-1), w, h, stride, cx, cy, fx, fy, depth_factor,
+        None if cam_to_world is None else _c(cam_to_world, np.float32).reshape(-1),
+        None if bounds is None else _c(bounds, np.float64).reshape(-1),
+        None if rgb is None else _c(rgb, np.uint8).reshape(-1), xyz.reshape(-1), out_rgb.reshape(-1), cap)
+    return xyz[:cnt].copy(), (out_rgb[:cnt].copy() if rgb is not None else None)
+
+
 def knn1(r_xyz, r_label, o_xyz, label_start=None, label_end=None):
     r_xyz = _c(r_xyz, np.float32).reshape(-1, 3)
     o_xyz = _c(o_xyz, np.float32).reshape(-1, 3)
@@ -240,3 +261,23 @@ def evaluate_icp(tris, tris_model_count, poses, pose_model, pose_label, width, h
         _c(label_end, np.int32), nl, _c(pose_obs_total, np.float32), cost_type, int(calc_obs), sensor_resolution, k,
         max_iter, rot_eps, trans_eps, adj.reshape(-1), iters, rc, oc, df, nthreads)
     return adj, iters, rc, oc, df
+
+
+def pose_distances(pts, T_gt, T_est, chunk=2048):
+    """ADD / ADD-S per pose pair, float64 brute force (pose_error.py:72-108; fat_pose_image.py:2116-2136):
+    ADD = mean_i |G p_i - E p_i|, ADD-S = mean_i min_j |G p_i - E p_j|."""
+    P = np.asarray(pts, np.float64).reshape(-1, 3)
+    G = np.asarray(T_gt, np.float64).reshape(-1, 4, 4)
+    E = np.asarray(T_est, np.float64).reshape(-1, 4, 4)
+    add = np.zeros(len(G))
+    adds = np.zeros(len(G))
+    for m in range(len(G)):
+        a = P @ G[m, :3, :3].T + G[m, :3, 3]
+        b = P @ E[m, :3, :3].T + E[m, :3, 3]
+        add[m] = np.linalg.norm(a - b, axis=1).mean()
+        best = np.empty(len(a))
+        for c0 in range(0, len(a), chunk):
+            d = ((a[c0:c0 + chunk, None, :] - b[None, :, :]) ** 2).sum(-1)
+            best[c0:c0 + chunk] = np.sqrt(d.min(1))
+        adds[m] = best.mean()
+    return add, adds

@@ -238,6 +238,42 @@ int orc_depth_to_cloud(const int32_t* depth, int num_poses, int width, int heigh
     return count;
 }
 
+// depth2cloud_global with camera_transform + observed_cloud_bounds (3-DoF; compute_point_clouds.cuh:14-35,
+// 79-91, 125-157): keep a pixel when its world point (R p left to right, then + t, in float) is inside the
+// bounds (x_max, x_min, y_max, y_min, z_max, z_min as floats); emit the CAMERA-frame point and its colour.
+int orc_depth_to_cloud_bounded(const int32_t* depth, int width, int height, int stride, float cx, float cy, float fx,
+                               float fy, float depth_factor, const float* cam_to_world, const double* bounds,
+                               const uint8_t* rgb, float* out_xyz, uint8_t* out_rgb, int cap) {
+    int count = 0;
+    float b[6];
+    for (int i = 0; i < 6; i++) b[i] = bounds ? (float)bounds[i] : 0.0f;
+    for (int y = 0; y < height; y += stride)
+        for (int x = 0; x < width; x += stride) {
+            const size_t idx = (size_t)x + (size_t)y * width;
+            if (depth[idx] <= 0) continue;
+            float xp, yp, zp;
+            transform_point(x, y, depth[idx], cx, cy, fx, fy, depth_factor, xp, yp, zp);
+            if (cam_to_world != nullptr) {
+                const float* m = cam_to_world;
+                const float wx = (m[0] * xp + m[1] * yp + m[2] * zp) + m[3];
+                const float wy = (m[4] * xp + m[5] * yp + m[6] * zp) + m[7];
+                const float wz = (m[8] * xp + m[9] * yp + m[10] * zp) + m[11];
+                if (wx > b[0] || wx < b[1]) continue;
+                if (wy > b[2] || wy < b[3]) continue;
+                if (wz > b[4] || wz < b[5]) continue;
+            }
+            if (count < cap) {
+                out_xyz[3 * (size_t)count + 0] = xp;
+                out_xyz[3 * (size_t)count + 1] = yp;
+                out_xyz[3 * (size_t)count + 2] = zp;
+                if (out_rgb != nullptr && rgb != nullptr)
+                    for (int ch = 0; ch < 3; ch++) out_rgb[3 * (size_t)count + ch] = rgb[3 * idx + ch];
+            }
+            count++;
+        }
+    return count;
+}
+
 void orc_knn1(const float* r_xyz, const int32_t* r_label, int num_r, const float* o_xyz, int num_o,
               const int32_t* label_start, const int32_t* label_end, int num_labels, float* out_d2, int32_t* out_idx) {
 #pragma omp parallel for schedule(static)

@@ -48,6 +48,11 @@ int orc_depth_to_cloud(const int32_t* depth, int num_poses, int width, int heigh
                        float cx, float cy, float fx, float fy, float depth_factor,
                        const uint8_t* label_mask, const int32_t* pose_label,
                        float* out_xyz, int32_t* out_pose, int32_t* out_label, int cap);
+/* depth2cloud_global with camera_transform + observed_cloud_bounds (3-DoF): camera-frame points of the
+ * pixels whose world point lies inside bounds; colours copied from rgb (H x W x 3, nullable). */
+int orc_depth_to_cloud_bounded(const int32_t* depth, int width, int height, int stride, float cx, float cy, float fx,
+                               float fy, float depth_factor, const float* cam_to_world, const double* bounds,
+                               const uint8_t* rgb, float* out_xyz, uint8_t* out_rgb, int cap);
 
 /* fast_gicp::brute_force_knn_search(k=1) as called at renderer.cu:1852-1871 (label-restricted
  * via observed_label_indices).  Build-owned spec: squared distance ((dx*dx + dy*dy) + dz*dz),

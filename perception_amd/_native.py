@@ -26,7 +26,8 @@ EXPORTED_SYMBOLS = (
     "pcore_create", "pcore_destroy", "pcore_last_error", "pcore_abi_version", "pcore_upload_meshes",
     "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_evaluate_icp",
     "pcore_render",
-    "pcore_depth_to_cloud", "pcore_select",
+    "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
+    "pcore_observed_cloud_bounded",
 )
 
 
@@ -103,6 +104,9 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     L.pcore_depth_to_cloud.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, i32,
                                        ctypes.POINTER(i32), vp]
     L.pcore_select.argtypes = [vp, vp, vp, vp, i32, i64, i32, vp, vp]
+    L.pcore_pose_distances.argtypes = [vp, vp, i32, vp, vp, i32, vp, vp, vp]
+    L.pcore_observed_cloud_bounded.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, vp, vp, vp, i32,
+                                               ctypes.POINTER(i32), vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("pcore_destroy", "pcore_last_error"):
             getattr(L, name).restype = ctypes.c_int

@@ -7,7 +7,7 @@ current stream.  There is no CPU fallback: a missing libpcore.so or a non-GPU te
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -101,6 +101,27 @@ class PoseCore:
             ctypes.byref(cnt), _stream(stream)))
         n = cnt.value
         return xyz[:n], lab[:n]
+
+    def observed_cloud_bounded(self, depth: torch.Tensor, stride: int, depth_factor: float,
+                               cam_to_world: Optional[np.ndarray] = None, bounds: Optional[Sequence[float]] = None,
+                               rgb: Optional[torch.Tensor] = None, stream=None
+                               ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """3-DoF depth2cloud_global: camera-frame points of the pixels whose world point (cam_to_world, 4x4)
+        lies inside bounds = (x_max, x_min, y_max, y_min, z_max, z_min); with `rgb` (H, W, 3) uint8 also the
+        points' colours.  Returns (xyz (P,3) f32, rgb (P,3) u8 or None) on the GPU."""
+        h, w = depth.shape[-2:]
+        cap = ((w + stride - 1) // stride) * ((h + stride - 1) // stride)
+        xyz = torch.empty((max(cap, 1), 3), dtype=torch.float32, device=depth.device)
+        out_rgb = torch.empty((max(cap, 1), 3), dtype=torch.uint8, device=depth.device) if rgb is not None else None
+        M = None if cam_to_world is None else (ctypes.c_float * 16)(*np.asarray(cam_to_world, np.float32).reshape(16))
+        B = None if bounds is None else (ctypes.c_double * 6)(*np.asarray(bounds, np.float64).reshape(6))
+        cnt = ctypes.c_int32(0)
+        self._check(self.lib.pcore_observed_cloud_bounded(
+            self._h, _ptr(depth, torch.int32, "depth"), _ptr(None if rgb is None else rgb.contiguous(), torch.uint8, "rgb"),
+            w, h, stride, float(depth_factor), M, B, _ptr(xyz, torch.float32, "xyz"),
+            _ptr(out_rgb, torch.uint8, "out_rgb"), cap, ctypes.byref(cnt), _stream(stream)))
+        n = cnt.value
+        return xyz[:n], (out_rgb[:n] if out_rgb is not None else None)
 
     def set_observation(self, src_depth_cm: torch.Tensor, src_mask: Optional[torch.Tensor],
                         obs_xyz: torch.Tensor, obs_label: Optional[torch.Tensor], sensor_resolution: float,

@@ -69,6 +69,8 @@ struct pcore_ctx {
     DevBuf<float4> icp_cloud;
     DevBuf<int32_t> icp_count;
     DevBuf<double> icp_cov;
+    DevBuf<int32_t> icp_counter;
+    DevBuf<double> metric_part;  // ADD / ADD-S per-block partial sums
     // scratch (parity stages)
     DevBuf<int32_t> scratch_counts, scratch_offsets, scratch_total;
 };
@@ -282,7 +284,8 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter);
+    (void)dev_free(c->metric_part);
     delete c;
 }
 
@@ -377,6 +380,45 @@ int pcore_observed_cloud(pcore_ctx* c, const int32_t* d_depth, const uint8_t* d_
     if (!c->have_cam) return fail(c, PCORE_E_STATE, "observed_cloud: camera not set");
     return pcore_depth_to_cloud(c, d_depth, 1, width, height, stride, depth_factor, d_label_mask, nullptr, d_out_xyz,
                                 nullptr, d_out_label, cap, out_count, stream);
+}
+
+int pcore_observed_cloud_bounded(pcore_ctx* c, const int32_t* d_depth, const uint8_t* d_rgb, int32_t width,
+                                 int32_t height, int32_t stride, float depth_factor, const float* cam_to_world,
+                                 const double* bounds, float* d_out_xyz, uint8_t* d_out_rgb, int32_t cap,
+                                 int32_t* out_count, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!c->have_cam) return fail(c, PCORE_E_STATE, "observed_cloud_bounded: camera not set");
+    if (width <= 0 || height <= 0 || stride <= 0 || !d_depth || cap < 0 || (cap > 0 && !d_out_xyz) || !out_count ||
+        (!cam_to_world) != (!bounds) || (d_out_rgb && !d_rgb))
+        return fail(c, PCORE_E_INVALID_ARG, "observed_cloud_bounded: bad arguments");
+    if (width % stride != 0) return fail(c, PCORE_E_INVALID_ARG, "observed_cloud_bounded: width % stride != 0");
+    CloudBounds cb{};
+    if (cam_to_world) {
+        cb.on = 1;
+        for (int i = 0; i < 12; i++) cb.m[i] = cam_to_world[i];
+        for (int i = 0; i < 6; i++) cb.b[i] = (float)bounds[i];
+        cb.cx = c->cam.cx;
+        cb.cy = c->cam.cy;
+        cb.fx = c->cam.fx;
+        cb.fy = c->cam.fy;
+        cb.depth_factor = depth_factor;
+    }
+    *out_count = 0;
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(c, dev_reserve(c->scratch_counts, 1));
+    HIPC(c, dev_reserve(c->scratch_offsets, 1));
+    HIPC(c, dev_reserve(c->scratch_total, 1));
+    HIPC(c, launch_cloud_count(d_depth, 1, width, height, stride, nullptr, cb, c->scratch_counts.p, s));
+    HIPC(c, launch_exclusive_scan(c->scratch_counts.p, c->scratch_offsets.p, 1, c->scratch_total.p, s));
+    HIPC(c, launch_cloud_write(d_depth, 1, width, height, stride, c->cam.cx, c->cam.cy, c->cam.fx, c->cam.fy,
+                               depth_factor, nullptr, nullptr, c->scratch_offsets.p, d_out_xyz, nullptr, nullptr, cap,
+                               cb, d_rgb, d_out_rgb, s));
+    int32_t total = 0;
+    HIPC(c, hipMemcpyAsync(&total, c->scratch_total.p, 4, hipMemcpyDeviceToHost, s));
+    HIPC(c, hipStreamSynchronize(s));
+    *out_count = total;
+    return PCORE_OK;
 }
 
 int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uint8_t* d_src_mask,
@@ -642,13 +684,17 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         c->cov_k_all = k;
     }
     const int nsamp = ws * hs;
-    // equal chunks of <= 8192 poses (8192 x 4800 slots: 0.5 GB clouds + 1.9 GB covariances), so no chunk
-    // is a short tail that leaves most of the chip idle
-    const int nchunks = (num_poses + 8191) / 8192;
+    // GICP scratch per pose: nsamp cloud slots (16 B) + covariances (48 B).  Chunks are as large as an
+    // 8 GiB budget allows (26k poses at 640x480 / stride 8) and equal in size: every chunk ends with
+    // the tail of its slowest pose, so fewer chunks mean fewer tails.
+    const size_t per_pose = (size_t)nsamp * 64;
+    const int max_chunk = (int)std::max<size_t>(1, ((size_t)8 << 30) / per_pose);
+    const int nchunks = (num_poses + max_chunk - 1) / max_chunk;
     const int chunk = (num_poses + nchunks - 1) / nchunks;
     HIPC(c, dev_reserve(c->icp_cloud, (size_t)chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_count, (size_t)chunk));
     HIPC(c, dev_reserve(c->icp_cov, (size_t)6 * chunk * nsamp));
+    HIPC(c, dev_reserve(c->icp_counter, 1));
     FusedArgs a;
     fill_fused_args(c, p, a);
     GicpArgs g{};
@@ -669,6 +715,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.max_iter = ip->max_iterations;
     g.rot_eps = ip->rotation_epsilon;
     g.trans_eps = ip->transformation_epsilon;
+    g.work_counter = c->icp_counter.p;
     for (int base = 0; base < num_poses; base += chunk) {
         const int n = std::min(chunk, num_poses - base);
         a.poses = d_poses + (size_t)16 * base;
@@ -728,11 +775,13 @@ int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses
     HIPC(c, dev_reserve(c->scratch_counts, num_poses));
     HIPC(c, dev_reserve(c->scratch_offsets, num_poses));
     HIPC(c, dev_reserve(c->scratch_total, 1));
-    HIPC(c, launch_cloud_count(d_depth, num_poses, width, height, stride, d_label_mask, c->scratch_counts.p, s));
+    const CloudBounds no_bounds{};
+    HIPC(c, launch_cloud_count(d_depth, num_poses, width, height, stride, d_label_mask, no_bounds,
+                               c->scratch_counts.p, s));
     HIPC(c, launch_exclusive_scan(c->scratch_counts.p, c->scratch_offsets.p, num_poses, c->scratch_total.p, s));
     HIPC(c, launch_cloud_write(d_depth, num_poses, width, height, stride, c->cam.cx, c->cam.cy, c->cam.fx, c->cam.fy,
                                depth_factor, d_label_mask, d_pose_label, c->scratch_offsets.p, d_out_xyz, d_out_pose,
-                               d_out_label, cap, s));
+                               d_out_label, cap, no_bounds, nullptr, nullptr, s));
     int32_t total = 0;
     HIPC(c, hipMemcpyAsync(&total, c->scratch_total.p, 4, hipMemcpyDeviceToHost, s));
     HIPC(c, hipStreamSynchronize(s));
@@ -749,6 +798,20 @@ int pcore_select(pcore_ctx* c, const float* d_rc, const float* d_oc, const int32
     if (num_poses == 0) return PCORE_OK;
     HIPC(c, hipSetDevice(c->device));
     HIPC(c, launch_select(d_rc, d_oc, d_pose_model, num_poses, index_base, num_models, d_keys, (hipStream_t)stream));
+    return PCORE_OK;
+}
+
+int pcore_pose_distances(pcore_ctx* c, const float* d_pts, int32_t n, const double* d_T_gt, const double* d_T_est,
+                         int32_t num_pairs, double* d_add, double* d_adds, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (n <= 0 || num_pairs < 0 || (num_pairs > 0 && (!d_pts || !d_T_gt || !d_T_est)))
+        return fail(c, PCORE_E_INVALID_ARG, "pose_distances: need n > 0 points and pose pointers");
+    if (num_pairs == 0 || (!d_add && !d_adds)) return PCORE_OK;
+    if (num_pairs > 65535) return fail(c, PCORE_E_INVALID_ARG, "pose_distances: at most 65535 pairs per call");
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, dev_reserve(c->metric_part, (size_t)2 * num_pairs * pose_dist_blocks(n)));
+    HIPC(c, launch_pose_distances(d_pts, n, d_T_gt, d_T_est, num_pairs, c->metric_part.p, d_add, d_adds,
+                                  (hipStream_t)stream));
     return PCORE_OK;
 }
 

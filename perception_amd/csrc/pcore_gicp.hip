@@ -16,8 +16,9 @@
 //                      concatenate_transforms (renderer.cu:1412-1429).
 #include "pcore_internal.h"
 
-#include <climits>
+#include <algorithm>
 #include <cfloat>
+#include <climits>
 
 #pragma clang fp contract(off)
 
@@ -26,8 +27,18 @@ namespace pcore {
 namespace {
 
 constexpr int kGThreads = 256;
-constexpr int kGWaves = kGThreads / 64;
 constexpr int kMaxK = 16;
+// Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only).
+#ifdef PCORE_GICP_PROFILE
+__device__ unsigned long long g_gicp_prof[4];
+#define GPROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define GPROF_ADD(k, a, b) \
+    if (lane == 0) atomicAdd(&g_gicp_prof[k], (unsigned long long)((b) - (a)))
+#else
+#define GPROF_T(v)
+#define GPROF_ADD(k, a, b)
+#endif
+
 constexpr int kTgtTile = 512;  // targets staged per wave in LDS, SoA (6 KiB)
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -83,10 +94,14 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
                 V[k][q] = ss * vkp + cc * vkq;
             }
         }
+    // smallest eigenvalue's column, first on ties (selects, not a dynamic register index)
     int m = 0;
-    if (A[1][1] < A[m][m]) m = 1;
-    if (A[2][2] < A[m][m]) m = 2;
-    const double n0 = V[0][m], n1 = V[1][m], n2 = V[2][m];
+    double am = A[0][0];
+    if (A[1][1] < am) { m = 1; am = A[1][1]; }
+    if (A[2][2] < am) m = 2;
+    const double n0 = m == 0 ? V[0][0] : (m == 1 ? V[0][1] : V[0][2]);
+    const double n1 = m == 0 ? V[1][0] : (m == 1 ? V[1][1] : V[1][2]);
+    const double n2 = m == 0 ? V[2][0] : (m == 1 ? V[2][1] : V[2][2]);
     out[0] = 1.0 - kPlaneScale * (n0 * n0);
     out[1] = 0.0 - kPlaneScale * (n0 * n1);
     out[2] = 0.0 - kPlaneScale * (n0 * n2);
@@ -184,9 +199,10 @@ hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const i
 // Stage tn targets into a wave's SoA tile, padded to a multiple of 4 with +inf.  A non-finite target
 // (never the nearest in the oracle's scan: its distance is NaN or inf) is staged as +inf too, so no
 // distance in the packed scan is NaN for a finite query.
-__device__ __forceinline__ void stage_targets(TgtTile& T, const float4* tgt, int tn, int lane) {
+template <int NT>
+__device__ __forceinline__ void stage_targets(TgtTile& T, const float4* tgt, int tn, int tid) {
     const int tn4 = (tn + 3) & ~3;
-    for (int o = lane; o < tn4; o += 64) {
+    for (int o = tid; o < tn4; o += NT) {
         float4 p = o < tn ? tgt[o] : make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
         if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) p = make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
         T.x[o] = p.x;
@@ -221,9 +237,16 @@ __device__ __forceinline__ void scan_targets(const TgtTile& T, int tn, int t0, f
     }
 }
 
+__device__ __forceinline__ void load_source(const float4* src, const double* scov, int i, float4& sp, double (&cs)[6]) {
+    sp = src[i];
+    const double2* c2 = reinterpret_cast<const double2*>(scov + (size_t)6 * i);
+    const double2 a = c2[0], b = c2[1], c = c2[2];
+    cs[0] = a.x; cs[1] = a.y; cs[2] = b.x; cs[3] = b.y; cs[4] = c.x; cs[5] = c.y;
+}
+
 // One point's Gauss-Newton contribution (orc gicp_contrib) given its transformed position q and its
 // correspondence tj / ct: acc[0..20] upper(H), [21..26] b, [27] error.
-__device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double* cs,
+__device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6],
                                              float4 tj, const double* ct, double (&acc)[28]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
@@ -311,136 +334,225 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
     return true;
 }
 
-// One wave per pose, 4 poses per workgroup: no block barriers; the wave's lanes accumulate their
-// points' contributions sequentially (point i -> lane i % 64), a shuffle-down tree reduces them to
-// lane 0, which solves and updates; other waves of the CU hide the serial solve.
-__global__ void __launch_bounds__(kGThreads) gicp_kernel(GicpArgs g, int num_poses) {
-    __shared__ double sRT[kGWaves][12];
-    __shared__ TgtTile sT[kGWaves];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int pose = __builtin_amdgcn_readfirstlane(blockIdx.x * kGWaves + wave);  // chunk-local, wave-uniform
-    if (pose >= num_poses) return;
-    const int gp = g.pose_base + pose;
-    const int ns = g.src_count[pose];
-    const float4* src = g.src + (size_t)pose * g.src_cap;
-    const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
-    int seg = g.whole_seg;
-    if (g.pose_label) {
-        const int pl = g.pose_label[gp];
-        seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
-    }
-    seg = __builtin_amdgcn_readfirstlane(seg);
-    const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
-    const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
-    const double* tcov = g.tgt_cov + (size_t)6 * lo;
-    const float4* tgt = g.tgt + lo;
-    double* RT = sRT[wave];
-    TgtTile& T = sT[wave];
-    const bool resident = nt <= kTgtTile;  // the whole segment stays in LDS for all iterations
-    if (resident) stage_targets(T, tgt, min(nt, kTgtTile), lane);
-    if (lane == 0) {
-        for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
-    }
-    int iters = 0;
-    bool done = ns <= 0 || nt <= 0;
-    for (int it = 0; it < g.max_iter && !done; it++) {
+// Synchronise the WPP waves that share one pose: LDS writes of any lane visible to all of them.
+template <int WPP>
+__device__ __forceinline__ void group_sync() {
+    if constexpr (WPP == 1)
         wave_lds_sync();
-        double R[3][3], t[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-#pragma unroll
-            for (int c = 0; c < 3; c++) R[r][c] = RT[3 * r + c];
-            t[r] = RT[9 + r];
+    else
+        __syncthreads();
+}
+
+// One pose per workgroup of WPP waves; persistent workgroups pull poses from a counter.  The group's
+// threads accumulate their points' contributions sequentially (point i -> thread i % (64 WPP)), each
+// wave reduces with a shuffle-down tree, thread 0 adds the wave sums in order, solves and updates.
+// The per-pose iteration chain is latency-bound, so the slowest pose sets a chunk's tail; WPP > 1
+// splits each iteration's scan over more lanes.
+#ifndef PCORE_GICP_WAVES_PER_EU
+#define PCORE_GICP_WAVES_PER_EU 2
+#endif
+#ifndef PCORE_GICP_WPP
+#define PCORE_GICP_WPP 1
+#endif
+constexpr int kGicpWpp = PCORE_GICP_WPP;  // must match kGicpThreads / 64 of orc_gicp
+
+template <int WPP>
+__global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
+gicp_kernel(GicpArgs g, int num_poses) {
+    constexpr int NT = 64 * WPP;
+    __shared__ double RT[12];
+    __shared__ TgtTile T;
+    __shared__ double sPart[WPP][28];
+    __shared__ int sPose, sFlag;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (;;) {
+        group_sync<WPP>();  // the previous pose's reads of the shared state are done
+        if (tid == 0) sPose = atomicAdd(g.work_counter, 1);
+        group_sync<WPP>();
+        const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
+        if (pose >= num_poses) break;
+        const int gp = g.pose_base + pose;
+        const int ns = g.src_count[pose];
+        const float4* src = g.src + (size_t)pose * g.src_cap;
+        const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
+        int seg = g.whole_seg;
+        if (g.pose_label) {
+            const int pl = g.pose_label[gp];
+            seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
         }
-        double acc[28];
+        seg = __builtin_amdgcn_readfirstlane(seg);
+        const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
+        const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
+        const double* tcov = g.tgt_cov + (size_t)6 * lo;
+        const float4* tgt = g.tgt + lo;
+        const bool resident = nt <= kTgtTile;  // the whole segment stays in LDS for all iterations
+        if (resident) stage_targets<NT>(T, tgt, min(nt, kTgtTile), tid);
+        if (tid == 0) {
+            for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
+        }
+        int iters = 0;
+        bool done = ns <= 0 || nt <= 0;
+        for (int it = 0; it < g.max_iter && !done; it++) {
+            group_sync<WPP>();
+            GPROF_T(t_a);
+            double R[3][3], t[3];
 #pragma unroll
-        for (int v = 0; v < 28; v++) acc[v] = 0.0;
-        for (int i0 = 0; i0 < ns; i0 += 64) {
-            const int i = i0 + lane;
-            const bool act = i < ns;
-            const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-            double q[3];
+            for (int r = 0; r < 3; r++) {
 #pragma unroll
-            for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
-            const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
-            // nearest target: first strict minimum of the float squared distance (orc gicp_nn)
-            int j = -1;
-            float best = INFINITY;
-            for (int t0 = 0; t0 < nt; t0 += kTgtTile) {
-                const int tn = min(kTgtTile, nt - t0);
-                if (!resident) {
-                    wave_lds_sync();
-                    stage_targets(T, tgt + t0, tn, lane);
-                    wave_lds_sync();
-                }
-                scan_targets(T, tn, t0, qx, qy, qz, best, j);
+                for (int c = 0; c < 3; c++) R[r][c] = RT[3 * r + c];
+                t[r] = RT[9 + r];
             }
-            if (act && j >= 0) gicp_contrib(R, q, scov + (size_t)6 * i, tgt[j], tcov + (size_t)6 * j, acc);
-        }
+            double acc[28];
 #pragma unroll
-        for (int v = 0; v < 28; v++) {
-            double x = acc[v];
+            for (int v = 0; v < 28; v++) acc[v] = 0.0;
+            // rounds of NT source points; the next round's point and covariance are loaded while this
+            // round scans
+            float4 sp_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            double cs_n[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            if (tid < ns) load_source(src, scov, tid, sp_n, cs_n);
+            for (int i0 = 0; i0 < ns; i0 += NT) {
+                const int i = i0 + tid;
+                const bool act = i < ns;
+                const float4 sp = sp_n;
+                double cs[6];
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
-            acc[v] = x;
-        }
-        int flag = 0;  // 0 continue, 1 stop (no update), 2 stop after update
-        if (lane == 0) {
-            double d[6];
-            if (!ldlt_solve6(acc, acc + 21, d)) {
-                flag = 1;
-            } else {
-                double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
-                const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
-                const double inv = 1.0 / nrm;
-                qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
-                const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
-                const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
-                const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
-                                         {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
-                                         {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
-                double dr = 0.0, dt = 0.0;
-                for (int r = 0; r < 3; r++) {
-                    for (int c = 0; c < 3; c++) {
-                        RT[3 * r + c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
-                        const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
-                        dr = v > dr ? v : dr;
+                for (int k = 0; k < 6; k++) cs[k] = cs_n[k];
+                if (i + NT < ns) load_source(src, scov, i + NT, sp_n, cs_n);
+                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+                double q[3];
+#pragma unroll
+                for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
+                const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
+                // nearest target: first strict minimum of the float squared distance (orc gicp_nn)
+                int j = -1;
+                float best = INFINITY;
+                for (int t0 = 0; t0 < nt; t0 += kTgtTile) {
+                    const int tn = min(kTgtTile, nt - t0);
+                    if (!resident) {
+                        group_sync<WPP>();
+                        stage_targets<NT>(T, tgt + t0, tn, tid);
+                        group_sync<WPP>();
                     }
-                    RT[9 + r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
-                    const double v = fabs(d[3 + r]);
-                    dt = v > dt ? v : dt;
+                    scan_targets(T, tn, t0, qx, qy, qz, best, j);
                 }
-                flag = (dr < g.rot_eps && dt < g.trans_eps) ? 2 : 0;
+                if (act && j >= 0) {
+                    // a selected target is finite, so the staged copy equals the original
+                    const float4 tj = resident ? make_float4(T.x[j], T.y[j], T.z[j], 0.0f) : tgt[j];
+                    gicp_contrib(R, q, cs, tj, tcov + (size_t)6 * j, acc);
+                }
             }
+            GPROF_T(t_b);
+#pragma unroll
+            for (int v = 0; v < 28; v++) {
+                double x = acc[v];
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
+                acc[v] = x;
+            }
+            if constexpr (WPP > 1) {
+                if (lane == 0) {
+#pragma unroll
+                    for (int v = 0; v < 28; v++) sPart[wave][v] = acc[v];
+                }
+                __syncthreads();
+                if (tid == 0) {
+#pragma unroll
+                    for (int v = 0; v < 28; v++) {
+                        double x = sPart[0][v];
+                        for (int w = 1; w < WPP; w++) x = x + sPart[w][v];
+                        acc[v] = x;
+                    }
+                }
+            }
+            GPROF_T(t_c);
+            if (tid == 0) {
+                int flag = 0;  // 0 continue, 1 stop (no update), 2 stop after update
+                double d[6];
+                if (!ldlt_solve6(acc, acc + 21, d)) {
+                    flag = 1;
+                } else {
+                    double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
+                    const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+                    const double inv = 1.0 / nrm;
+                    qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
+                    const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
+                    const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
+                    const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
+                                             {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
+                                             {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
+                    double dr = 0.0, dt = 0.0;
+                    for (int r = 0; r < 3; r++) {
+                        for (int c = 0; c < 3; c++) {
+                            RT[3 * r + c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
+                            const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
+                            dr = v > dr ? v : dr;
+                        }
+                        RT[9 + r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
+                        const double v = fabs(d[3 + r]);
+                        dt = v > dt ? v : dt;
+                    }
+                    flag = (dr < g.rot_eps && dt < g.trans_eps) ? 2 : 0;
+                }
+                sFlag = flag;
+            }
+            group_sync<WPP>();
+            const int flag = __builtin_amdgcn_readfirstlane(sFlag);
+            GPROF_T(t_d);
+            GPROF_ADD(0, t_a, t_b);
+            GPROF_ADD(1, t_b, t_c);
+            GPROF_ADD(2, t_c, t_d);
+            if (flag != 1) iters++;
+            done = flag != 0;
         }
-        flag = __shfl(flag, 0, 64);
-        if (flag != 1) iters++;
-        done = flag != 0;
-    }
-    wave_lds_sync();
-    if (lane == 0) {
-        // concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
-        const float* pin = g.poses_in + (size_t)16 * gp;
-        float A[4][4], Tf[4][4];
-        for (int r = 0; r < 4; r++)
-            for (int c = 0; c < 4; c++) {
-                A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
-                Tf[r][c] = r < 3 ? (float)(c < 3 ? RT[3 * r + c] : RT[9 + r]) : (c == 3 ? 1.0f : 0.0f);
-            }
-        float* pout = g.poses_out + (size_t)16 * gp;
-        for (int r = 0; r < 4; r++)
-            for (int c = 0; c < 4; c++) {
-                const float p = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
-                pout[4 * r + c] = r < 3 ? (float)((double)p * 100) : p;
-            }
-        if (g.iters_out) g.iters_out[gp] = iters;
+        group_sync<WPP>();
+        if (tid == 0) {
+            // concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
+            const float* pin = g.poses_in + (size_t)16 * gp;
+            float A[4][4], Tf[4][4];
+            for (int r = 0; r < 4; r++)
+                for (int c = 0; c < 4; c++) {
+                    A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
+                    Tf[r][c] = r < 3 ? (float)(c < 3 ? RT[3 * r + c] : RT[9 + r]) : (c == 3 ? 1.0f : 0.0f);
+                }
+            float* pout = g.poses_out + (size_t)16 * gp;
+            for (int r = 0; r < 4; r++)
+                for (int c = 0; c < 4; c++) {
+                    const float p = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
+                    pout[4 * r + c] = r < 3 ? (float)((double)p * 100) : p;
+                }
+            if (g.iters_out) g.iters_out[gp] = iters;
+        }
     }
 }
 
+#ifdef PCORE_GICP_PROFILE
+extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gicp_prof), sizeof(unsigned long long) * 4);
+    if (e == hipSuccess && reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_gicp_prof), z, sizeof(z));
+    }
+    return e == hipSuccess ? 0 : 1;
+}
+#endif
+
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gicp_kernel, dim3((num_poses + kGWaves - 1) / kGWaves), dim3(kGThreads), 0, s, g, num_poses);
+    static int resident_wgs = 0;  // workgroups the whole device holds at once (occupancy x CUs)
+    if (resident_wgs == 0) {
+        int dev = 0, per_cu = 0;
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipGetDeviceProperties(&prop, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gicp_kernel<kGicpWpp>, 64 * kGicpWpp, 0);
+        if (e != hipSuccess) return e;
+        resident_wgs = std::max(1, per_cu) * prop.multiProcessorCount;
+    }
+    const int wgs = std::min(resident_wgs, num_poses);
+    hipError_t e = hipMemsetAsync(g.work_counter, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gicp_kernel<kGicpWpp>, dim3(wgs), dim3(64 * kGicpWpp), 0, s, g, num_poses);
     return hipGetLastError();
 }
 

@@ -92,6 +92,7 @@ struct GicpArgs {
     int32_t pose_base;        // first batch index of this chunk
     int32_t max_iter;
     double rot_eps, trans_eps;
+    int32_t* work_counter;    // device int, zeroed by launch_gicp (persistent-wave pose queue)
 };
 
 // launchers (pcore_kernels.hip)
@@ -99,6 +100,10 @@ hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s);
 hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const int32_t* seg_cnt, int seg_stride,
                               int num_segs, int k, double* cov_out, hipStream_t s);
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s);
+// pcore_metrics.hip
+int pose_dist_blocks(int n);
+hipError_t launch_pose_distances(const float* pts, int n, const double* T_gt, const double* T_est, int pairs,
+                                 double* part, double* out_add, double* out_adds, hipStream_t s);
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
 size_t fused_lds_bytes(int ws, int hs, int bitmap_words);
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
@@ -108,13 +113,23 @@ hipError_t launch_render_finalize(int32_t* depth, const int32_t* src_depth, cons
                                   const int32_t* pose_label, int num_poses, int width, int height,
                                   float occlusion_threshold, hipStream_t s);
 hipError_t launch_fill_i32(int32_t* p, int32_t v, size_t n, hipStream_t s);
+// 3-DoF world-frame bounds of depth2cloud_global (compute_point_clouds.cuh:79-91, 125-133): a pixel is
+// kept when its camera-frame point, moved to the world by m (3 x 4 row-major, camera_transform), lies
+// inside [b1, b0] x [b3, b2] x [b5, b4] (the reference's xmax, xmin, ymax, ymin, zmax, zmin, as floats).
+struct CloudBounds {
+    int32_t on;
+    float m[12];
+    float b[6];
+    float cx, cy, fx, fy, depth_factor;
+};
 hipError_t launch_cloud_count(const int32_t* depth, int num_poses, int width, int height, int stride,
-                              const uint8_t* label_mask, int32_t* counts, hipStream_t s);
+                              const uint8_t* label_mask, const CloudBounds& cb, int32_t* counts, hipStream_t s);
 hipError_t launch_exclusive_scan(const int32_t* in, int32_t* out, int n, int32_t* total, hipStream_t s);
 hipError_t launch_cloud_write(const int32_t* depth, int num_poses, int width, int height, int stride, float cx,
                               float cy, float fx, float fy, float depth_factor, const uint8_t* label_mask,
                               const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose,
-                              int32_t* label, int cap, hipStream_t s);
+                              int32_t* label, int cap, const CloudBounds& cb, const uint8_t* rgb_in,
+                              uint8_t* rgb_out, hipStream_t s);
 hipError_t launch_sample_source(const int32_t* src_depth, const uint8_t* src_mask, int width, int height,
                                 int stride, int32_t* src_s, uint8_t* lab_s, hipStream_t s);
 hipError_t launch_select(const float* rc, const float* oc, const int32_t* pose_model, int num_poses,

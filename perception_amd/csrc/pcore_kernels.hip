@@ -710,22 +710,39 @@ hipError_t launch_render_finalize(int32_t* depth, const int32_t* src_depth, cons
 // Stage CLOUD / depth2cloud_global (compute_point_clouds.cuh:37-184, 265-346)
 // ------------------------------------------------------------------------------------------------
 
-__device__ __forceinline__ bool cloud_valid(const int32_t* depth, const uint8_t* label_mask, size_t idx) {
+__device__ __forceinline__ bool cloud_valid(const int32_t* depth, const uint8_t* label_mask, size_t idx, int x, int y,
+                                            const CloudBounds& cb) {
     if (depth[idx] <= 0) return false;                                 // :64, :123
     if (label_mask != nullptr && label_mask[idx] <= 0) return false;  // :74, :127
+    if (cb.on) {
+        // transform_point with camera_transform (:14-35): camera point, then R p (left to right) + t
+        const float zc = (float)depth[idx] / cb.depth_factor;
+        const float xc = ((float)x - cb.cx) / cb.fx * zc;
+        const float yc = ((float)y - cb.cy) / cb.fy * zc;
+        float w[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            w[r] = cb.m[4 * r] * xc + cb.m[4 * r + 1] * yc + cb.m[4 * r + 2] * zc;
+            w[r] = w[r] + cb.m[4 * r + 3];
+        }
+        if (w[0] > cb.b[0] || w[0] < cb.b[1]) return false;  // :86-88, :130-132
+        if (w[1] > cb.b[2] || w[1] < cb.b[3]) return false;
+        if (w[2] > cb.b[4] || w[2] < cb.b[5]) return false;
+    }
     return true;
 }
 
 // one block per image: number of valid stride samples
 __global__ void cloud_count_kernel(const int32_t* depth, int width, int height, int stride, const uint8_t* label_mask,
-                                   int32_t* counts) {
+                                   CloudBounds cb, int32_t* counts) {
     const int n = blockIdx.x;
     const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
     const size_t npx = (size_t)width * height;
     int c = 0;
     for (int k = threadIdx.x; k < ws * hs; k += blockDim.x) {
         const int ky = k / ws, kx = k - ky * ws;
-        c += cloud_valid(depth, label_mask, npx * n + (size_t)(kx * stride) + (size_t)(ky * stride) * width) ? 1 : 0;
+        c += cloud_valid(depth, label_mask, npx * n + (size_t)(kx * stride) + (size_t)(ky * stride) * width,
+                         kx * stride, ky * stride, cb) ? 1 : 0;
     }
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
     __shared__ int part[16];
@@ -771,7 +788,8 @@ __global__ void exclusive_scan_kernel(const int32_t* in, int32_t* out, int n, in
 __global__ void cloud_write_kernel(const int32_t* depth, int width, int height, int stride, float cx, float cy,
                                    float fx, float fy, float depth_factor, const uint8_t* label_mask,
                                    const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose_out,
-                                   int32_t* label_out, int cap) {
+                                   int32_t* label_out, int cap, CloudBounds cb, const uint8_t* rgb_in,
+                                   uint8_t* rgb_out) {
     __shared__ int wsum[16];
     __shared__ int carry_s;
     const int n = blockIdx.x;
@@ -788,7 +806,7 @@ __global__ void cloud_write_kernel(const int32_t* depth, int width, int height, 
         if (k < ws * hs) {
             ky = k / ws; kx = k - ky * ws;
             idx = npx * n + (size_t)(kx * stride) + (size_t)(ky * stride) * width;
-            v = cloud_valid(depth, label_mask, idx);
+            v = cloud_valid(depth, label_mask, idx, kx * stride, ky * stride, cb);
         }
         const uint64_t b = __ballot(v);
         if (lane == 0) wsum[wave] = __popcll(b);
@@ -810,6 +828,11 @@ __global__ void cloud_write_kernel(const int32_t* depth, int width, int height, 
                 xyz[3 * (size_t)o + 1] = yp;
                 xyz[3 * (size_t)o + 2] = zp;
                 if (pose_out) pose_out[o] = n;
+                if (rgb_out) {  // depth_to_2d_cloud :155-157, the input image's channels in order
+                    rgb_out[3 * (size_t)o + 0] = rgb_in[3 * idx + 0];
+                    rgb_out[3 * (size_t)o + 1] = rgb_in[3 * idx + 1];
+                    rgb_out[3 * (size_t)o + 2] = rgb_in[3 * idx + 2];
+                }
                 if (label_out) {
                     if (label_mask) label_out[o] = (int32_t)label_mask[idx] - 1;
                     else if (pose_label) label_out[o] = pose_label[n];
@@ -824,10 +847,10 @@ __global__ void cloud_write_kernel(const int32_t* depth, int width, int height, 
 }
 
 hipError_t launch_cloud_count(const int32_t* depth, int num_poses, int width, int height, int stride,
-                              const uint8_t* label_mask, int32_t* counts, hipStream_t s) {
+                              const uint8_t* label_mask, const CloudBounds& cb, int32_t* counts, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;
     hipLaunchKernelGGL(cloud_count_kernel, dim3(num_poses), dim3(256), 0, s, depth, width, height, stride, label_mask,
-                       counts);
+                       cb, counts);
     return hipGetLastError();
 }
 
@@ -839,10 +862,12 @@ hipError_t launch_exclusive_scan(const int32_t* in, int32_t* out, int n, int32_t
 hipError_t launch_cloud_write(const int32_t* depth, int num_poses, int width, int height, int stride, float cx,
                               float cy, float fx, float fy, float depth_factor, const uint8_t* label_mask,
                               const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose,
-                              int32_t* label, int cap, hipStream_t s) {
+                              int32_t* label, int cap, const CloudBounds& cb, const uint8_t* rgb_in,
+                              uint8_t* rgb_out, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;
     hipLaunchKernelGGL(cloud_write_kernel, dim3(num_poses), dim3(256), 0, s, depth, width, height, stride, cx, cy, fx,
-                       fy, depth_factor, label_mask, pose_label, offsets, xyz, pose, label, cap);
+                       fy, depth_factor, label_mask, pose_label, offsets, xyz, pose, label, cap, cb, rgb_in,
+                       rgb_out);
     return hipGetLastError();
 }
 

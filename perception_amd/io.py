@@ -181,10 +181,10 @@ def save_ply(path: str, model: Model, binary: bool = True):
 # ------------------------------------------------------------------------------------------------
 
 def write_poses_txt(path: str, poses_xyz_qxyzw: np.ndarray, decimals: int = 4):
-    """fat_pose_image.py:774-775 writes 'x y z qx qy qz qw' per line (metres)."""
-    with open(path, "w") as f:
-        for p in np.asarray(poses_xyz_qxyzw, np.float64).reshape(-1, 7):
-            f.write(" ".join(f"{v:.{decimals}f}" for v in p) + "\n")
+    """fat_pose_image.py:760-775: np.savetxt(path, np.around(poses, 4)) of rows 'x y z qx qy qz qw'
+    (metres), i.e. '%.18e' fields separated by one space."""
+    rows = np.asarray(poses_xyz_qxyzw, np.float64).reshape(-1, 7)
+    np.savetxt(path, np.around(rows, decimals))
 
 
 def read_poses_txt(path: str) -> np.ndarray:

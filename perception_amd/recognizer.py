@@ -48,6 +48,7 @@ class PerchParams:
     gpu_depth_factor: int = 100              # search_env.h:411
     use_color_cost: bool = False
     color_distance_threshold: float = 15.0
+    use_cylinder_observed: bool = False      # 3-DoF observed totals from the pose's cylinder
     # fast_gicp settings hard-coded at renderer.cu:1696-1699
     icp_k: int = ICP_K
     icp_max_iterations: int = ICP_MAX_ITER
@@ -73,6 +74,7 @@ class ModelMetaData:
     model: Optional[Model] = None
     flipped: bool = False
     symmetric: bool = False
+    symmetry_mode: int = 0                   # 1 = semi-symmetric (yaw grid stops past pi)
     mesh_in_mm: bool = False
     mesh_scaling_factor: float = 1.0
 
@@ -231,6 +233,19 @@ class ObjectRecognizer:
                 states.append((ii, req, p))
         return states
 
+    # -- per-state inputs of the GPU call (GetStateImagesUnifiedGPU, search_env.cpp:1577-1620) -------
+    def _cost_type(self) -> int:
+        return COST_DEPTH_6DOF
+
+    def _pose_labels(self, states) -> Optional[torch.Tensor]:
+        """pose_segmentation_label: the state's required object id (6-DoF)."""
+        return torch.tensor([s[1] for s in states], dtype=torch.int32, device=self.device)
+
+    def _obs_totals(self, states) -> np.ndarray:
+        """pose_observed_points_total: segmented_observed_point_count of the label (6-DoF)."""
+        seg = np.append(self.segmented_count, 0.0)
+        return np.array([seg[min(s[1], len(seg) - 1)] for s in states], np.float32)
+
     def _pose_in_cam(self, states) -> np.ndarray:
         """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576)."""
         cam_z_front = self.camera_pose @ CAM_TO_BODY
@@ -258,9 +273,9 @@ class ObjectRecognizer:
         if mine:
             poses = torch.from_numpy(self._pose_in_cam(mine)).to(self.device)
             pm = torch.tensor([s[0] for s in mine], dtype=torch.int32, device=self.device)
-            pl = torch.tensor([s[1] for s in mine], dtype=torch.int32, device=self.device)
-            seg = np.append(self.segmented_count, 0.0)
-            tot = torch.from_numpy(np.array([seg[min(s[1], len(seg) - 1)] for s in mine], np.float32)).to(self.device)
+            pl = self._pose_labels(mine)
+            tot = torch.from_numpy(self._obs_totals(mine)).to(self.device)
+            cost_type = self._cost_type()
             n = len(mine)
             rc = torch.empty(n, dtype=torch.float32, device=self.device)
             oc = torch.empty_like(rc)
@@ -273,8 +288,9 @@ class ObjectRecognizer:
             for b0 in range(0, n, bs):
                 b1 = min(n, b0 + bs)
                 sl = slice(b0, b1)
+                pls = pl[sl] if pl is not None else None
                 if p.icp_type == 3 and inp.use_icp:
-                    self.core.evaluate_icp(poses[sl], pm[sl], pl[sl], tot[sl], cost_type=COST_DEPTH_6DOF,
+                    self.core.evaluate_icp(poses[sl], pm[sl], pls, tot[sl], cost_type=cost_type,
                                            stride=p.gpu_stride, depth_factor=p.gpu_depth_factor,
                                            sensor_resolution=p.sensor_resolution,
                                            occlusion_threshold=p.gpu_occlusion_threshold, k=p.icp_k,
@@ -283,7 +299,7 @@ class ObjectRecognizer:
                                            transformation_epsilon=p.icp_transformation_epsilon,
                                            out=(adj_all[sl], iters[sl], rc[sl], oc[sl], df[sl]))
                 else:
-                    self.core.evaluate(poses[sl], pm[sl], pl[sl], tot[sl], cost_type=COST_DEPTH_6DOF,
+                    self.core.evaluate(poses[sl], pm[sl], pls, tot[sl], cost_type=cost_type,
                                        stride=p.gpu_stride, depth_factor=p.gpu_depth_factor,
                                        sensor_resolution=p.sensor_resolution,
                                        occlusion_threshold=p.gpu_occlusion_threshold, out=(rc[sl], oc[sl], df[sl]))

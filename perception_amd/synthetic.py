@@ -249,3 +249,80 @@ def default_gt_pose(rng: np.random.Generator, center=(0.03, -0.02, 0.80)) -> np.
     T[:3, :3] = _rot_align_z(np.array([0.3, -0.4, 1.0])) @ _rot_z(0.7)
     T[:3, 3] = center
     return T
+
+
+# ---------------------------------------------------------------------------------------------
+# 3-DoF table-top scenes (f4)
+# ---------------------------------------------------------------------------------------------
+
+CAM_TO_BODY = np.array([[0, 0, 1, 0], [-1, 0, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1]], np.float64)
+
+
+def tabletop_camera_pose(height: float, pitch: float = 0.7) -> np.ndarray:
+    """Camera body pose in the world (x forward, z up) at `height`, pitched down by `pitch` rad."""
+    c, s = np.cos(pitch), np.sin(pitch)
+    T = np.eye(4)
+    T[:3, :3] = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    T[:3, 3] = [0.0, 0.0, height]
+    return T
+
+
+@dataclass
+class TabletopScene:
+    width: int
+    height: int
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+    proj: np.ndarray
+    bank: ModelBank
+    camera_pose: np.ndarray      # body pose in the world
+    world_poses: np.ndarray      # (K, 4, 4) object model frame -> world
+    depth_raw: np.ndarray        # (H, W) int32 at depth_factor
+    rgb: np.ndarray              # (H, W, 3) uint8
+    depth_factor: float
+    table_height: float
+
+
+def make_tabletop_scene(names: Sequence[str], placements: Sequence[Tuple[float, float, float]],
+                        preprocess: Sequence[np.ndarray], render_fn: RenderFn, table_height: float = 0.7,
+                        cam: dict = CAM_640, depth_factor: float = 1000.0, noise_m: float = 0.001,
+                        rng: Optional[np.random.Generator] = None, k: int = 32,
+                        colors: Optional[Sequence[Sequence[int]]] = None) -> TabletopScene:
+    """Objects standing on a table plane z = table_height at (x, y, yaw) (world = ContPose * preprocess),
+    seen by a camera 0.6 m above the table looking down the +x axis.  Depth: the table plane by ray
+    intersection, objects by `render_fn`; colours: the table grey, object k colours[k]."""
+    from .tabletop import yaw_pose_matrix
+    rng = rng or np.random.default_rng(SEED)
+    bank = model_bank(names, k)
+    if colors is not None:
+        for m, c in zip(bank.models, colors):
+            m.colors = np.tile(np.asarray(c, np.uint8), (m.num_tris, 1))
+    W, H = cam["width"], cam["height"]
+    proj = compute_proj(cam["fx"], cam["fy"], cam["cx"], cam["cy"], W, H)
+    cam_pose = tabletop_camera_pose(table_height + 0.6)
+    optical = cam_pose @ CAM_TO_BODY
+    world = np.stack([yaw_pose_matrix(x, y, table_height, yaw) @ pre for (x, y, yaw), pre in zip(placements, preprocess)])
+    in_cam = np.stack([np.linalg.inv(optical) @ T for T in world])
+    zb = render_fn(bank.tris, bank.tris_model_count, init_from_eigen_batch(in_cam), np.arange(len(names), dtype=np.int32),
+                   W, H, proj)
+    # table plane: ray through pixel (u, v) in the optical frame, intersect with z_world = table_height
+    u, v = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
+    ray = np.stack([(u - cam["cx"]) / cam["fx"], (v - cam["cy"]) / cam["fy"], np.ones_like(u)], -1)
+    dz = ray @ optical[2, :3]
+    t = (table_height - optical[2, 3]) / np.where(np.abs(dz) > 1e-9, dz, np.nan)
+    table_m = np.where(t > 0, t, 0.0)
+    table_m = np.nan_to_num(table_m, nan=0.0)
+    depth_m = table_m.copy()
+    rgb = np.zeros((H, W, 3), np.uint8)
+    rgb[table_m > 0] = (90, 90, 90)
+    for obj in range(len(names)):
+        z = zb[obj].astype(np.float64) / 100.0
+        closer = (z > 0) & ((depth_m == 0) | (z < depth_m))
+        depth_m[closer] = z[closer]
+        rgb[closer] = bank.models[obj].colors[0]
+    raw = depth_m * depth_factor + rng.normal(0.0, noise_m * depth_factor, depth_m.shape) * (depth_m > 0)
+    raw = np.clip(np.rint(raw), 0, 65535).astype(np.int32)
+    return TabletopScene(W, H, cam["fx"], cam["fy"], cam["cx"], cam["cy"], proj, bank, cam_pose, world, raw, rgb,
+                         float(depth_factor), float(table_height))

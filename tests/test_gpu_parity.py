@@ -291,12 +291,14 @@ def test_evaluate_icp_3dof_matches_oracle(one_object):
     assert _bits_equal(rc.cpu().numpy(), orc)
 
 
-def test_evaluate_icp_dense_targets_matches_oracle(one_object):
-    """Observed cloud at stride 2 (label segment of ~2k points): the GICP kernel's target tiling path."""
+@pytest.mark.parametrize("obs_stride", [2, 1])
+def test_evaluate_icp_dense_targets_matches_oracle(one_object, obs_stride):
+    """Observed cloud at stride 2 / 1 (label segments of ~2k / ~8k points): the target tiling paths of the
+    GICP and covariance kernels."""
     case, core, t = one_object
     sc = case.scene
-    xyz, lab = core.observed_cloud(t["raw"], t["mask"], 2, sc.depth_factor)
-    oxyz, _, olab = oracle.depth_to_cloud(sc.depth_raw, 2, sc.cx, sc.cy, sc.fx, sc.fy, sc.depth_factor,
+    xyz, lab = core.observed_cloud(t["raw"], t["mask"], obs_stride, sc.depth_factor)
+    oxyz, _, olab = oracle.depth_to_cloud(sc.depth_raw, obs_stride, sc.cx, sc.cy, sc.fx, sc.fy, sc.depth_factor,
                                           label_mask=sc.mask)
     assert _bits_equal(xyz.cpu().numpy(), oxyz) and np.array_equal(lab.cpu().numpy(), olab)
     order = np.argsort(olab, kind="stable")
@@ -324,3 +326,27 @@ def test_evaluate_icp_dense_targets_matches_oracle(one_object):
     assert _bits_equal(adj.cpu().numpy(), oadj)
     assert _bits_equal(rc.cpu().numpy(), orc)
     assert _bits_equal(oc.cpu().numpy(), ooc)
+
+
+def test_observed_cloud_bounded_matches_oracle(one_object):
+    """3-DoF depth2cloud_global: world-frame table bounds filter and colours (f4)."""
+    case, core, t = one_object
+    sc = case.scene
+    rng = np.random.default_rng(11)
+    rgb = rng.integers(0, 256, (sc.height, sc.width, 3), dtype=np.uint8)
+    cam_to_world = np.array([[0, 0, 1, 0.1], [-1, 0, 0, 0.2], [0, -1, 0, 0.9], [0, 0, 0, 1]], np.float32)
+    dev = t["raw"].device
+    for stride in (8, 4):
+        for bounds in (None, [1.0, 0.0, 0.3, -0.3, 1.2, 0.5], [0.9, 0.8, 0.2, 0.1, 1.0, 0.85]):
+            M = None if bounds is None else cam_to_world
+            xyz, col = core.observed_cloud_bounded(t["raw"], stride, sc.depth_factor, M, bounds,
+                                                   rgb=torch.from_numpy(rgb).to(dev))
+            oxyz, ocol = oracle.depth_to_cloud_bounded(sc.depth_raw, stride, sc.cx, sc.cy, sc.fx, sc.fy,
+                                                       sc.depth_factor, M, bounds, rgb)
+            assert len(oxyz) > 0
+            assert _bits_equal(xyz.cpu().numpy(), oxyz)
+            assert np.array_equal(col.cpu().numpy(), ocol)
+    # without bounds the point set equals pcore_observed_cloud without a mask
+    xyz, _ = core.observed_cloud_bounded(t["raw"], 8, sc.depth_factor)
+    ref, _ = core.observed_cloud(t["raw"], None, 8, sc.depth_factor)
+    assert torch.equal(xyz, ref)

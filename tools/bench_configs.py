@@ -20,8 +20,10 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from perception_amd import metrics  # noqa: E402
 from perception_amd import synthetic as syn  # noqa: E402
 from perception_amd import workloads  # noqa: E402
+from perception_amd.model import to_eigen  # noqa: E402
 from perception_amd._native import PCORE_KEY_NONE  # noqa: E402
 from perception_amd.core import decode_keys  # noqa: E402
 
@@ -69,6 +71,22 @@ def run(name, names, per_model, cam, icp, steps, warmup):
         it = out[1].float()
         res["gicp_iters_mean"] = float(it.mean().item())
         res["gicp_iters_max"] = int(it.max().item())
+    # pose accuracy of the selected poses against the synthetic ground truth (f3 metrics, on the GPU)
+    final = (out[0] if icp else w.poses).cpu().numpy()
+    errs_add, errs_adds = [], []
+    for m in range(w.num_models):
+        if idx[m] < 0:
+            errs_add.append(np.inf)
+            errs_adds.append(np.inf)
+            continue
+        est = to_eigen(final[idx[m]]).astype(np.float64)
+        pts = np.unique(w.scene.bank.models[m].tris.reshape(-1, 3), axis=0)
+        a, s_ = metrics.pose_distances(w.core, pts, w.scene.gt_poses[m][None], est[None])
+        errs_add.append(float(a[0]))
+        errs_adds.append(float(s_[0]))
+    res["add_m"] = errs_add
+    res["adds_m"] = errs_adds
+    res["adds_auc"] = metrics.compute_pose_metrics(np.array(errs_adds))["auc"]
     print(json.dumps(res), flush=True)
     del w
     torch.cuda.empty_cache()

@@ -1,0 +1,39 @@
+#!/usr/bin/env python
+"""Per-phase shader clocks of gicp_kernel (build with -DPCORE_GICP_PROFILE, load with PCORE_LIB):
+scan+contributions / 28-term wave reduction / lane-0 solve, per pose-iteration."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from perception_amd import _native, workloads  # noqa: E402
+
+
+def main():
+    w = workloads.build(poses_per_model=10000)
+    lib = _native.load()
+    fn = lib.pcore_debug_gicp_profile
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = (ctypes.c_ulonglong * 4)()
+    w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    adj, iters, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                 stride=w.stride)
+    torch.cuda.synchronize()
+    fn(buf, 0)
+    it = iters.cpu().numpy()
+    total = int(it.sum()) + int((it < 150).sum())  # + the final non-updating solve
+    names = ["scan+contrib", "reduction", "solve"]
+    print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())
+    for k in range(3):
+        print(f"{names[k]:14s} {buf[k] / max(total, 1):10.0f} clk per pose-iteration")
+
+
+if __name__ == "__main__":
+    main()
