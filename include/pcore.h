@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PCORE_ABI_VERSION 1
+#define PCORE_ABI_VERSION 2
 
 enum pcore_status {
     PCORE_OK = 0,
@@ -39,8 +39,9 @@ enum pcore_status {
     PCORE_E_STATE = 4        /* required setup call missing (meshes / camera / observation) */
 };
 
-/* Cost types of render_cuda_multi_unified (renderer.cu:1498): 0 = 3-DoF depth, 1 = 3-DoF RGB-D
- * (CIEDE2000 colour gate; not implemented yet -> PCORE_E_INVALID_ARG), 2 = 6-DoF depth + labels. */
+/* Cost types of render_cuda_multi_unified (renderer.cu:1498): 0 = 3-DoF depth, 1 = 3-DoF RGB-D (a
+ * matched point also needs CIEDE2000 <= color_distance_threshold, compute_costs.cuh:57-159, 222-240;
+ * needs pcore_set_observation_colors), 2 = 6-DoF depth + labels. */
 enum pcore_cost_type { PCORE_COST_DEPTH_3DOF = 0, PCORE_COST_RGBD_3DOF = 1, PCORE_COST_DEPTH_6DOF = 2 };
 
 typedef struct pcore_ctx pcore_ctx;
@@ -62,6 +63,7 @@ typedef struct pcore_eval_params {
     float depth_factor;          /* rendered cm -> metres (the reference passes 100) */
     float sensor_resolution;     /* metres; squared internally like renderer.cu:1877 */
     float occlusion_threshold;   /* 3-DoF source-occlusion threshold in cm (gpu_occlusion_threshold) */
+    float color_distance_threshold; /* cost_type 1: CIEDE2000 gate (renderer.h:247) */
 } pcore_eval_params;
 
 /* ---- lifetime ---------------------------------------------------------------------------------- */
@@ -113,6 +115,14 @@ int pcore_observed_cloud_bounded(pcore_ctx* ctx, const int32_t* d_depth, const u
 int pcore_set_observation(pcore_ctx* ctx, const int32_t* d_src_depth_cm, const uint8_t* d_src_mask,
                           const float* d_obs_xyz, const int32_t* d_obs_label, int32_t num_obs,
                           float sensor_resolution, pcore_stream stream);
+
+/* Colours of the observed points for cost_type 1 (the observed_color argument, renderer.h:236-238):
+ * n x 3 uint8 (DEVICE) in the order of the d_obs_xyz given to pcore_set_observation, channels as the
+ * image (the reference's result_observed_cloud_color planes).  The context converts them to CIE Lab with
+ * the reference's channel order (rgb2lab(c2, c1, c0), compute_costs.cuh:57-88, 214-220).  Valid until the
+ * next pcore_set_observation.  Triangle colours come from pcore_upload_meshes (tri_rgb; 128 grey when
+ * NULL, model.cpp:97-101). */
+int pcore_set_observation_colors(pcore_ctx* ctx, const uint8_t* d_obs_rgb, int32_t num_obs, pcore_stream stream);
 
 /* ---- per-batch hot path ------------------------------------------------------------------------ */
 /* Stage "COST" of render_cuda_multi_unified with do_icp = false: render every pose, unproject at

@@ -281,3 +281,59 @@ def pose_distances(pts, T_gt, T_est, chunk=2048):
             best[c0:c0 + chunk] = np.sqrt(d.min(1))
         adds[m] = best.mean()
     return add, adds
+
+
+def _colour_lib():
+    L = lib()
+    if not getattr(L, "_colour_ready", False):
+        f = ctypes.c_float
+        L.orc_rgb2lab.argtypes = [_u8p, _f32p]
+        L.orc_colour_distance.argtypes = [_f32p, _f32p]
+        L.orc_colour_distance.restype = ctypes.c_double
+        for n in ("orc_sin_f", "orc_cos_f", "orc_exp_f"):
+            getattr(L, n).argtypes = [f]
+            getattr(L, n).restype = f
+        L.orc_atan2_f.argtypes = [f, f]
+        L.orc_atan2_f.restype = f
+        L.orc_evaluate_colour.argtypes = [
+            _f32p, ctypes.c_int, _u8p, _i32p, ctypes.c_int, _f32p, _i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+            _f32p, _i32p, f, ctypes.c_int, f, f, f, f, f, _f32p, _u8p, ctypes.c_int, _f32p, ctypes.c_int, f, f,
+            _f32p, _f32p, _f32p, ctypes.c_int]
+        L._colour_ready = True
+    return L
+
+
+def rgb2lab(rgb):
+    """(3,) uint8 -> (3,) float32 Lab with the reference cost's channel order."""
+    out = np.zeros(3, np.float32)
+    _colour_lib().orc_rgb2lab(_c(rgb, np.uint8).reshape(3), out)
+    return out
+
+
+def colour_distance(lab1, lab2) -> float:
+    return _colour_lib().orc_colour_distance(_c(lab1, np.float32).reshape(3), _c(lab2, np.float32).reshape(3))
+
+
+def colour_math(name, *args) -> float:
+    return getattr(_colour_lib(), "orc_" + name)(*[float(a) for a in args])
+
+
+def evaluate_colour(tris, tri_rgb, tris_model_count, poses, pose_model, width, height, proj, src_depth,
+                    occlusion_threshold, stride, cx, cy, fx, fy, depth_factor, o_xyz, o_rgb, pose_obs_total,
+                    calc_obs=True, sensor_resolution=0.01, colour_thr=15.0, nthreads=0):
+    """Cost type 1 (3-DoF RGB-D) for every pose -> (rc, oc, diff)."""
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    o_xyz = _c(o_xyz, np.float32).reshape(-1)
+    rc = np.zeros(n, np.float32)
+    oc = np.zeros(n, np.float32)
+    df = np.zeros(n, np.float32)
+    _colour_lib().orc_evaluate_colour(
+        tris, tris.size // 9, _c(tri_rgb, np.uint8).reshape(-1), _c(tris_model_count, np.int32),
+        len(tris_model_count), poses, _c(pose_model, np.int32), n, width, height, _c(proj, np.float32),
+        _c(src_depth, np.int32).reshape(-1), float(occlusion_threshold), stride, cx, cy, fx, fy, depth_factor,
+        o_xyz if o_xyz.size else np.zeros(3, np.float32),
+        _c(o_rgb, np.uint8).reshape(-1) if o_xyz.size else np.zeros(3, np.uint8), o_xyz.size // 3,
+        _c(pose_obs_total, np.float32), int(calc_obs), sensor_resolution, colour_thr, rc, oc, df, nthreads)
+    return rc, oc, df

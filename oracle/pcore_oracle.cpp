@@ -3,6 +3,10 @@
 // Build: oracle/Makefile (g++ -O2 -ffp-contract=off -fno-fast-math -fopenmp).
 #include "pcore_oracle.h"
 
+// The colour spec (deterministic sin / cos / atan2 / exp, CIEDE2000 term order) is shared with the GPU
+// build: it defines the arithmetic, like the GICP spec; tests/test_colour_spec.py pins it against numpy.
+#include "../perception_amd/csrc/pcore_colour.h"
+
 #include <climits>
 #include <cfloat>
 #include <cmath>
@@ -71,7 +75,8 @@ inline F3 barycentric(const float* A, const float* B, const float* C, const uint
 // image_renderer.cuh:59-210, executed for one triangle of one pose, serially.
 void rasterize_with_source(const F3 tri[3], F3 last_row, int32_t* depth, int width, int height,
                            const int32_t* src_depth, const uint8_t* src_mask, bool use_seg,
-                           int32_t pose_label, float occlusion_threshold) {
+                           int32_t pose_label, float occlusion_threshold, int32_t* dmin = nullptr,
+                           int32_t* tri_id = nullptr, int32_t t = 0) {
     const float W = (float)width, H = (float)height;
     float pts2[3][2];
     const float lr[3] = {last_row.x, last_row.y, last_row.z};
@@ -100,6 +105,11 @@ void rasterize_with_source(const F3 tri[3], F3 last_row, int32_t* depth, int wid
             const size_t y = (size_t)height - 1 - (size_t)P[1];
             const size_t idx = x + y * (size_t)width;
             const int32_t curr = cvt_i32_gpu(frag_depth + 0.5f);
+            // colour of the pixel: the first triangle (serial order) reaching the minimum fragment depth
+            if (dmin != nullptr && curr < dmin[idx]) {
+                dmin[idx] = curr;
+                tri_id[idx] = t;
+            }
             // z-test (image_renderer.cuh:146-159), serial order
             if (curr < depth[idx]) depth[idx] = curr;
             const int32_t nd = depth[idx];
@@ -116,9 +126,15 @@ void rasterize_with_source(const F3 tri[3], F3 last_row, int32_t* depth, int wid
 
 void render_one_pose(const float* tris, int lo, int hi, const float* pose, int width, int height,
                      const float* proj, const int32_t* src_depth, const uint8_t* src_mask, bool use_seg,
-                     int32_t pose_label, float occlusion_threshold, int32_t* depth) {
+                     int32_t pose_label, float occlusion_threshold, int32_t* depth, int32_t* dmin = nullptr,
+                     int32_t* tri_id = nullptr) {
     const size_t npx = (size_t)width * height;
     for (size_t i = 0; i < npx; i++) depth[i] = INT_MAX;
+    if (dmin != nullptr)
+        for (size_t i = 0; i < npx; i++) {
+            dmin[i] = INT_MAX;
+            tri_id[i] = -1;
+        }
     for (int t = lo; t < hi; t++) {
         const float* tp = tris + (size_t)9 * t;
         F3 v[3] = {{tp[0], tp[1], tp[2]}, {tp[3], tp[4], tp[5]}, {tp[6], tp[7], tp[8]}};
@@ -128,7 +144,7 @@ void render_one_pose(const float* tris, int lo, int hi, const float* pose, int w
         F3 last_row = {local[0].z, local[1].z, local[2].z};
         for (int k = 0; k < 3; k++) projd[k] = mat_mul_v(proj, local[k]);
         rasterize_with_source(projd, last_row, depth, width, height, src_depth, src_mask, use_seg, pose_label,
-                              occlusion_threshold);
+                              occlusion_threshold, dmin, tri_id, t);
     }
     // max2zero (image_renderer.cuh:324-333, 465-466)
     for (size_t i = 0; i < npx; i++)
@@ -728,6 +744,103 @@ void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model
             out_rc[n] = rc;
             out_oc[n] = oc;
             out_diff[n] = df;
+        }
+    }
+}
+
+
+// rgb2lab (compute_costs.cuh:57-88) in double, with the cost's channel order rgb2lab(c2, c1, c0)
+// (compute_costs.cuh:214-220).
+void orc_rgb2lab(const uint8_t c[3], float lab[3]) {
+    double r = c[2] / 255.0, g = c[1] / 255.0, b = c[0] / 255.0;
+    r = ((r > 0.04045) ? std::pow((r + 0.055) / 1.055, 2.4) : (r / 12.92)) * 100.0;
+    g = ((g > 0.04045) ? std::pow((g + 0.055) / 1.055, 2.4) : (g / 12.92)) * 100.0;
+    b = ((b > 0.04045) ? std::pow((b + 0.055) / 1.055, 2.4) : (b / 12.92)) * 100.0;
+    double x = r * 0.4124564 + g * 0.3575761 + b * 0.1804375;
+    double y = r * 0.2126729 + g * 0.7151522 + b * 0.0721750;
+    double z = r * 0.0193339 + g * 0.1191920 + b * 0.9503041;
+    x = x / 95.047;
+    y = y / 100.00;
+    z = z / 108.883;
+    x = (x > 0.008856) ? std::cbrt(x) : (7.787 * x + 16.0 / 116.0);
+    y = (y > 0.008856) ? std::cbrt(y) : (7.787 * y + 16.0 / 116.0);
+    z = (z > 0.008856) ? std::cbrt(z) : (7.787 * z + 16.0 / 116.0);
+    lab[0] = (float)((116.0 * y) - 16);
+    lab[1] = (float)(500 * (x - y));
+    lab[2] = (float)(200 * (y - z));
+}
+
+double orc_colour_distance(const float* lab1, const float* lab2) {
+    return pcore::colour::colour_distance(lab1[0], lab1[1], lab1[2], lab2[0], lab2[1], lab2[2]);
+}
+
+float orc_sin_f(float x) { return pcore::colour::sin_f(x); }
+float orc_cos_f(float x) { return pcore::colour::cos_f(x); }
+float orc_exp_f(float x) { return pcore::colour::exp_f(x); }
+float orc_atan2_f(float y, float x) { return pcore::colour::atan2_f(y, x); }
+
+// Cost type 1 (3-DoF RGB-D): as orc_evaluate without labels, plus the colour gate of
+// compute_render_cost (compute_costs.cuh:201-240): a point within the sensor radius of its nearest
+// observed point is explained only if CIEDE2000(observed, rendered) <= colour_thr, else it is bad.
+// Rendered colour = tri_rgb of the first triangle (serial order) reaching the pixel's minimum depth.
+void orc_evaluate_colour(const float* tris, int num_tris, const uint8_t* tri_rgb, const int32_t* tris_model_count,
+                         int num_models, const float* poses, const int32_t* pose_model, int num_poses, int width,
+                         int height, const float* proj, const int32_t* src_depth, float occlusion_threshold,
+                         int stride, float cx, float cy, float fx, float fy, float depth_factor, const float* o_xyz,
+                         const uint8_t* o_rgb, int num_o, const float* pose_obs_total, int calc_obs,
+                         float sensor_resolution, float colour_thr, float* out_rc, float* out_oc, float* out_diff,
+                         int nthreads) {
+    std::vector<int> lo, hi;
+    model_ranges(tris_model_count, num_models, lo, hi);
+    const size_t npx = (size_t)width * height;
+    std::vector<float> tri_lab((size_t)3 * num_tris), o_lab((size_t)3 * (num_o > 0 ? num_o : 1));
+    for (int t = 0; t < num_tris; t++) orc_rgb2lab(tri_rgb + (size_t)3 * t, &tri_lab[(size_t)3 * t]);
+    for (int o = 0; o < num_o; o++) orc_rgb2lab(o_rgb + (size_t)3 * o, &o_lab[(size_t)3 * o]);
+    const float r2 = sensor_resolution * sensor_resolution;
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+    {
+        std::vector<int32_t> depth(npx), dmin(npx), tid(npx);
+        std::vector<uint8_t> explained(num_o > 0 ? num_o : 1);
+#pragma omp for schedule(dynamic, 1)
+        for (int n = 0; n < num_poses; n++) {
+            const int m = pose_model[n];
+            render_one_pose(tris, lo[m], hi[m], poses + (size_t)16 * n, width, height, proj, src_depth, nullptr,
+                            false, 0, occlusion_threshold, depth.data(), dmin.data(), tid.data());
+            std::fill(explained.begin(), explained.end(), 0);
+            float num = 0.0f, bad = 0.0f;
+            for (int y = 0; y < height; y += stride)
+                for (int x = 0; x < width; x += stride) {
+                    const size_t idx = (size_t)x + (size_t)y * width;
+                    if (depth[idx] <= 0) continue;
+                    float q[3];
+                    transform_point(x, y, depth[idx], cx, cy, fx, fy, depth_factor, q[0], q[1], q[2]);
+                    float d2;
+                    int32_t nn;
+                    knn1_range(q, o_xyz, 0, num_o, d2, nn);
+                    num += 1.0f;
+                    if (d2 > r2) { bad += 1.0f; continue; }
+                    if (nn < 0) continue;
+                    const int t = tid[idx];
+                    const double cd = orc_colour_distance(&o_lab[(size_t)3 * nn], &tri_lab[(size_t)3 * t]);
+                    if (cd > (double)colour_thr) bad += 1.0f;
+                    else explained[nn] = 1;
+                }
+            const float rendered_explained = num - bad;
+            float rc = (num == 0) ? -1.0f : bad / num;
+            rc = (rc == -1.0f) ? -1.0f : rc * 100.0f;
+            out_rc[n] = rc;
+            if (calc_obs) {
+                float expl = 0.0f;
+                for (int o = 0; o < num_o; o++) expl += (float)explained[o];
+                out_diff[n] = rendered_explained - expl;
+                float oc = pose_obs_total[n] - expl;
+                oc = oc / pose_obs_total[n];
+                out_oc[n] = oc * 100.0f;
+            } else {
+                out_oc[n] = 0.0f;
+                out_diff[n] = 0.0f;
+            }
         }
     }
 }

@@ -122,6 +122,23 @@ void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model
                       double trans_eps, float* out_adj, int32_t* out_iters, float* out_rc, float* out_oc,
                       float* out_diff, int nthreads);
 
+/* Colour cost (cost_type 1, f4): rgb2lab with the cost's channel order, the CIEDE2000 distance of the
+ * shared colour spec, its float transcendentals, and the 3-DoF RGB-D evaluation (serial raster keeping
+ * the first triangle that reaches each pixel's minimum depth). */
+void orc_rgb2lab(const uint8_t c[3], float lab[3]);
+double orc_colour_distance(const float* lab1, const float* lab2);
+float orc_sin_f(float x);
+float orc_cos_f(float x);
+float orc_exp_f(float x);
+float orc_atan2_f(float y, float x);
+void orc_evaluate_colour(const float* tris, int num_tris, const uint8_t* tri_rgb, const int32_t* tris_model_count,
+                         int num_models, const float* poses, const int32_t* pose_model, int num_poses, int width,
+                         int height, const float* proj, const int32_t* src_depth, float occlusion_threshold,
+                         int stride, float cx, float cy, float fx, float fy, float depth_factor, const float* o_xyz,
+                         const uint8_t* o_rgb, int num_o, const float* pose_obs_total, int calc_obs,
+                         float sensor_resolution, float colour_thr, float* out_rc, float* out_oc, float* out_diff,
+                         int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_evaluate_icp",
     "pcore_render",
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
-    "pcore_observed_cloud_bounded",
+    "pcore_observed_cloud_bounded", "pcore_set_observation_colors",
 )
 
 
@@ -46,7 +46,7 @@ class Camera(ctypes.Structure):
 class EvalParams(ctypes.Structure):
     _fields_ = [("cost_type", ctypes.c_int32), ("calc_obs_cost", ctypes.c_int32), ("stride", ctypes.c_int32),
                 ("depth_factor", ctypes.c_float), ("sensor_resolution", ctypes.c_float),
-                ("occlusion_threshold", ctypes.c_float)]
+                ("occlusion_threshold", ctypes.c_float), ("color_distance_threshold", ctypes.c_float)]
 
 
 class IcpParams(ctypes.Structure):
@@ -105,6 +105,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
                                        ctypes.POINTER(i32), vp]
     L.pcore_select.argtypes = [vp, vp, vp, vp, i32, i64, i32, vp, vp]
     L.pcore_pose_distances.argtypes = [vp, vp, i32, vp, vp, i32, vp, vp, vp]
+    L.pcore_set_observation_colors.argtypes = [vp, vp, i32, vp]
     L.pcore_observed_cloud_bounded.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, vp, vp, vp, i32,
                                                ctypes.POINTER(i32), vp]
     for name in EXPORTED_SYMBOLS:

@@ -135,13 +135,21 @@ class PoseCore:
             _ptr(None if obs_label is None else obs_label.contiguous(), torch.int32, "obs_label") if n else None,
             n, float(sensor_resolution), _stream(stream)))
 
+    def set_observation_colors(self, obs_rgb: torch.Tensor, stream=None):
+        """Colours (n, 3) uint8 of the observed points given to set_observation, in the same order
+        (cost_type 1)."""
+        rgb = obs_rgb.contiguous()
+        n = int(rgb.shape[0])
+        self._check(self.lib.pcore_set_observation_colors(
+            self._h, _ptr(rgb, torch.uint8, "obs_rgb") if n else None, n, _stream(stream)))
+
     # -- per-batch hot path -----------------------------------------------------------------------
     def evaluate(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
                  pose_obs_total: Optional[torch.Tensor], cost_type: int = _native.COST_DEPTH_6DOF,
                  calc_obs_cost: bool = True, stride: int = 8, depth_factor: float = 100.0,
                  sensor_resolution: float = 0.01, occlusion_threshold: float = 1.0,
                  out: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                 dbg_zs: Optional[torch.Tensor] = None, stream=None):
+                 dbg_zs: Optional[torch.Tensor] = None, color_distance_threshold: float = 15.0, stream=None):
         """Stage COST (do_icp = false).  Returns (rendered_cost, observed_cost, points_diff_cost)."""
         n = int(poses.shape[0])
         dev = poses.device
@@ -149,7 +157,7 @@ class PoseCore:
             out = tuple(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3))
         rc, oc, df = out
         p = EvalParams(int(cost_type), int(bool(calc_obs_cost)), int(stride), float(depth_factor),
-                       float(sensor_resolution), float(occlusion_threshold))
+                       float(sensor_resolution), float(occlusion_threshold), float(color_distance_threshold))
         self._check(self.lib.pcore_evaluate(
             self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
             _ptr(pose_label, torch.int32, "pose_label"), _ptr(pose_obs_total, torch.float32, "pose_obs_total"),
@@ -163,7 +171,8 @@ class PoseCore:
                      sensor_resolution: float = 0.01, occlusion_threshold: float = 1.0,
                      k: int = _native.ICP_K, max_iterations: int = _native.ICP_MAX_ITER,
                      rotation_epsilon: float = _native.ICP_ROT_EPS,
-                     transformation_epsilon: float = _native.ICP_TRANS_EPS, out=None, stream=None):
+                     transformation_epsilon: float = _native.ICP_TRANS_EPS, out=None,
+                     color_distance_threshold: float = 15.0, stream=None):
         """Stage COST with do_icp = true.  Returns (adjusted poses (N,16), iterations (N,), rc, oc, diff)."""
         n = int(poses.shape[0])
         dev = poses.device
@@ -172,7 +181,7 @@ class PoseCore:
                    *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)))
         adj, iters, rc, oc, df = out
         p = EvalParams(int(cost_type), int(bool(calc_obs_cost)), int(stride), float(depth_factor),
-                       float(sensor_resolution), float(occlusion_threshold))
+                       float(sensor_resolution), float(occlusion_threshold), float(color_distance_threshold))
         ip = IcpParams(int(k), int(max_iterations), float(rotation_epsilon), float(transformation_epsilon))
         self._check(self.lib.pcore_evaluate_icp(
             self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),

@@ -70,6 +70,13 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_count;
     DevBuf<double> icp_cov;
     DevBuf<int32_t> icp_counter;
+    // colour gate (cost_type 1)
+    DevBuf<uint32_t> mtri_orig;   // original triangle of every meshlet triangle
+    DevBuf<float4> tri_lab;       // Lab per original triangle
+    DevBuf<float4> obs_lab;       // Lab per observed point, label-sorted
+    DevBuf<int32_t> colour_id;    // N x nsamp scratch of the fused kernel's colour id pass
+    std::vector<int> obs_order;   // label-sorted position -> caller's observed index
+    bool have_obs_colours = false;
     DevBuf<double> metric_part;  // ADD / ADD-S per-block partial sums
     // scratch (parity stages)
     DevBuf<int32_t> scratch_counts, scratch_offsets, scratch_total;
@@ -131,8 +138,30 @@ struct VKeyHash {
 };
 
 // Greedy adjacency-growth meshlet builder for one model.  verts: unique vertex ids per triangle corner.
-void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std::vector<float>& vxyz,
-                    std::vector<float4>& out_v, std::vector<uint32_t>& out_t, std::vector<Meshlet>& out_m) {
+// rgb2lab (compute_costs.cuh:57-88) in double with glibc pow / cbrt, stored as float.  The cost reads
+// its "red" from colour plane 2 and "blue" from plane 0 (compute_costs.cuh:214-220): rgb2lab(c2, c1, c0).
+float4 lab_of(const uint8_t c[3]) {
+    const uint8_t rr = c[2], gg = c[1], bbb = c[0];
+    double r = rr / 255.0, g = gg / 255.0, b = bbb / 255.0;
+    r = ((r > 0.04045) ? std::pow((r + 0.055) / 1.055, 2.4) : (r / 12.92)) * 100.0;
+    g = ((g > 0.04045) ? std::pow((g + 0.055) / 1.055, 2.4) : (g / 12.92)) * 100.0;
+    b = ((b > 0.04045) ? std::pow((b + 0.055) / 1.055, 2.4) : (b / 12.92)) * 100.0;
+    double x = r * 0.4124564 + g * 0.3575761 + b * 0.1804375;
+    double y = r * 0.2126729 + g * 0.7151522 + b * 0.0721750;
+    double z = r * 0.0193339 + g * 0.1191920 + b * 0.9503041;
+    x = x / 95.047;
+    y = y / 100.00;
+    z = z / 108.883;
+    x = (x > 0.008856) ? std::cbrt(x) : (7.787 * x + 16.0 / 116.0);
+    y = (y > 0.008856) ? std::cbrt(y) : (7.787 * y + 16.0 / 116.0);
+    z = (z > 0.008856) ? std::cbrt(z) : (7.787 * z + 16.0 / 116.0);
+    const float l = (float)((116.0 * y) - 16), a = (float)(500 * (x - y)), bb = (float)(200 * (y - z));
+    return make_float4(l, a, bb, 0.0f);
+}
+
+void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std::vector<float>& vxyz, int tri_base,
+                    std::vector<float4>& out_v, std::vector<uint32_t>& out_t, std::vector<uint32_t>& out_orig,
+                    std::vector<Meshlet>& out_m) {
     const int T = (int)tri_verts.size() / 3;
     std::vector<std::vector<int>> adj(num_verts);
     for (int t = 0; t < T; t++)
@@ -181,9 +210,11 @@ void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std:
         m.nv = (int)mv.size();
         m.nt = (int)mt.size();
         for (int v : mv) out_v.push_back(make_float4(vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], 0.0f));
-        for (int t : mt)
+        for (int t : mt) {
             out_t.push_back((uint32_t)local[tri_verts[3 * t]] | ((uint32_t)local[tri_verts[3 * t + 1]] << 8) |
                             ((uint32_t)local[tri_verts[3 * t + 2]] << 16));
+            out_orig.push_back((uint32_t)(tri_base + t));
+        }
         out_m.push_back(m);
         for (int v : mv) local[v] = -1;
     }
@@ -285,6 +316,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
     (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter);
+    (void)dev_free(c->mtri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part);
     delete c;
 }
@@ -293,7 +325,6 @@ const char* pcore_last_error(const pcore_ctx* c) { return c ? c->err.c_str() : "
 
 int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_rgb, int32_t num_tris,
                         const int32_t* tris_model_count, int32_t num_models) {
-    (void)tri_rgb;  // colour is only used by cost type 1 (not implemented yet)
     if (!c) return PCORE_E_INVALID_ARG;
     if (!tri_xyz || num_tris <= 0 || !tris_model_count || num_models <= 0)
         return fail(c, PCORE_E_INVALID_ARG, "upload_meshes: empty mesh");
@@ -306,7 +337,7 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     HIPC(c, hipSetDevice(c->device));
 
     std::vector<float4> mv;
-    std::vector<uint32_t> mt;
+    std::vector<uint32_t> mt, mo;
     std::vector<Meshlet> ml;
     std::vector<int32_t> mlo(num_models), mhi(num_models), tlo(num_models), thi(num_models);
     int t0 = 0;
@@ -340,7 +371,7 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
                 tv[(size_t)3 * t + k] = id;
             }
         mlo[m] = (int)ml.size();
-        build_meshlets(tv, (int)(vxyz.size() / 3), vxyz, mv, mt, ml);
+        build_meshlets(tv, (int)(vxyz.size() / 3), vxyz, t0, mv, mt, mo, ml);
         mhi[m] = (int)ml.size();
         t0 += T;
     }
@@ -350,7 +381,15 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     HIPC(c, dev_upload(c->tri_hi, thi));
     HIPC(c, dev_upload(c->mverts, mv));
     HIPC(c, dev_upload(c->mtris, mt));
+    HIPC(c, dev_upload(c->mtri_orig, mo));
     HIPC(c, dev_upload(c->meshlets, ml));
+    std::vector<float4> tl((size_t)num_tris);
+    for (int t = 0; t < num_tris; t++) {
+        uint8_t col[3] = {128, 128, 128};
+        if (tri_rgb) for (int k = 0; k < 3; k++) col[k] = tri_rgb[3 * (size_t)t + k];
+        tl[t] = lab_of(col);
+    }
+    HIPC(c, dev_upload(c->tri_lab, tl));
     HIPC(c, dev_upload(c->model_ml_lo, mlo));
     HIPC(c, dev_upload(c->model_ml_hi, mhi));
     c->num_models = num_models;
@@ -421,6 +460,23 @@ int pcore_observed_cloud_bounded(pcore_ctx* c, const int32_t* d_depth, const uin
     return PCORE_OK;
 }
 
+int pcore_set_observation_colors(pcore_ctx* c, const uint8_t* d_obs_rgb, int32_t num_obs, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (!c->have_obs) return fail(c, PCORE_E_STATE, "set_observation_colors: call pcore_set_observation first");
+    if (num_obs != (int)c->obs_order.size() || (num_obs > 0 && !d_obs_rgb))
+        return fail(c, PCORE_E_INVALID_ARG, "set_observation_colors: num_obs differs from the observation");
+    HIPC(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<uint8_t> rgb((size_t)num_obs * 3);
+    if (num_obs > 0) HIPC(c, hipMemcpyAsync(rgb.data(), d_obs_rgb, rgb.size(), hipMemcpyDeviceToHost, s));
+    HIPC(c, hipStreamSynchronize(s));
+    std::vector<float4> labv(std::max(num_obs, 1), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (int k = 0; k < num_obs; k++) labv[k] = lab_of(&rgb[3 * (size_t)c->obs_order[k]]);
+    HIPC(c, dev_upload(c->obs_lab, labv));
+    c->have_obs_colours = true;
+    return PCORE_OK;
+}
+
 int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uint8_t* d_src_mask,
                           const float* d_obs_xyz, const int32_t* d_obs_label, int32_t num_obs,
                           float sensor_resolution, pcore_stream stream) {
@@ -453,6 +509,8 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
     std::vector<int> order(num_obs);
     for (int i = 0; i < num_obs; i++) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lab[a] < lab[b]; });
+    c->obs_order = order;
+    c->have_obs_colours = false;
     std::vector<LabelGrid> grids(num_labels + 1);
     std::vector<int32_t> cell_start;
     std::vector<float4> gpts;
@@ -542,10 +600,12 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
         return fail(c, PCORE_E_STATE, "evaluate: meshes, camera and observation must be set first");
     if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_rc)))
         return fail(c, PCORE_E_INVALID_ARG, "evaluate: null pose / output pointer");
-    if (p->cost_type == PCORE_COST_RGBD_3DOF)
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate: cost_type 1 (CIEDE2000 colour) is not implemented");
-    if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF)
+    if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF &&
+        p->cost_type != PCORE_COST_RGBD_3DOF)
         return fail(c, PCORE_E_INVALID_ARG, "evaluate: unknown cost_type");
+    if (p->cost_type == PCORE_COST_RGBD_3DOF && (d_pose_label || !c->have_obs_colours))
+        return fail(c, PCORE_E_INVALID_ARG,
+                    "evaluate: cost_type 1 is 3-DoF (no pose labels) and needs pcore_set_observation_colors");
     if (num_poses == 0) return PCORE_OK;
     if (p->cost_type == PCORE_COST_DEPTH_6DOF && (!d_pose_label || !c->obs_has_mask))
         return fail(c, PCORE_E_INVALID_ARG, "evaluate: cost_type 2 needs pose labels and a source mask");
@@ -556,7 +616,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
         return fail(c, PCORE_E_INVALID_ARG, "evaluate: width must be a multiple of stride");
     const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
     if (ws > 4095 || hs > 4095) return fail(c, PCORE_E_INVALID_ARG, "evaluate: sampled image too large");
-    const size_t lds = fused_lds_bytes(ws, hs, c->bitmap_words);
+    const size_t lds = fused_lds_bytes(ws, hs, c->bitmap_words, p->cost_type == PCORE_COST_RGBD_3DOF);
     if (lds > (size_t)c->prop.sharedMemPerBlock)
         return fail(c, PCORE_E_INVALID_ARG,
                     "evaluate: sampled z-buffer does not fit in LDS (use a larger stride); need " +
@@ -603,6 +663,14 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.out_oc = d_out_oc;
     a.out_diff = d_out_diff;
     a.dbg_zs = d_dbg_zs;
+    if (p->cost_type == PCORE_COST_RGBD_3DOF) {
+        a.mtri_orig = c->mtri_orig.p;
+        a.tri_lab = c->tri_lab.p;
+        a.obs_lab = c->obs_lab.p;
+        a.colour_thr = p->color_distance_threshold;
+        HIPC(c, dev_reserve(c->colour_id, (size_t)num_poses * ws * hs));
+        a.cid = c->colour_id.p;
+    }
     if (const char* e = getenv("PCORE_DEBUG_SKIP")) a.dbg_skip = atoi(e);
     HIPC(c, launch_fused_cost(a, s));
     return PCORE_OK;

@@ -211,43 +211,61 @@ __device__ __forceinline__ void stage_targets(TgtTile& T, const float4* tgt, int
     }
 }
 
-// Nearest of a staged tile, four targets per step with packed f32 arithmetic (same IEEE operations,
-// per element, as sqdist3).  A 4-way tournament that prefers the later target only when strictly
-// nearer, then one strict update of (best, j): the lexicographic minimum of (distance, index), i.e.
-// the oracle's first strict minimum.
+// Nearest of a staged tile with packed f32 arithmetic (same IEEE operations, per element, as
+// sqdist3).  Four targets form a tournament that prefers the later target only when strictly nearer;
+// alternate quads feed two independent (best, index) chains, merged at the end by (distance, index):
+// together the lexicographic minimum of (distance, index), i.e. the oracle's first strict minimum.
+__device__ __forceinline__ void quad_min(const TgtTile& T, int o, f2v qx2, f2v qy2, f2v qz2, float& m, int& i) {
+    const f4v X = *reinterpret_cast<const f4v*>(&T.x[o]);
+    const f4v Y = *reinterpret_cast<const f4v*>(&T.y[o]);
+    const f4v Z = *reinterpret_cast<const f4v*>(&T.z[o]);
+    const f2v dxa = qx2 - X.xy, dya = qy2 - Y.xy, dza = qz2 - Z.xy;
+    const f2v dxb = qx2 - X.zw, dyb = qy2 - Y.zw, dzb = qz2 - Z.zw;
+    const f2v da = dxa * dxa + dya * dya + dza * dza;
+    const f2v db = dxb * dxb + dyb * dyb + dzb * dzb;
+    const bool c01 = da.y < da.x, c23 = db.y < db.x;
+    const float m01 = c01 ? da.y : da.x, m23 = c23 ? db.y : db.x;
+    const int i01 = c01 ? 1 : 0, i23 = c23 ? 3 : 2;
+    const bool c = m23 < m01;
+    m = c ? m23 : m01;
+    i = o + (c ? i23 : i01);
+}
+
 __device__ __forceinline__ void scan_targets(const TgtTile& T, int tn, int t0, float qx, float qy, float qz,
                                              float& best, int& j) {
     const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+    float bA = INFINITY, bB = INFINITY;
+    int jA = -1, jB = -1;
+    int o = 0;
 #pragma unroll 2
-    for (int o = 0; o < tn; o += 4) {
-        const f4v X = *reinterpret_cast<const f4v*>(&T.x[o]);
-        const f4v Y = *reinterpret_cast<const f4v*>(&T.y[o]);
-        const f4v Z = *reinterpret_cast<const f4v*>(&T.z[o]);
-        const f2v dxa = qx2 - X.xy, dya = qy2 - Y.xy, dza = qz2 - Z.xy;
-        const f2v dxb = qx2 - X.zw, dyb = qy2 - Y.zw, dzb = qz2 - Z.zw;
-        const f2v da = dxa * dxa + dya * dya + dza * dza;
-        const f2v db = dxb * dxb + dyb * dyb + dzb * dzb;
-        const bool c01 = da.y < da.x, c23 = db.y < db.x;
-        const float m01 = c01 ? da.y : da.x, m23 = c23 ? db.y : db.x;
-        const int i01 = c01 ? 1 : 0, i23 = c23 ? 3 : 2;
-        const bool c = m23 < m01;
-        const float m = c ? m23 : m01;
-        const int i = c ? i23 : i01;
-        if (m < best) { best = m; j = t0 + o + i; }
+    for (; o + 8 <= tn; o += 8) {
+        float m;
+        int i;
+        quad_min(T, o, qx2, qy2, qz2, m, i);
+        if (m < bA) { bA = m; jA = i; }
+        quad_min(T, o + 4, qx2, qy2, qz2, m, i);
+        if (m < bB) { bB = m; jB = i; }
     }
+    for (; o < tn; o += 4) {  // the last < 8 targets; tiles are padded to a multiple of 4
+        float m;
+        int i;
+        quad_min(T, o, qx2, qy2, qz2, m, i);
+        if (m < bA) { bA = m; jA = i; }
+    }
+    if (bB < bA || (bB == bA && jB >= 0 && jB < jA)) { bA = bB; jA = jB; }
+    if (bA < best) { best = bA; j = t0 + jA; }  // earlier tiles hold lower indices
 }
 
-__device__ __forceinline__ void load_source(const float4* src, const double* scov, int i, float4& sp, double (&cs)[6]) {
-    sp = src[i];
-    const double2* c2 = reinterpret_cast<const double2*>(scov + (size_t)6 * i);
-    const double2 a = c2[0], b = c2[1], c = c2[2];
-    cs[0] = a.x; cs[1] = a.y; cs[2] = b.x; cs[3] = b.y; cs[4] = c.x; cs[5] = c.y;
+__device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6]) {
+    const double2* c2 = reinterpret_cast<const double2*>(cov + (size_t)6 * i);
+    const double2 a = c2[0], b = c2[1], d = c2[2];
+    c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y; c[4] = d.x; c[5] = d.y;
 }
 
 // One point's Gauss-Newton contribution (orc gicp_contrib) given its transformed position q and its
 // correspondence tj / ct: acc[0..20] upper(H), [21..26] b, [27] error.
 __device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6],
-                                             float4 tj, const double* ct, double (&acc)[28]) {
+                                             float4 tj, const double (&ct)[6], double (&acc)[28]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
     double RC[3][3], A[3][3];
@@ -405,19 +423,21 @@ gicp_kernel(GicpArgs g, int num_poses) {
             double acc[28];
 #pragma unroll
             for (int v = 0; v < 28; v++) acc[v] = 0.0;
-            // rounds of NT source points; the next round's point and covariance are loaded while this
-            // round scans
+            // rounds of NT source points, software-pipelined: round r's nearest-target scan runs while
+            // round r-1's target covariance (a gather) and round r+1's source point are in flight, then
+            // round r-1's contribution is added; per lane the contributions keep their point order
             float4 sp_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            double cs_n[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-            if (tid < ns) load_source(src, scov, tid, sp_n, cs_n);
+            if (tid < ns) sp_n = src[tid];
+            bool p_ok = false;  // previous round's pending contribution
+            double p_q[3] = {0.0, 0.0, 0.0}, p_cs[6], p_ct[6];
+            float4 p_tj = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             for (int i0 = 0; i0 < ns; i0 += NT) {
                 const int i = i0 + tid;
                 const bool act = i < ns;
                 const float4 sp = sp_n;
-                double cs[6];
-#pragma unroll
-                for (int k = 0; k < 6; k++) cs[k] = cs_n[k];
-                if (i + NT < ns) load_source(src, scov, i + NT, sp_n, cs_n);
+                double cs[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // consumed after the next round's scan
+                if (act) load_cov(scov, i, cs);
+                if (i + NT < ns) sp_n = src[i + NT];
                 const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
                 double q[3];
 #pragma unroll
@@ -435,12 +455,19 @@ gicp_kernel(GicpArgs g, int num_poses) {
                     }
                     scan_targets(T, tn, t0, qx, qy, qz, best, j);
                 }
-                if (act && j >= 0) {
+                if (p_ok) gicp_contrib(R, p_q, p_cs, p_tj, p_ct, acc);
+                p_ok = act && j >= 0;
+                if (p_ok) {
                     // a selected target is finite, so the staged copy equals the original
-                    const float4 tj = resident ? make_float4(T.x[j], T.y[j], T.z[j], 0.0f) : tgt[j];
-                    gicp_contrib(R, q, cs, tj, tcov + (size_t)6 * j, acc);
+                    p_tj = resident ? make_float4(T.x[j], T.y[j], T.z[j], 0.0f) : tgt[j];
+                    load_cov(tcov, j, p_ct);
+#pragma unroll
+                    for (int k = 0; k < 3; k++) p_q[k] = q[k];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) p_cs[k] = cs[k];
                 }
             }
+            if (p_ok) gicp_contrib(R, p_q, p_cs, p_tj, p_ct, acc);
             GPROF_T(t_b);
 #pragma unroll
             for (int v = 0; v < 28; v++) {

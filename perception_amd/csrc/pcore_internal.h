@@ -68,6 +68,12 @@ struct FusedArgs {
     float4* cloud_out;
     int32_t* cloud_count;
     int32_t cloud_cap;
+    // colour gate of cost_type 1 (compute_costs.cuh:201-240); null / 0 otherwise
+    const uint32_t* mtri_orig;  // original triangle index of every meshlet triangle
+    const float4* tri_lab;      // Lab of every original triangle's colour (reference channel order)
+    const float4* obs_lab;      // Lab of every observed point, label-sorted order
+    int32_t* cid;               // N x nsamp scratch: original triangle of each sample's nearest fragment
+    float colour_thr;           // color_distance_threshold
     // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
     // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
     int32_t dbg_skip;
@@ -105,7 +111,7 @@ int pose_dist_blocks(int n);
 hipError_t launch_pose_distances(const float* pts, int n, const double* T_gt, const double* T_est, int pairs,
                                  double* part, double* out_add, double* out_adds, hipStream_t s);
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
-size_t fused_lds_bytes(int ws, int hs, int bitmap_words);
+size_t fused_lds_bytes(int ws, int hs, int bitmap_words, bool colour = false);
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
                               const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
                               const float* proj, int32_t* depth, hipStream_t s);

@@ -16,6 +16,7 @@
 //   cloud_count / cloud_write  stage CLOUD and depth2cloud_global: stride mask, ordered compaction, unprojection.
 //   select_kernel          host selection of the reference (int cost, filter, per-model argmin key).
 #include "pcore_internal.h"
+#include "pcore_colour.h"
 
 #include <climits>
 #include <cfloat>
@@ -176,30 +177,44 @@ struct FusedSmem {
     float* vz;      // camera z (cm)
     uint2* vwin;    // kWaves * 64: packed int16 sample-window bounds per vertex (see vertex_window)
     TriRec* ring;   // kWaves * kRecCap (phase 1); reused as int32 point queues in phase 2
+    uint32_t* ring_id;  // kWaves * kRecCap original triangle ids (colour id pass only)
     uint32_t* bitmap;
     int32_t* counters;  // [0] bad, [1] explained, [2] points
 };
 
-__device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, int s, int H, int ws, int32_t* zbuf) {
+// IDPASS = false: depth pass (atomicMin of the fragment depth).  IDPASS = true: colour id pass over the
+// final depths: the fragments whose depth equals the sample's minimum leave the lowest original triangle
+// index -- the colour the reference's serial z-test (strict <) keeps.
+template <bool IDPASS = false>
+__device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, int s, int H, int ws, int32_t* zbuf,
+                                              int32_t* cid = nullptr, uint32_t id = 0) {
     const float P0 = (float)(kx * s);
     const float P1 = (float)(H - 1 - ky * s);
     int32_t d;
-    if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d))
-        atomicMin(&zbuf[ky * ws + kx], d);
+    if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d)) {
+        const int k = ky * ws + kx;
+        if constexpr (IDPASS) {
+            if (d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
+        } else {
+            atomicMin(&zbuf[k], d);
+        }
+    }
 }
 
-size_t fused_lds_bytes(int ws, int hs, int bitmap_words) {
+size_t fused_lds_bytes(int ws, int hs, int bitmap_words, bool colour) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
     size_t b = al((size_t)ws * hs * 4);
     b += al((size_t)kWaves * kWave * 4) * 3;
     b += al((size_t)kWaves * kWave * 8);
     b += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+    if (colour) b += al((size_t)kWaves * kRecCap * 4);
     b += al((size_t)bitmap_words * 4);
     b += 16;
     return b;
 }
 
-__device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsamp, int bitmap_words) {
+__device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsamp, int bitmap_words,
+                                                bool colour = false) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
     FusedSmem sm;
     unsigned char* p = smem_raw;
@@ -209,6 +224,8 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
     sm.vz = (float*)p; p += al((size_t)kWaves * kWave * 4);
     sm.vwin = (uint2*)p; p += al((size_t)kWaves * kWave * 8);
     sm.ring = (TriRec*)p; p += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+    sm.ring_id = nullptr;
+    if (colour) { sm.ring_id = (uint32_t*)p; p += al((size_t)kWaves * kRecCap * 4); }
     sm.bitmap = (uint32_t*)p; p += al((size_t)bitmap_words * 4);
     sm.counters = (int32_t*)p;
     return sm;
@@ -247,8 +264,8 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
 
-template <int STRIDE>
-__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose) {
+template <int STRIDE, bool IDPASS = false>
+__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, int32_t* cid = nullptr) {
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
@@ -270,6 +287,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     float* vz = sm.vz + wave * kWave;
     uint2* vwin = sm.vwin + wave * kWave;
     TriRec* ring = sm.ring + wave * kRecCap;
+    uint32_t* ring_id = IDPASS ? sm.ring_id + wave * kRecCap : nullptr;
     const short2v wzero = {0, 0};
     const short2v wlim = {(short)(ws - 1), (short)(a.hs - 1)};
     int rec_count = 0;  // wave-uniform
@@ -282,10 +300,12 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             const int j = base + lane;
             if (j < count) {
                 const TriRec r = ring[j];
+                const uint32_t id = IDPASS ? ring_id[j] : 0u;
                 const int kx0 = r.meta & 0xfff, ky0 = (r.meta >> 12) & 0xfff;
                 const int nx = ((r.meta >> 24) & 0xf) + 1, ny = ((r.meta >> 28) & 0xf) + 1;
                 for (int iy = 0; iy < ny; iy++)
-                    for (int ix = 0; ix < nx; ix++) raster_sample(r, kx0 + ix, ky0 + iy, s, H, ws, sm.zbuf);
+                    for (int ix = 0; ix < nx; ix++)
+                        raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, ws, sm.zbuf, cid, id);
             }
         }
         wave_sync();
@@ -296,24 +316,32 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     int m = ml_lo + wave;
     Meshlet ml = {0, 0, 0, 0};
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint32_t pk0 = 0, pk1 = 0;
+    uint32_t pk0 = 0, pk1 = 0, id0 = 0, id1 = 0;
     if (m < ml_hi) {
         ml = a.meshlets[m];
         if (lane < ml.nv) v = a.mverts[ml.vbase + lane];
         if (lane < ml.nt) pk0 = a.mtris[ml.tbase + lane];
         if (kWave + lane < ml.nt) pk1 = a.mtris[ml.tbase + kWave + lane];
+        if (IDPASS) {
+            if (lane < ml.nt) id0 = a.mtri_orig[ml.tbase + lane];
+            if (kWave + lane < ml.nt) id1 = a.mtri_orig[ml.tbase + kWave + lane];
+        }
     }
     for (; m < ml_hi; m += kWaves) {
         // prefetch the next meshlet of this wave while this one is processed
         const int mn = m + kWaves;
         Meshlet mln = {0, 0, 0, 0};
         float4 vn = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t pn0 = 0, pn1 = 0;
+        uint32_t pn0 = 0, pn1 = 0, in0 = 0, in1 = 0;
         if (mn < ml_hi) {
             mln = a.meshlets[mn];
             if (lane < mln.nv) vn = a.mverts[mln.vbase + lane];
             if (lane < mln.nt) pn0 = a.mtris[mln.tbase + lane];
             if (kWave + lane < mln.nt) pn1 = a.mtris[mln.tbase + kWave + lane];
+            if (IDPASS) {
+                if (lane < mln.nt) in0 = a.mtri_orig[mln.tbase + lane];
+                if (kWave + lane < mln.nt) in1 = a.mtri_orig[mln.tbase + kWave + lane];
+            }
         }
         // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
         // (image_renderer.cuh:296-305, 82-84)
@@ -340,6 +368,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             if (t0 >= ml.nt || (dbg & 2)) break;
             const int t = t0 + lane;
             const uint32_t pk = half == 0 ? pk0 : pk1;
+            const uint32_t oid = half == 0 ? id0 : id1;
             int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
             int i0 = 0, i1 = 0, i2 = 0;
             if (t < ml.nt) {
@@ -381,9 +410,10 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 rb.c0 = __shfl(r.c0, j); rb.c1 = __shfl(r.c1, j);
                 rb.z0 = __shfl(r.z0, j); rb.z1 = __shfl(r.z1, j); rb.z2 = __shfl(r.z2, j);
                 const int bkx0 = __shfl(kx0, j), bky0 = __shfl(ky0, j), bnx = __shfl(nx, j), bnk = __shfl(nk, j);
+                const uint32_t bid = IDPASS ? (uint32_t)__shfl((int)oid, j) : 0u;
                 for (int q = lane; q < bnk; q += kWave) {
                     const int iy = q / bnx, ix = q - iy * bnx;
-                    raster_sample(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf);
+                    raster_sample<IDPASS>(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf, cid, bid);
                 }
             }
             // small triangles: queue into the wave's ring
@@ -392,6 +422,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             if (qd) {
                 r.meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) | ((uint32_t)(ny - 1) << 28);
                 ring[rec_count + mbcnt64(bq)] = r;
+                if (IDPASS) ring_id[rec_count + mbcnt64(bq)] = oid;
             }
             rec_count += __popcll(bq);
             if (rec_count > kRecCap - kWave) {
@@ -404,11 +435,13 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         v = vn;
         pk0 = pn0;
         pk1 = pn1;
+        id0 = in0;
+        id1 = in1;
     }
     if (rec_count > 0) flush(rec_count);
 }
 
-template <int STRIDE>
+template <int STRIDE, bool COLOUR = false>
 __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int pose = blockIdx.x;
@@ -419,7 +452,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     const int ws = a.ws, hs = a.hs;
     const int nsamp = ws * hs;
 
-    const FusedSmem sm = carve_smem(smem_raw, nsamp, a.bitmap_words);
+    const FusedSmem sm = carve_smem(smem_raw, nsamp, a.bitmap_words, COLOUR);
     for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
     for (int i = tid; i < a.bitmap_words; i += kThreads) sm.bitmap[i] = 0u;
     if (tid < 4) sm.counters[tid] = 0;
@@ -428,6 +461,15 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
     raster_phase<STRIDE>(a, sm, pose);
     __syncthreads();
+    int32_t* cid = nullptr;
+    if constexpr (COLOUR) {
+        // colour id pass (cost_type 1): which triangle left each sample's minimum depth
+        cid = a.cid + (size_t)pose * nsamp;
+        for (int i = tid; i < nsamp; i += kThreads) cid[i] = INT_MAX;
+        __syncthreads();
+        raster_phase<STRIDE, true>(a, sm, pose, cid);
+        __syncthreads();
+    }
 
     // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
     int32_t* queue = reinterpret_cast<int32_t*>(sm.ring) + wave * (kRecCap * (int)sizeof(TriRec) / 4);
@@ -477,9 +519,21 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
                                 }
                     }
                 }
-                // compute_costs.cuh:201-270 (cost types 0 / 2: explained marking only)
-                if (best > a.r2) is_bad = true;
-                else if (bidx != 0x7fffffff) atomicOr(&sm.bitmap[bidx >> 5], 1u << (bidx & 31));
+                // compute_costs.cuh:201-270 (cost types 0 / 2: explained marking; type 1: colour gate first)
+                if (best > a.r2) {
+                    is_bad = true;
+                } else if (bidx != 0x7fffffff) {
+                    bool expl = true;
+                    if constexpr (COLOUR) {
+                        const int id = cid[k];
+                        const float4 lr = a.tri_lab[id == INT_MAX ? 0 : id];  // a valid sample has an id
+                        const float4 lo = a.obs_lab[bidx];
+                        const double cd = colour::colour_distance(lo.x, lo.y, lo.z, lr.x, lr.y, lr.z);
+                        expl = !(cd > (double)a.colour_thr);
+                    }
+                    if (expl) atomicOr(&sm.bitmap[bidx >> 5], 1u << (bidx & 31));
+                    else is_bad = true;
+                }
             }
             my_bad += is_bad ? 1 : 0;
         }
@@ -608,9 +662,12 @@ hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s) {
-    const size_t lds = fused_lds_bytes(a.ws, a.hs, a.bitmap_words);
+    const bool colour = a.cid != nullptr;
+    const size_t lds = fused_lds_bytes(a.ws, a.hs, a.bitmap_words, colour);
     if (a.num_poses <= 0) return hipSuccess;
-    if (a.stride == 8)
+    if (colour)
+        hipLaunchKernelGGL((fused_cost_kernel<0, true>), dim3(a.num_poses), dim3(kThreads), lds, s, a);
+    else if (a.stride == 8)
         hipLaunchKernelGGL(fused_cost_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
     else
         hipLaunchKernelGGL(fused_cost_kernel<0>, dim3(a.num_poses), dim3(kThreads), lds, s, a);

@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out}
-timeout -k 10 500 python -m pytest tests -q -x -m gpu -k "icp or recognizer or metrics" > $OUT/icp_pytest.log 2>&1 || { tail -30 $OUT/icp_pytest.log; exit 1; }
+timeout -k 10 600 python -m pytest tests -q -m gpu ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/icp_pytest.log 2>&1 || { tail -30 $OUT/icp_pytest.log; exit 1; }
 tail -1 $OUT/icp_pytest.log
 if [ -n "$LIBS" ]; then KERNEL=gicp ARGS="--icp" bash tools/ab_time.sh || exit 1; fi
 if [ -f build_ab/prof.so ]; then
