@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Turn two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into per-launch HBM bytes of the fused
-kernel at the bench batch size.  gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE / WRITE_SIZE
+kernel at the bench batch size (median launch).  gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE / WRITE_SIZE
 are in KiB; FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled (an upper bound
 for narrower accesses).  Writes profiles/pmc_traffic.json."""
 import csv
@@ -22,8 +22,9 @@ def main(fetch_csv, write_csv, out, poses_per_launch=10000, threads=256):
     grid = poses_per_launch * threads
     f = load(fetch_csv, "FETCH_SIZE")[grid]
     w = load(write_csv, "WRITE_SIZE")[grid]
-    fetch_kib = sum(f) / len(f)
-    write_kib = sum(w) / len(w)
+    # median over launches: bench.py's first launch also writes the P_r debug z-samples
+    fetch_kib = sorted(f)[len(f) // 2]
+    write_kib = sorted(w)[len(w) // 2]
     res = {
         "poses_per_launch": poses_per_launch,
         "fetch_size_kib_raw": fetch_kib,

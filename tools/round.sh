@@ -1,0 +1,28 @@
+#!/bin/bash
+# Full GPU session: parity tests, smoke, bench, rocprofv3 kernel-trace summary of the bench command,
+# and the two PMC passes (FETCH_SIZE, WRITE_SIZE) of the same command.  Every GPU step has its own
+# time limit; the chain stops at the first failure.
+set -o pipefail
+OUT=${OUT:-gpurun_out}; TAG=${TAG:-r01}
+mkdir -p $OUT; export TMPDIR=/tmp
+if [ -z "$SKIP_TESTS" ]; then
+  echo "== pytest"
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1 || { tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
+  tail -3 $OUT/pytest_gpu_$TAG.log
+  echo "== smoke"
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -30 $OUT/smoke_$TAG.log; exit 1; }
+  cat $OUT/smoke_$TAG.log
+fi
+echo "== bench"
+timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -20 $OUT/bench_$TAG.err; exit 1; }
+cat $OUT/bench_$TAG.json
+echo "== rocprof stats"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python bench.py --no-cpu ${BENCH_ARGS} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
+cat $OUT/prof_bench_$TAG.json
+if [ -z "$SKIP_PMC" ]; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "== pmc $C"
+    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${TAG}_$C -o run -- python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmc_${TAG}_$C.json 2> $OUT/pmc_${TAG}_$C.err || { tail -20 $OUT/pmc_${TAG}_$C.err; exit 1; }
+  done
+fi
+find $OUT -path "*_$TAG*" -name "*.csv" | head -20
