@@ -9,7 +9,8 @@ RCCL all-reduce(MIN).  Inputs are resident in HBM before the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--poses P] [--cpu-seconds S]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
-Rank 0 prints ONE JSON line (see DESIGN.md "Measurement" for the roofline / cpu_baseline fields).
+Rank 0 prints ONE JSON line (see DESIGN.md "Measurement" for the roofline / cpu_baseline fields;
+cpu_reference_path times the reference's own CPU/OMP path, SURVEY.md row a14, on config C1).
 """
 from __future__ import annotations
 
@@ -63,6 +64,33 @@ def cpu_baseline(w, seconds: float):
                       f"render + stride-8 cloud + brute-force 1-NN + costs), OpenMP over poses, {dt:.1f} s"}
 
 
+def cpu_reference_path(seconds: float):
+    """SURVEY.md 8(a) row a14 on BASELINE.json configs[0] (C1): the reference's own CPU/OMP path --
+    render_cpu -> depth2cloud_cpu (stride 1) -> ICP_Point2Plane_cpu against the projective scene -- restated
+    in oracle/ref_cpu_path.cpp, over the 128 3-DoF table-top poses of the 003_cracker_box proxy."""
+    import oracle
+    from perception_amd import workloads
+
+    def render_fn(tris, cnt, p16, pm, W, H, proj):
+        return oracle.ref_render_cpu(tris, p16, W, H, proj)
+
+    c1 = workloads.c1_tabletop(render_fn)
+    sc = c1.scene
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 64))
+    done, iters, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, fit, _, its, _ = oracle.ref_cpu_pipeline(sc.bank.tris, c1.poses, sc.width, sc.height, sc.proj, sc.fx,
+                                                    sc.fy, sc.cx, sc.cy, c1.src_depth_cm, nthreads=threads)
+        done += len(c1.poses)
+        iters += int(its.sum())
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "poses/s", "cores": threads, "kind": "port",
+            "sample": f"C1: {done // len(c1.poses)} passes over 128 3-DoF poses of the 003_cracker_box proxy at "
+                      f"640x480 through render_cpu + depth2cloud_cpu + ICP_Point2Plane_cpu (mean "
+                      f"{iters / max(done, 1):.1f} ICP iterations), one pose per OpenMP thread, {dt:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +98,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--poses", type=int, default=10000, help="candidate poses per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--ref-cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -81,7 +110,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; the modulo only matters for a several-ranks-per-GPU rehearsal (PCORE_DIST_BACKEND=gloo)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     pdist.init_from_env()
     dev = torch.device("cuda", local)
@@ -172,6 +202,7 @@ def main():
     }
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+        line["cpu_reference_path"] = cpu_reference_path(args.ref_cpu_seconds)
     print(json.dumps(line), flush=True)
 
 

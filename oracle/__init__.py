@@ -337,3 +337,99 @@ def evaluate_colour(tris, tri_rgb, tris_model_count, poses, pose_model, width, h
         _c(o_rgb, np.uint8).reshape(-1) if o_xyz.size else np.zeros(3, np.uint8), o_xyz.size // 3,
         _c(pose_obs_total, np.float32), int(calc_obs), sensor_resolution, colour_thr, rc, oc, df, nthreads)
     return rc, oc, df
+
+
+# ---- a14: the reference's CPU/OMP path (ref_cpu_path.cpp) -------------------------------------------
+# ICPConvergenceCriteria defaults (cuda_icp/include/cuda_icp/icp.h:39-51) and Scene_projective's
+# max_dist_diff default (depth_scene.h:11)
+REF_ICP_REL_FITNESS = 1e-5
+REF_ICP_REL_RMSE = 1e-5
+REF_ICP_MAX_ITER = 30
+REF_SCENE_MAX_DIST_DIFF = 0.1
+
+
+def _ref_lib():
+    L = lib()
+    if not getattr(L, "_ref_ready", False):
+        c_int, f = ctypes.c_int, ctypes.c_float
+        L.orc_ref_render_cpu.argtypes = [_f32p, c_int, _f32p, c_int, c_int, c_int, _f32p, _i32p, c_int]
+        L.orc_ref_depth2cloud.restype = c_int
+        L.orc_ref_depth2cloud.argtypes = [_i32p, c_int, c_int, f, f, f, f, _f32p, c_int]
+        L.orc_ref_scene.argtypes = [_i32p, c_int, c_int, f, f, f, f, _f32p, _f32p]
+        L.orc_ref_icp.restype = c_int
+        L.orc_ref_icp.argtypes = [_f32p, c_int, _f32p, _f32p, c_int, c_int, f, f, f, f, f, f, f, c_int, _f32p,
+                                  ctypes.POINTER(f), ctypes.POINTER(f)]
+        L.orc_ref_cpu_pipeline.argtypes = [_f32p, c_int, _f32p, c_int, c_int, c_int, _f32p, f, f, f, f, _i32p, f, f,
+                                           f, c_int, _f32p, _f32p, _f32p, _opt(_i32p), _opt(_i32p), c_int]
+        L.orc_ref_solver666.argtypes = [_f32p, _f32p, _f32p]
+        L._ref_ready = True
+    return L
+
+
+def ref_render_cpu(tris, poses, width, height, proj, nthreads=0):
+    """render_cpu (renderer.cpp:291-330): (N, H, W) int32 cm, no source occlusion."""
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    out = np.zeros((n, height, width), np.int32)
+    _ref_lib().orc_ref_render_cpu(tris, tris.size // 9, poses, n, width, height, _c(proj, np.float32), out, nthreads)
+    return out
+
+
+def ref_depth2cloud(depth, fx, fy, cx, cy):
+    """depth2cloud_cpu at stride 1 (icp.cpp:64-108): (P, 3) float32 metres, row-major order."""
+    d = _c(depth, np.int32)
+    h, w = d.shape
+    out = np.zeros((h * w, 3), np.float32)
+    n = _ref_lib().orc_ref_depth2cloud(d.reshape(-1), w, h, fx, fy, cx, cy, out.reshape(-1), h * w)
+    return out[:n]
+
+
+def ref_scene(depth, fx, fy, cx, cy):
+    """Scene_projective buffers: (H, W, 3) points (dep2pcd) and (H, W, 3) get_normal normals."""
+    d = _c(depth, np.int32)
+    h, w = d.shape
+    pcd = np.zeros((h, w, 3), np.float32)
+    nrm = np.zeros((h, w, 3), np.float32)
+    _ref_lib().orc_ref_scene(d.reshape(-1), w, h, fx, fy, cx, cy, pcd.reshape(-1), nrm.reshape(-1))
+    return pcd, nrm
+
+
+def ref_icp(model_xyz, scene_pcd, scene_normal, fx, fy, cx, cy, max_dist_diff=REF_SCENE_MAX_DIST_DIFF,
+            rel_fitness=REF_ICP_REL_FITNESS, rel_rmse=REF_ICP_REL_RMSE, max_iter=REF_ICP_MAX_ITER):
+    """ICP_Point2Plane_cpu (icp.cpp:116-179) -> (T (4,4) f32, fitness, rmse, iteration, moved cloud)."""
+    pts = np.array(model_xyz, np.float32, copy=True).reshape(-1)
+    h, w = scene_pcd.shape[:2]
+    T = np.zeros(16, np.float32)
+    fit, rmse = ctypes.c_float(0), ctypes.c_float(0)
+    it = _ref_lib().orc_ref_icp(pts, pts.size // 3, _c(scene_pcd, np.float32).reshape(-1),
+                                _c(scene_normal, np.float32).reshape(-1), w, h, fx, fy, cx, cy, max_dist_diff,
+                                rel_fitness, rel_rmse, max_iter, T, ctypes.byref(fit), ctypes.byref(rmse))
+    return T.reshape(4, 4), fit.value, rmse.value, it, pts.reshape(-1, 3)
+
+
+def ref_solver666(A, b):
+    """eigen_slover_666 (icp.cpp:29-36): LDLT solve in double, ZYX Euler + translation -> (4,4) float32."""
+    out = np.zeros(16, np.float32)
+    _ref_lib().orc_ref_solver666(np.ascontiguousarray(np.asarray(A, np.float32).T).reshape(-1),
+                                 _c(b, np.float32).reshape(6), out)
+    return out.reshape(4, 4)
+
+
+def ref_cpu_pipeline(tris, poses, width, height, proj, fx, fy, cx, cy, scene_depth_cm,
+                     max_dist_diff=REF_SCENE_MAX_DIST_DIFF, rel_fitness=REF_ICP_REL_FITNESS,
+                     rel_rmse=REF_ICP_REL_RMSE, max_iter=REF_ICP_MAX_ITER, nthreads=0):
+    """a14 per pose: render_cpu -> depth2cloud_cpu -> ICP_Point2Plane_cpu vs the projective scene.
+    Returns (T (N,4,4), fitness (N,), rmse (N,), iterations (N,), rendered points (N,))."""
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    T = np.zeros((n, 16), np.float32)
+    fit = np.zeros(n, np.float32)
+    rmse = np.zeros(n, np.float32)
+    its = np.zeros(n, np.int32)
+    pts = np.zeros(n, np.int32)
+    _ref_lib().orc_ref_cpu_pipeline(tris, tris.size // 9, poses, n, width, height, _c(proj, np.float32), fx, fy, cx,
+                                    cy, _c(scene_depth_cm, np.int32).reshape(-1), max_dist_diff, rel_fitness,
+                                    rel_rmse, max_iter, T.reshape(-1), fit, rmse, its, pts, nthreads)
+    return T.reshape(n, 4, 4), fit, rmse, its, pts

@@ -139,6 +139,27 @@ void orc_evaluate_colour(const float* tris, int num_tris, const uint8_t* tri_rgb
                          float sensor_resolution, float colour_thr, float* out_rc, float* out_oc, float* out_diff,
                          int nthreads);
 
+/* ---- a14: the reference's CPU/OMP path (ref_cpu_path.cpp) -------------------------------------------
+ * render_cpu (renderer.cpp:228-330: full frame, no source occlusion) -> depth2cloud_cpu at stride 1
+ * (icp.cpp:64-108) -> ICP_Point2Plane_cpu against Scene_projective of the observed depth (icp.cpp:116-179,
+ * depth_scene.h:25-48, get_normal common.cpp:17-107), host float semantics (x86 conversions).
+ * out_T: the ICP transform (metres, row-major 4x4) per pose. */
+void orc_ref_render_cpu(const float* tris, int num_tris, const float* poses, int num_poses, int width, int height,
+                        const float* proj, int32_t* out, int nthreads);
+int orc_ref_depth2cloud(const int32_t* depth, int width, int height, float fx, float fy, float cx, float cy,
+                        float* out_xyz, int cap);
+void orc_ref_scene(const int32_t* depth, int width, int height, float fx, float fy, float cx, float cy,
+                   float* out_pcd, float* out_normal);
+int orc_ref_icp(float* model_xyz, int n, const float* scene_pcd, const float* scene_normal, int width, int height,
+                float fx, float fy, float cx, float cy, float max_dist_diff, float rel_fitness, float rel_rmse,
+                int max_iter, float* out_T, float* out_fitness, float* out_rmse);
+void orc_ref_solver666(const float* A, const float* b, float* out_T);
+void orc_ref_cpu_pipeline(const float* tris, int num_tris, const float* poses, int num_poses, int width, int height,
+                          const float* proj, float fx, float fy, float cx, float cy, const int32_t* scene_depth,
+                          float max_dist_diff, float rel_fitness, float rel_rmse, int max_iter, float* out_T,
+                          float* out_fitness, float* out_rmse, int32_t* out_iters, int32_t* out_points,
+                          int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

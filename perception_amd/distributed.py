@@ -29,7 +29,9 @@ def init_from_env(backend: str = None):
     if world <= 1 or dist.is_initialized():
         return
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # PCORE_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU (RCCL refuses
+        # two ranks on one device); production multi-GPU runs use "nccl" = RCCL over xGMI
+        backend = os.environ.get("PCORE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kw = {}
     if backend == "nccl":

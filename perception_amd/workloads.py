@@ -7,6 +7,7 @@ unprojected with depth2cloud_global on the GPU.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from typing import Sequence
 
@@ -102,3 +103,37 @@ def step(w: Workload, out, keys):
                                  stride=w.stride, out=out)
     w.core.select(rc, oc, w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
     return rc, oc, df
+
+
+@dataclass
+class C1Workload:
+    """BASELINE.json configs[0]: one 003_cracker_box proxy, 128 3-DoF poses (4 x 4 x 8 yaw steps of pi/4 on
+    the table plane, the ground truth among them) at 640x480."""
+    scene: "syn.TabletopScene"
+    poses: np.ndarray          # (128, 16) f32 cm-scaled mat4x4, camera frame
+    states: np.ndarray         # (128, 3) x, y, yaw in the world
+    gt_index: int
+    src_depth_cm: np.ndarray   # (H, W) int32 cm (search_env.cpp:2487-2498)
+
+
+def c1_tabletop(render_fn, gt=(0.60, -0.04, math.pi / 4), step=0.04) -> C1Workload:
+    """The C1 scene (render_fn renders the GT object into the table scene) and its 128 candidate poses."""
+    from .recognizer import preprocessing_transform
+    from .tabletop import yaw_pose_matrix
+    names = ["003_cracker_box"]
+    bank = syn.model_bank(names)
+    pre = preprocessing_transform(bank.models[0], six_dof=False)
+    sc = syn.make_tabletop_scene(names, [gt], [pre], render_fn, table_height=0.7,
+                                 rng=np.random.default_rng(syn.SEED))
+    optical_inv = np.linalg.inv(sc.camera_pose @ syn.CAM_TO_BODY)
+    states, mats = [], []
+    for ix in range(4):
+        for iy in range(4):
+            for k in range(8):
+                x, y, yaw = gt[0] + (ix - 2) * step, gt[1] + (iy - 2) * step, k * math.pi / 4
+                states.append((x, y, yaw))
+                mats.append(optical_inv @ yaw_pose_matrix(x, y, sc.table_height, yaw) @ pre)
+    gt_index = (2 * 4 + 2) * 8 + 1
+    div = np.float32(sc.depth_factor) / np.float32(100.0)
+    src_cm = (sc.depth_raw.astype(np.float32) / div).astype(np.int32)
+    return C1Workload(sc, init_from_eigen_batch(np.stack(mats)), np.array(states), gt_index, src_cm)

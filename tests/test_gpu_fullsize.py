@@ -1,0 +1,114 @@
+"""GPU tests at BASELINE.json's full sizes (the bench workloads themselves): a seeded random subset checked
+bit-exactly against the CPU oracle, plus size-independent properties over the whole batch -- permutation
+and chunking invariance of the per-pose costs (poses are independent), the ground-truth pose scoring 0 and
+winning the selection, and selection equal to the oracle's rule applied to the GPU's own costs."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle
+from perception_amd import synthetic as syn
+from perception_amd import workloads
+from perception_amd._native import PCORE_KEY_NONE
+from perception_amd.core import decode_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_subset(w, idx):
+    sc = w.scene
+    poses = w.poses.cpu().numpy()[idx]
+    pm = w.pose_model.cpu().numpy()[idx]
+    tot = w.pose_obs_total.cpu().numpy()[idx]
+    xyz = w.obs_xyz.cpu().numpy()
+    lab = w.obs_label.cpu().numpy()
+    order = np.argsort(lab, kind="stable")
+    oxyz, olab = xyz[order], lab[order]
+    nl = int(olab.max()) + 1
+    ls = np.array([np.searchsorted(olab, L, "left") for L in range(nl)], np.int32)
+    le = np.array([np.searchsorted(olab, L, "right") for L in range(nl)], np.int32)
+    return oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, poses, pm, pm, sc.width, sc.height, sc.proj,
+                           sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, ls, le,
+                           tot, 2, True, 0.01)
+
+
+def _bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def c2():
+    w = workloads.build(poses_per_model=10000)
+    rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+    torch.cuda.synchronize()
+    return w, (rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy())
+
+
+def test_c2_random_subset_bit_exact_vs_oracle(c2):
+    w, (rc, oc, df) = c2
+    idx = np.sort(np.random.default_rng(20250112).choice(len(rc), 64, replace=False))
+    idx = np.unique(np.concatenate([idx, [w.gt_index[0]]]))
+    orc, ooc, odf = _oracle_subset(w, idx)
+    assert np.array_equal(_bits(rc[idx]), _bits(orc))
+    assert np.array_equal(_bits(oc[idx]), _bits(ooc))
+    assert np.array_equal(_bits(df[idx]), _bits(odf))
+
+
+def test_c2_permutation_and_chunking_invariance(c2):
+    w, (rc, oc, df) = c2
+    n = len(rc)
+    perm = torch.from_numpy(np.random.default_rng(7).permutation(n)).to(w.poses.device)
+    prc, poc, pdf = w.core.evaluate(w.poses[perm].contiguous(), w.pose_model[perm].contiguous(),
+                                    w.pose_label[perm].contiguous(), w.pose_obs_total[perm].contiguous(),
+                                    stride=w.stride)
+    p = perm.cpu().numpy()
+    assert np.array_equal(_bits(prc.cpu().numpy()), _bits(rc[p]))
+    assert np.array_equal(_bits(poc.cpu().numpy()), _bits(oc[p]))
+    assert np.array_equal(_bits(pdf.cpu().numpy()), _bits(df[p]))
+    parts = []
+    for lo, hi in ((0, 1), (1, 4097), (4097, 9999), (9999, n)):
+        parts.append(w.core.evaluate(w.poses[lo:hi], w.pose_model[lo:hi], w.pose_label[lo:hi],
+                                     w.pose_obs_total[lo:hi], stride=w.stride)[0].cpu().numpy())
+    assert np.array_equal(_bits(np.concatenate(parts)), _bits(rc))
+
+
+def test_c2_gt_pose_wins_and_selection_matches_oracle_rule(c2):
+    w, (rc, oc, df) = c2
+    gt = w.gt_index[0]
+    assert rc[gt] == 0.0
+    keys = w.core.select(torch.from_numpy(rc).cuda(), torch.from_numpy(oc).cuda(), w.pose_model, w.num_models)
+    cost, idx = decode_keys(keys)
+    ocost, oidx = oracle.select(rc, oc, w.pose_model.cpu().numpy(), w.num_models)
+    assert int(idx[0]) == int(oidx[0]) == gt and int(cost[0]) == int(ocost[0])
+
+
+def test_c5_1280x720_subset_bit_exact_vs_oracle():
+    """C5's camera (1280x720, 57.6 KB LDS z-samples per pose) on a 2,000-pose batch."""
+    w = workloads.build(poses_per_model=2000, cam=syn.CAM_1280)
+    rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+    rc, oc, df = rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy()
+    idx = np.sort(np.random.default_rng(5).choice(len(rc), 24, replace=False))
+    idx = np.unique(np.concatenate([idx, [w.gt_index[0]]]))
+    orc, ooc, odf = _oracle_subset(w, idx)
+    assert np.array_equal(_bits(rc[idx]), _bits(orc))
+    assert np.array_equal(_bits(oc[idx]), _bits(ooc))
+    assert np.array_equal(_bits(df[idx]), _bits(odf))
+    assert (rc >= 0).sum() > len(rc) // 4
+
+
+def test_c4_21_models_selection_bit_exact_vs_oracle():
+    """C4's 21-model bank (per-GPU share scaled down): every model's winner equals the oracle rule over the
+    GPU costs, and a random subset of the costs equals the oracle."""
+    w = workloads.build(names=list(syn.YCB_PROXIES), poses_per_model=120)
+    rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=rc.device)
+    w.core.select(rc, oc, w.pose_model, w.num_models, keys=keys)
+    rc, oc = rc.cpu().numpy(), oc.cpu().numpy()
+    cost, idx = decode_keys(keys)
+    ocost, oidx = oracle.select(rc, oc, w.pose_model.cpu().numpy(), w.num_models)
+    assert np.array_equal(idx, oidx) and np.array_equal(cost, ocost)
+    sub = np.sort(np.random.default_rng(9).choice(len(rc), 42, replace=False))
+    orc, ooc, _ = _oracle_subset(w, sub)
+    assert np.array_equal(_bits(rc[sub]), _bits(orc))
+    assert np.array_equal(_bits(oc[sub]), _bits(ooc))

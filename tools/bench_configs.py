@@ -2,6 +2,8 @@
 """Time the BASELINE.json configs other than the headline one on ONE GPU (per-GPU shares of the
 multi-GPU configs).  Prints one JSON line per config.  Not the driver's bench (bench.py is).
 
+  C1  1 mesh, 128 3-DoF table-top poses, render + GICP + re-render + score (cost type 0), 640x480 -- the GPU
+      side of the workload bench.py's cpu_reference_path times on the reference's CPU/OMP path
   C2  1 mesh, 10k poses, render + score, 640x480
   C3  5 objects, 50k poses, render + GICP + re-render + score, 640x480 (+ argmin vs GT)
   C4  21 objects, 200k poses over 8 GPUs -> 25k poses per GPU, render + score
@@ -92,15 +94,53 @@ def run(name, names, per_model, cam, icp, steps, warmup):
     torch.cuda.empty_cache()
 
 
+def run_c1(steps, warmup, stride=4):
+    """C1 on the GPU: the 128 3-DoF poses of workloads.c1_tabletop, scored against the whole observed cloud
+    (3-DoF, no labels), with and without GICP."""
+    from perception_amd.core import PoseCore
+    from perception_amd.model import compute_proj
+    dev = torch.device("cuda", 0)
+    bank = syn.model_bank(["003_cracker_box"])
+    core = PoseCore(0)
+    core.upload_meshes(bank.tris, bank.tris_model_count)
+    cam = syn.CAM_640
+    core.set_camera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"],
+                    compute_proj(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["width"], cam["height"]))
+    W, H = cam["width"], cam["height"]
+    core.set_observation(torch.zeros((H, W), dtype=torch.int32, device=dev), None,
+                         torch.zeros((0, 3), dtype=torch.float32, device=dev), None, 0.01)
+    c1 = workloads.c1_tabletop(workloads.gpu_render_fn(core, dev))
+    sc = c1.scene
+    xyz, _ = core.observed_cloud_bounded(torch.from_numpy(sc.depth_raw).to(dev), stride, sc.depth_factor)
+    core.set_observation(torch.from_numpy(c1.src_depth_cm).to(dev), None, xyz, None, 0.0075)
+    n = len(c1.poses)
+    poses = torch.from_numpy(c1.poses).to(dev)
+    pm = torch.zeros(n, dtype=torch.int32, device=dev)
+    tot = torch.full((n,), float(xyz.shape[0]), dtype=torch.float32, device=dev)
+    for icp in (False, True):
+        if icp:
+            fn = lambda: core.evaluate_icp(poses, pm, None, tot, cost_type=0, stride=stride,  # noqa: E731
+                                           sensor_resolution=0.0075)
+        else:
+            fn = lambda: core.evaluate(poses, pm, None, tot, cost_type=0, stride=stride,  # noqa: E731
+                                       sensor_resolution=0.0075)
+        dt = timed(fn, steps, warmup)
+        print(json.dumps({"config": "C1", "poses": n, "models": 1, "width": W, "height": H, "stride": stride,
+                          "icp": icp, "s_per_step": dt, "poses_per_s": n / dt, "observed_points": int(xyz.shape[0])}),
+              flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="C2,C3,C4,C5")
+    ap.add_argument("--configs", default="C1,C2,C3,C4,C5")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the per-GPU pose count")
     a = ap.parse_args()
     sel = a.configs.split(",")
     sc = a.scale
+    if "C1" in sel:
+        run_c1(max(a.steps, 10), max(a.warmup, 2))
     if "C2" in sel:
         run("C2", ["003_cracker_box"], int(10000 * sc), syn.CAM_640, False, a.steps, a.warmup)
     if "C3" in sel:
