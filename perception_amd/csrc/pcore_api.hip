@@ -63,6 +63,7 @@ struct pcore_ctx {
     int max_seg = 0;
     DevBuf<float4> tgt;
     DevBuf<int32_t> seg_lo, seg_hi, seg_cnt;
+    std::vector<int32_t> seg_lo_h, seg_cnt_h;  // host copies (grid covariance launches)
     DevBuf<double> tgt_cov_label, tgt_cov_all;
     int cov_k_label = 0, cov_k_all = 0;
     // GICP scratch
@@ -229,6 +230,7 @@ void build_grid(const std::vector<float4>& pts, float radius, LabelGrid& g, std:
     if (pts.empty()) {
         g.ox = g.oy = g.oz = 0.0f;
         g.inv_c = 1.0f;
+        g.cell = 1.0f;
         g.nx = g.ny = g.nz = 1;
         cell_start.push_back((int32_t)grid_pts.size());
         cell_start.push_back((int32_t)grid_pts.size());
@@ -253,6 +255,7 @@ void build_grid(const std::vector<float4>& pts, float radius, LabelGrid& g, std:
     g.oy = lo[1];
     g.oz = lo[2];
     g.inv_c = 1.0f / cell;
+    g.cell = cell;
     g.nx = std::max(1, (int)std::floor((hi[0] - lo[0]) * g.inv_c) + 1);
     g.ny = std::max(1, (int)std::floor((hi[1] - lo[1]) * g.inv_c) + 1);
     g.nz = std::max(1, (int)std::floor((hi[2] - lo[2]) * g.inv_c) + 1);
@@ -566,6 +569,8 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
         HIPC(c, dev_upload(c->seg_lo, slo));
         HIPC(c, dev_upload(c->seg_hi, shi));
         HIPC(c, dev_upload(c->seg_cnt, scnt));
+        c->seg_lo_h = slo;
+        c->seg_cnt_h = scnt;
         c->num_obs = num_obs;
         c->max_seg = mx;
         c->cov_k_label = 0;
@@ -743,12 +748,17 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     const int nl = c->num_grids;
     if (six && c->cov_k_label != k) {
         HIPC(c, dev_reserve(c->tgt_cov_label, (size_t)6 * std::max(c->num_obs, 1)));
-        HIPC(c, launch_covariances(c->tgt.p, c->seg_lo.p, c->seg_cnt.p, 0, nl, k, c->tgt_cov_label.p, s));
+        HIPC(c, launch_covariances(c->tgt.p, c->seg_lo.p, c->seg_cnt.p, 0, nl, k, c->tgt_cov_label.p, s, kGridNNMin));
+        HIPC(c, launch_covariances_grid(c->tgt.p, c->seg_lo_h.data(), c->seg_cnt_h.data(), nl, 0, c->grids.p,
+                                        c->cell_start.p, c->grid_pts.p, k, c->tgt_cov_label.p, s));
         c->cov_k_label = k;
     }
     if (!six && c->cov_k_all != k) {
         HIPC(c, dev_reserve(c->tgt_cov_all, (size_t)6 * std::max(c->num_obs, 1)));
-        HIPC(c, launch_covariances(c->tgt.p, c->seg_lo.p + nl, c->seg_cnt.p + nl, 0, 1, k, c->tgt_cov_all.p, s));
+        HIPC(c, launch_covariances(c->tgt.p, c->seg_lo.p + nl, c->seg_cnt.p + nl, 0, 1, k, c->tgt_cov_all.p, s,
+                                   kGridNNMin));
+        HIPC(c, launch_covariances_grid(c->tgt.p, c->seg_lo_h.data() + nl, c->seg_cnt_h.data() + nl, 1, nl, c->grids.p,
+                                        c->cell_start.p, c->grid_pts.p, k, c->tgt_cov_all.p, s));
         c->cov_k_all = k;
     }
     const int nsamp = ws * hs;
@@ -784,6 +794,9 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.rot_eps = ip->rotation_epsilon;
     g.trans_eps = ip->transformation_epsilon;
     g.work_counter = c->icp_counter.p;
+    g.grids = c->grids.p;
+    g.cell_start = c->cell_start.p;
+    g.grid_pts = c->grid_pts.p;
     for (int base = 0; base < num_poses; base += chunk) {
         const int n = std::min(chunk, num_poses - base);
         a.poses = d_poses + (size_t)16 * base;

@@ -113,15 +113,116 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
+// Exact neighbour search over a segment's grid (segments above kGridNNMin points)
+// ------------------------------------------------------------------------------------------------
+//
+// Cells are visited in shells of growing Chebyshev radius r around the query's cell.  A point in an
+// unvisited cell has |floor(fp) - floor(fq)| >= r + 1 on some axis, hence |fp - fq| > r in the grid's
+// float cell coordinates, hence a true axis distance above (r - eps) * cell and a float squared distance
+// above B^2 (1 - 3e-7) with B = (r - 0.01 - 1e-6 |fq|) * cell.  Once the caller's limit (the best
+// distance, or the k-th best once k are held) is below 0.99999 B^2, no unvisited point can reach or tie
+// it, so the result equals the brute-force scan's lexicographic minimum of (float distance, index).
+// Returns false when the cell budget runs out first (or the query is far outside the grid): the caller
+// then scans the whole segment.  Non-finite queries are the caller's business.
+constexpr int kShellBudget = 343;  // cells, r <= 3 around an in-grid query
+
+template <typename Visit, typename Limit>
+__device__ __forceinline__ bool grid_shells(const LabelGrid& g, const int32_t* cell_start, float qx, float qy,
+                                            float qz, Visit&& visit, Limit&& limit) {
+    const float fx = (qx - g.ox) * g.inv_c, fy = (qy - g.oy) * g.inv_c, fz = (qz - g.oz) * g.inv_c;
+    const float fm = fmaxf(fabsf(fx), fmaxf(fabsf(fy), fabsf(fz)));
+    if (!(fm < 65536.0f)) return false;
+    const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+    int visited = 0;
+    for (int r = 0;; r++) {
+        const int z0 = max(0, cz - r), z1 = min(g.nz - 1, cz + r);
+        const int y0 = max(0, cy - r), y1 = min(g.ny - 1, cy + r);
+        const int x0 = max(0, cx - r), x1 = min(g.nx - 1, cx + r);
+        for (int iz = z0; iz <= z1; iz++)
+            for (int iy = y0; iy <= y1; iy++) {
+                const int row = g.cell_base + (iz * g.ny + iy) * g.nx;
+                const bool face = iz == cz - r || iz == cz + r || iy == cy - r || iy == cy + r;
+                if (face) {
+                    for (int ix = x0; ix <= x1; ix++) visit(cell_start[row + ix], cell_start[row + ix + 1]);
+                    visited += x1 >= x0 ? x1 - x0 + 1 : 0;
+                } else {
+                    if (cx - r >= 0 && cx - r < g.nx) {
+                        visit(cell_start[row + cx - r], cell_start[row + cx - r + 1]);
+                        visited++;
+                    }
+                    if (r > 0 && cx + r >= 0 && cx + r < g.nx) {
+                        visit(cell_start[row + cx + r], cell_start[row + cx + r + 1]);
+                        visited++;
+                    }
+                }
+            }
+        if (cx - r <= 0 && cx + r >= g.nx - 1 && cy - r <= 0 && cy + r >= g.ny - 1 && cz - r <= 0 &&
+            cz + r >= g.nz - 1)
+            return true;  // every cell visited
+        const float B = ((float)r - 0.01f - 1e-6f * fm) * g.cell;
+        if (B > 0.0f && limit() < B * B * 0.99999f) return true;
+        if (visited >= kShellBudget) return false;
+    }
+}
+
+// k best (distance, index) pairs in lexicographic order, as the brute-force insertion keeps them
+template <int KMAX>
+__device__ __forceinline__ void knn_insert_lex(float (&nd)[KMAX], int (&nb)[KMAX], int& cnt, int k, float d, int j) {
+    if (cnt == k && !(d < nd[k - 1] || (d == nd[k - 1] && j < nb[k - 1]))) return;
+    const int pos = cnt < k ? cnt : k - 1;
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) c += (q < pos && (nd[q] > d || (nd[q] == d && nb[q] > j))) ? 1 : 0;
+    const int fin = pos - c;
+#pragma unroll
+    for (int q = KMAX - 1; q >= 1; q--)
+        if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
+#pragma unroll
+    for (int q = 0; q < KMAX; q++)
+        if (q == fin) { nd[q] = d; nb[q] = j; }
+    if (cnt < k) cnt++;
+}
+
+// mean / covariance (double, list order) of the listed neighbours and PLANE regularisation (orc covariance_one)
+template <int KMAX>
+__device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[KMAX], int cnt, double* out6) {
+    double mx = 0.0, my = 0.0, mz = 0.0;
+#pragma unroll
+    for (int q = 0; q < KMAX; q++)
+        if (q < cnt) {
+            const float4 p = P[nb[q]];
+            mx += (double)p.x; my += (double)p.y; mz += (double)p.z;
+        }
+    const double kd = (double)cnt;
+    mx = mx / kd; my = my / kd; mz = mz / kd;
+    double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < KMAX; q++)
+        if (q < cnt) {
+            const float4 p = P[nb[q]];
+            const double dx = (double)p.x - mx, dy = (double)p.y - my, dz = (double)p.z - mz;
+            c6[0] += dx * dx; c6[1] += dx * dy; c6[2] += dx * dz;
+            c6[3] += dy * dy; c6[4] += dy * dz; c6[5] += dz * dz;
+        }
+#pragma unroll
+    for (int e = 0; e < 6; e++) c6[e] = c6[e] / kd;
+    double r6[6];
+    plane_regularize(c6, r6);
+#pragma unroll
+    for (int e = 0; e < 6; e++) out6[e] = r6[e];
+}
+
+// ------------------------------------------------------------------------------------------------
 // covariances
 // ------------------------------------------------------------------------------------------------
 template <int KMAX>
 __global__ void __launch_bounds__(kGThreads) covariance_kernel(const float4* pts, const int32_t* seg_off,
                                                                const int32_t* seg_cnt, int seg_stride, int k,
-                                                               double* cov_out) {
+                                                               double* cov_out, int max_n) {
     const int sg = blockIdx.x;
     const int off = seg_off ? seg_off[sg] : sg * seg_stride;
     const int n = seg_cnt[sg];
+    if (n > max_n) return;  // covariance_grid_kernel's segment
     const float4* P = pts + off;
     double* C = cov_out + (size_t)6 * off;
     for (int i = threadIdx.x; i < n; i += kGThreads) {
@@ -152,44 +253,74 @@ __global__ void __launch_bounds__(kGThreads) covariance_kernel(const float4* pts
                 if (q == fin) { nd[q] = d; nb[q] = j; }
             if (cnt < k) cnt++;
         }
-        double mx = 0.0, my = 0.0, mz = 0.0;
-#pragma unroll
-        for (int q = 0; q < KMAX; q++)
-            if (q < cnt) {
-                const float4 p = P[nb[q]];
-                mx += (double)p.x; my += (double)p.y; mz += (double)p.z;
-            }
-        const double kd = (double)cnt;
-        mx = mx / kd; my = my / kd; mz = mz / kd;
-        double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < KMAX; q++)
-            if (q < cnt) {
-                const float4 p = P[nb[q]];
-                const double dx = (double)p.x - mx, dy = (double)p.y - my, dz = (double)p.z - mz;
-                c6[0] += dx * dx; c6[1] += dx * dy; c6[2] += dx * dz;
-                c6[3] += dy * dy; c6[4] += dy * dz; c6[5] += dz * dz;
-            }
-#pragma unroll
-        for (int e = 0; e < 6; e++) c6[e] = c6[e] / kd;
-        double r6[6];
-        plane_regularize(c6, r6);
-#pragma unroll
-        for (int e = 0; e < 6; e++) C[(size_t)6 * i + e] = r6[e];
+        cov_from_list<KMAX>(P, nb, cnt, C + (size_t)6 * i);
     }
 }
 
+// Segments above kGridNNMin points: one thread per point, k-NN by the exact grid shell search
+template <int KMAX>
+__global__ void __launch_bounds__(kGThreads) covariance_grid_kernel(const float4* pts, int off, int n,
+                                                                    const LabelGrid* grid, const int32_t* cell_start,
+                                                                    const float4* gpts, int k, double* cov_out) {
+    const int i = blockIdx.x * kGThreads + threadIdx.x;
+    if (i >= n) return;
+    const LabelGrid g = *grid;
+    const float4* P = pts + off;
+    const float4 xi = P[i];
+    float nd[KMAX];
+    int nb[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) { nd[q] = 0.0f; nb[q] = 0; }
+    int cnt = 0;
+    auto visit = [&](int b, int e) {
+        for (int pi = b; pi < e; pi++) {
+            const float4 o = gpts[pi];
+            knn_insert_lex<KMAX>(nd, nb, cnt, k, sqdist3(xi.x, xi.y, xi.z, o.x, o.y, o.z), __float_as_int(o.w));
+        }
+    };
+    const bool ok = isfinite(xi.x) && isfinite(xi.y) && isfinite(xi.z) &&
+                    grid_shells(g, cell_start, xi.x, xi.y, xi.z, visit, [&] { return cnt == k ? nd[k - 1] : INFINITY; });
+    if (!ok) {
+        cnt = 0;
+        for (int j = 0; j < n; j++) {
+            const float4 xj = P[j];
+            knn_insert_lex<KMAX>(nd, nb, cnt, k, sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z), j);
+        }
+    }
+    cov_from_list<KMAX>(P, nb, cnt, cov_out + (size_t)6 * (off + i));
+}
+
 hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const int32_t* seg_cnt, int seg_stride,
-                              int num_segs, int k, double* cov_out, hipStream_t s) {
+                              int num_segs, int k, double* cov_out, hipStream_t s, int max_n) {
     if (num_segs <= 0) return hipSuccess;
     if (k <= 0 || k > kMaxK) return hipErrorInvalidValue;
     if (k <= 10)
         hipLaunchKernelGGL(covariance_kernel<10>, dim3(num_segs), dim3(kGThreads), 0, s, pts, seg_off, seg_cnt,
-                           seg_stride, k, cov_out);
+                           seg_stride, k, cov_out, max_n);
     else
         hipLaunchKernelGGL(covariance_kernel<kMaxK>, dim3(num_segs), dim3(kGThreads), 0, s, pts, seg_off, seg_cnt,
-                           seg_stride, k, cov_out);
+                           seg_stride, k, cov_out, max_n);
     return hipGetLastError();
+}
+
+hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_host, const int32_t* seg_cnt_host,
+                                   int num_segs, int first_grid, const LabelGrid* grids, const int32_t* cell_start,
+                                   const float4* grid_pts, int k, double* cov_out, hipStream_t s) {
+    if (k <= 0 || k > kMaxK) return hipErrorInvalidValue;
+    for (int sg = 0; sg < num_segs; sg++) {
+        const int n = seg_cnt_host[sg];
+        if (n <= kGridNNMin) continue;
+        const dim3 blocks((n + kGThreads - 1) / kGThreads);
+        if (k <= 10)
+            hipLaunchKernelGGL(covariance_grid_kernel<10>, blocks, dim3(kGThreads), 0, s, pts, seg_off_host[sg], n,
+                               grids + first_grid + sg, cell_start, grid_pts, k, cov_out);
+        else
+            hipLaunchKernelGGL(covariance_grid_kernel<kMaxK>, blocks, dim3(kGThreads), 0, s, pts, seg_off_host[sg], n,
+                               grids + first_grid + sg, cell_start, grid_pts, k, cov_out);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -254,6 +385,32 @@ __device__ __forceinline__ void scan_targets(const TgtTile& T, int tn, int t0, f
     }
     if (bB < bA || (bB == bA && jB >= 0 && jB < jA)) { bA = bB; jA = jB; }
     if (bA < best) { best = bA; j = t0 + jA; }  // earlier tiles hold lower indices
+}
+
+// Nearest target by the segment's grid (segments above kGridNNMin): the lexicographic minimum of (float
+// squared distance, index) -- the brute-force scan's first strict minimum -- or j = -1 when no distance is
+// below +inf (a non-finite query).  Falls back to an in-order scan of the segment.
+__device__ __forceinline__ void grid_nn(const LabelGrid& G, const int32_t* cell_start, const float4* gpts,
+                                        const float4* tgt, int nt, float qx, float qy, float qz, float& best, int& j) {
+    best = INFINITY;
+    j = -1;
+    if (!(isfinite(qx) && isfinite(qy) && isfinite(qz))) return;
+    auto visit = [&](int b, int e) {
+        for (int pi = b; pi < e; pi++) {
+            const float4 o = gpts[pi];
+            const float d = sqdist3(qx, qy, qz, o.x, o.y, o.z);
+            const int oi = __float_as_int(o.w);
+            if (d < best || (d == best && j >= 0 && oi < j)) { best = d; j = oi; }
+        }
+    };
+    if (grid_shells(G, cell_start, qx, qy, qz, visit, [&] { return best; })) return;
+    best = INFINITY;
+    j = -1;
+    for (int i = 0; i < nt; i++) {
+        const float4 o = tgt[i];
+        const float d = sqdist3(qx, qy, qz, o.x, o.y, o.z);
+        if (d < best) { best = d; j = i; }
+    }
 }
 
 __device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6]) {
@@ -404,6 +561,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
         const double* tcov = g.tgt_cov + (size_t)6 * lo;
         const float4* tgt = g.tgt + lo;
         const bool resident = nt <= kTgtTile;  // the whole segment stays in LDS for all iterations
+        const bool use_grid = nt > kGridNNMin && g.grids != nullptr && seg >= 0;  // exact grid shell search
+        LabelGrid G{};
+        if (use_grid) G = g.grids[seg];
         if (resident) stage_targets<NT>(T, tgt, min(nt, kTgtTile), tid);
         if (tid == 0) {
             for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
@@ -446,6 +606,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 // nearest target: first strict minimum of the float squared distance (orc gicp_nn)
                 int j = -1;
                 float best = INFINITY;
+                if (use_grid) {
+                    if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qx, qy, qz, best, j);
+                } else
                 for (int t0 = 0; t0 < nt; t0 += kTgtTile) {
                     const int tn = min(kTgtTile, nt - t0);
                     if (!resident) {
@@ -459,7 +622,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 p_ok = act && j >= 0;
                 if (p_ok) {
                     // a selected target is finite, so the staged copy equals the original
-                    p_tj = resident ? make_float4(T.x[j], T.y[j], T.z[j], 0.0f) : tgt[j];
+                    p_tj = (resident && !use_grid) ? make_float4(T.x[j], T.y[j], T.z[j], 0.0f) : tgt[j];
                     load_cov(tcov, j, p_ct);
 #pragma unroll
                     for (int k = 0; k < 3; k++) p_q[k] = q[k];

@@ -27,7 +27,8 @@ struct LabelGrid {
     int32_t nx, ny, nz;
     int32_t cell_base;  // offset of this grid's CSR row pointer in cell_start (nx*ny*nz + 1 entries)
     int32_t pt_count;   // points of this label (bitmap size)
-    int32_t pad0, pad1, pad2;
+    float cell;         // cell edge (inv_c = 1 / cell, rounded)
+    int32_t pad1, pad2;
 };
 
 struct FusedArgs {
@@ -99,12 +100,27 @@ struct GicpArgs {
     int32_t max_iter;
     double rot_eps, trans_eps;
     int32_t* work_counter;    // device int, zeroed by launch_gicp (persistent-wave pose queue)
+    // neighbour grids of the segments (grids[seg], same indices as seg_lo / seg_hi): segments larger than
+    // kGridNNMin targets take the exact grid search instead of the LDS scan
+    const LabelGrid* grids;
+    const int32_t* cell_start;
+    const float4* grid_pts;
 };
+
+// segments above this many points use the exact shell search of their neighbour grid (GICP
+// correspondences and target covariances); smaller ones the brute-force scans
+constexpr int kGridNNMin = 2048;
 
 // launchers (pcore_kernels.hip)
 hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s);
+// brute-force k-NN covariances, one workgroup per segment; segments above max_n points are skipped
 hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const int32_t* seg_cnt, int seg_stride,
-                              int num_segs, int k, double* cov_out, hipStream_t s);
+                              int num_segs, int k, double* cov_out, hipStream_t s, int max_n = 0x7fffffff);
+// covariances of the segments above kGridNNMin points via their grids (grids[first_grid + seg]), one
+// thread per point; seg_off_host / seg_cnt_host: host copies of the segment table
+hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_host, const int32_t* seg_cnt_host,
+                                   int num_segs, int first_grid, const LabelGrid* grids, const int32_t* cell_start,
+                                   const float4* grid_pts, int k, double* cov_out, hipStream_t s);
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s);
 // pcore_metrics.hip
 int pose_dist_blocks(int n);

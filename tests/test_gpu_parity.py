@@ -350,3 +350,37 @@ def test_observed_cloud_bounded_matches_oracle(one_object):
     xyz, _ = core.observed_cloud_bounded(t["raw"], 8, sc.depth_factor)
     ref, _ = core.observed_cloud(t["raw"], None, 8, sc.depth_factor)
     assert torch.equal(xyz, ref)
+
+
+def test_evaluate_icp_3dof_whole_scene_targets_matches_oracle():
+    """C1's table-top scene with the WHOLE observed cloud as the GICP target (~19k points at stride 4, no
+    labels): correspondences and target covariances take the exact grid shell search; the result must equal
+    the oracle's brute-force scans bit for bit."""
+    from perception_amd import workloads
+    from tests.helpers import oracle_render_fn
+    c1 = workloads.c1_tabletop(oracle_render_fn)
+    sc = c1.scene
+    core = PoseCore(0)
+    core.upload_meshes(sc.bank.tris, sc.bank.tris_model_count)
+    core.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+    dev = torch.device("cuda", 0)
+    xyz, _ = core.observed_cloud_bounded(torch.from_numpy(sc.depth_raw).to(dev), 4, sc.depth_factor)
+    assert xyz.shape[0] > 4 * 2048
+    core.set_observation(torch.from_numpy(c1.src_depth_cm).to(dev), None, xyz, None, 0.0075)
+    idx = np.array([c1.gt_index, 3, 70], np.int64)
+    n = len(idx)
+    poses = c1.poses[idx]
+    tot = np.full(n, xyz.shape[0], np.float32)
+    adj, iters, rc, oc, df = core.evaluate_icp(torch.from_numpy(poses).to(dev), torch.zeros(n, dtype=torch.int32,
+                                               device=dev), None, torch.from_numpy(tot).to(dev), cost_type=0,
+                                               stride=4, sensor_resolution=0.0075)
+    oxyz = xyz.cpu().numpy()
+    ocov = oracle.covariances(oxyz)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, poses, np.zeros(n, np.int32), None, sc.width, sc.height, sc.proj,
+        c1.src_depth_cm, None, 1.0, 4, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, ocov, None, None, tot, 0, True,
+        0.0075)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
