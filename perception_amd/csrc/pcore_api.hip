@@ -64,6 +64,8 @@ struct pcore_ctx {
     DevBuf<float4> tgt;
     DevBuf<int32_t> seg_lo, seg_hi, seg_cnt;
     std::vector<int32_t> seg_lo_h, seg_cnt_h;  // host copies (grid covariance launches)
+    DevBuf<float> tgt_quads;                   // GicpArgs::tgt_quads
+    DevBuf<int32_t> seg_qoff;
     DevBuf<double> tgt_cov_label, tgt_cov_all;
     int cov_k_label = 0, cov_k_all = 0;
     // GICP scratch
@@ -316,7 +318,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
     (void)dev_free(c->grids); (void)dev_free(c->cell_start); (void)dev_free(c->grid_pts);
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
-    (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt);
+    (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
     (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter);
     (void)dev_free(c->mtri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
@@ -571,6 +573,26 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
         HIPC(c, dev_upload(c->seg_cnt, scnt));
         c->seg_lo_h = slo;
         c->seg_cnt_h = scnt;
+        // quad-SoA copy of every segment (labels, then the whole cloud) for the scalar-cache scan
+        std::vector<int32_t> qoff(num_labels + 1);
+        std::vector<float> quads;
+        for (int L = 0; L <= num_labels; L++) {
+            qoff[L] = (int32_t)(quads.size() / 16);
+            const int n = scnt[L], nq = (n + 3) / 4;
+            const size_t q0 = quads.size();
+            quads.resize(q0 + (size_t)16 * nq, INFINITY);
+            for (int i = 0; i < n; i++) {
+                const float4 p = tp[slo[L] + i];
+                const bool fin = std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z);
+                float* Q = &quads[q0 + (size_t)16 * (i / 4)];
+                Q[i % 4] = fin ? p.x : INFINITY;
+                Q[4 + i % 4] = fin ? p.y : INFINITY;
+                Q[8 + i % 4] = fin ? p.z : INFINITY;
+            }
+        }
+        if (quads.empty()) quads.assign(16, INFINITY);
+        HIPC(c, dev_upload(c->tgt_quads, quads));
+        HIPC(c, dev_upload(c->seg_qoff, qoff));
         c->num_obs = num_obs;
         c->max_seg = mx;
         c->cov_k_label = 0;
@@ -794,6 +816,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.rot_eps = ip->rotation_epsilon;
     g.trans_eps = ip->transformation_epsilon;
     g.work_counter = c->icp_counter.p;
+    g.tgt_quads = c->tgt_quads.p;
+    g.seg_qoff = c->seg_qoff.p;
     g.grids = c->grids.p;
     g.cell_start = c->cell_start.p;
     g.grid_pts = c->grid_pts.p;

@@ -413,6 +413,56 @@ __device__ __forceinline__ void grid_nn(const LabelGrid& G, const int32_t* cell_
     }
 }
 
+// Nearest of a segment's targets read through the scalar cache: the segment is stored as quads of
+// 16 floats (x0..x3, y0..y3, z0..z3, 4 pad; non-finite and padding targets +inf), every lane scans the
+// same quads, so the loads are wave-uniform s_loads and the targets reach the VALU as SGPR operands --
+// no LDS traffic (an LDS broadcast read still moves 64 lanes x 16 B through the LDS pipe).  Same packed
+// arithmetic and tournament as quad_min, so the result is the oracle's first strict minimum.
+typedef __attribute__((address_space(4))) const f4v cf4v;
+
+__device__ __forceinline__ void quad_min_s(f4v X, f4v Y, f4v Z, int o, f2v qx2, f2v qy2, f2v qz2, float& m,
+                                           int& i) {
+    const f2v xa = X.xy, xb = X.zw, ya = Y.xy, yb = Y.zw, za = Z.xy, zb = Z.zw;
+    const f2v dxa = qx2 - xa, dya = qy2 - ya, dza = qz2 - za;
+    const f2v dxb = qx2 - xb, dyb = qy2 - yb, dzb = qz2 - zb;
+    const f2v da = dxa * dxa + dya * dya + dza * dza;
+    const f2v db = dxb * dxb + dyb * dyb + dzb * dzb;
+    const bool c01 = da.y < da.x, c23 = db.y < db.x;
+    const float m01 = c01 ? da.y : da.x, m23 = c23 ? db.y : db.x;
+    const int i01 = c01 ? 1 : 0, i23 = c23 ? 3 : 2;
+    const bool c = m23 < m01;
+    m = c ? m23 : m01;
+    i = o + (c ? i23 : i01);
+}
+
+__device__ __forceinline__ void scan_quads(const float* tq_generic, int nq, float qx, float qy, float qz, float& best,
+                                           int& j) {
+    const cf4v* tq = (const cf4v*)tq_generic;
+    const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+    float bA = INFINITY, bB = INFINITY;
+    int jA = -1, jB = -1;
+    int o = 0;
+#pragma unroll 2
+    for (; o + 2 <= nq; o += 2) {
+        float m;
+        int i;
+        const cf4v* q0 = tq + 4 * o;
+        quad_min_s(q0[0], q0[1], q0[2], 4 * o, qx2, qy2, qz2, m, i);
+        if (m < bA) { bA = m; jA = i; }
+        quad_min_s(q0[4], q0[5], q0[6], 4 * o + 4, qx2, qy2, qz2, m, i);
+        if (m < bB) { bB = m; jB = i; }
+    }
+    if (o < nq) {
+        float m;
+        int i;
+        const cf4v* q0 = tq + 4 * o;
+        quad_min_s(q0[0], q0[1], q0[2], 4 * o, qx2, qy2, qz2, m, i);
+        if (m < bA) { bA = m; jA = i; }
+    }
+    if (bB < bA || (bB == bA && jB >= 0 && jB < jA)) { bA = bB; jA = jB; }
+    if (bA < best) { best = bA; j = jA; }
+}
+
 __device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6]) {
     const double2* c2 = reinterpret_cast<const double2*>(cov + (size_t)6 * i);
     const double2 a = c2[0], b = c2[1], d = c2[2];
@@ -536,7 +586,6 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(P
 gicp_kernel(GicpArgs g, int num_poses) {
     constexpr int NT = 64 * WPP;
     __shared__ double RT[12];
-    __shared__ TgtTile T;
     __shared__ double sPart[WPP][28];
     __shared__ int sPose, sFlag;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -560,11 +609,10 @@ gicp_kernel(GicpArgs g, int num_poses) {
         const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
         const double* tcov = g.tgt_cov + (size_t)6 * lo;
         const float4* tgt = g.tgt + lo;
-        const bool resident = nt <= kTgtTile;  // the whole segment stays in LDS for all iterations
+        const float* tquads = g.tgt_quads + (seg >= 0 ? (size_t)16 * g.seg_qoff[seg] : 0);
         const bool use_grid = nt > kGridNNMin && g.grids != nullptr && seg >= 0;  // exact grid shell search
         LabelGrid G{};
         if (use_grid) G = g.grids[seg];
-        if (resident) stage_targets<NT>(T, tgt, min(nt, kTgtTile), tid);
         if (tid == 0) {
             for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
         }
@@ -608,21 +656,14 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 float best = INFINITY;
                 if (use_grid) {
                     if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qx, qy, qz, best, j);
-                } else
-                for (int t0 = 0; t0 < nt; t0 += kTgtTile) {
-                    const int tn = min(kTgtTile, nt - t0);
-                    if (!resident) {
-                        group_sync<WPP>();
-                        stage_targets<NT>(T, tgt + t0, tn, tid);
-                        group_sync<WPP>();
-                    }
-                    scan_targets(T, tn, t0, qx, qy, qz, best, j);
+                } else {
+                    scan_quads(tquads, (nt + 3) >> 2, qx, qy, qz, best, j);
                 }
                 if (p_ok) gicp_contrib(R, p_q, p_cs, p_tj, p_ct, acc);
                 p_ok = act && j >= 0;
                 if (p_ok) {
                     // a selected target is finite, so the staged copy equals the original
-                    p_tj = (resident && !use_grid) ? make_float4(T.x[j], T.y[j], T.z[j], 0.0f) : tgt[j];
+                    p_tj = tgt[j];
                     load_cov(tcov, j, p_ct);
 #pragma unroll
                     for (int k = 0; k < 3; k++) p_q[k] = q[k];

@@ -105,6 +105,10 @@ struct GicpArgs {
     const LabelGrid* grids;
     const int32_t* cell_start;
     const float4* grid_pts;
+    // the segments as quads of 16 floats (x0..3, y0..3, z0..3, pad; non-finite / padding = +inf), quad
+    // offset of segment s = seg_qoff[s]: the scalar-cache nearest-target scan
+    const float* tgt_quads;
+    const int32_t* seg_qoff;
 };
 
 // segments above this many points use the exact shell search of their neighbour grid (GICP

@@ -15,7 +15,14 @@ from perception_amd import _native, workloads  # noqa: E402
 
 
 def main():
-    w = workloads.build(poses_per_model=10000)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c3", action="store_true", help="the 5-object C3 scene instead of C2's single object")
+    ap.add_argument("--poses", type=int, default=10000, help="poses per model")
+    a = ap.parse_args()
+    names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can",
+             "024_bowl"] if a.c3 else ["003_cracker_box"]
+    w = workloads.build(names=names, poses_per_model=a.poses)
     lib = _native.load()
     fn = lib.pcore_debug_gicp_profile
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
