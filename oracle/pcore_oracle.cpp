@@ -6,6 +6,7 @@
 // The colour spec (deterministic sin / cos / atan2 / exp, CIEDE2000 term order) is shared with the GPU
 // build: it defines the arithmetic, like the GICP spec; tests/test_colour_spec.py pins it against numpy.
 #include "../perception_amd/csrc/pcore_colour.h"
+#include "../perception_amd/csrc/pcore_gicp_math.h"
 
 #include <climits>
 #include <cfloat>
@@ -521,46 +522,16 @@ bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const
         if (d < best) { best = d; j = o; }
     }
     if (j < 0) return false;
-    const double* ct = tcov + (size_t)6 * j;
-    const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
-    const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
-    double RC[3][3], A[3][3];
-    for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) RC[r][c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
-    for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) A[r][c] = Ct[r][c] + (RC[r][0] * R[c][0] + RC[r][1] * R[c][1] + RC[r][2] * R[c][2]);
-    double m[3][3];
-    m[0][0] = A[1][1] * A[2][2] - A[1][2] * A[2][1];
-    m[0][1] = A[0][2] * A[2][1] - A[0][1] * A[2][2];
-    m[0][2] = A[0][1] * A[1][2] - A[0][2] * A[1][1];
-    m[1][0] = A[1][2] * A[2][0] - A[1][0] * A[2][2];
-    m[1][1] = A[0][0] * A[2][2] - A[0][2] * A[2][0];
-    m[1][2] = A[0][2] * A[1][0] - A[0][0] * A[1][2];
-    m[2][0] = A[1][0] * A[2][1] - A[1][1] * A[2][0];
-    m[2][1] = A[0][1] * A[2][0] - A[0][0] * A[2][1];
-    m[2][2] = A[0][0] * A[1][1] - A[0][1] * A[1][0];
-    const double det = A[0][0] * m[0][0] + A[0][1] * m[1][0] + A[0][2] * m[2][0];
-    const double inv = 1.0 / det;
-    double M[3][3];
-    for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
-    const double* tp = nullptr;
-    (void)tp;
-    const double e[3] = {(double)tgt[3 * (size_t)j + 0] - q[0], (double)tgt[3 * (size_t)j + 1] - q[1],
-                         (double)tgt[3 * (size_t)j + 2] - q[2]};
-    const double J[3][6] = {{0.0, -q[2], q[1], -1.0, 0.0, 0.0},
-                            {q[2], 0.0, -q[0], 0.0, -1.0, 0.0},
-                            {-q[1], q[0], 0.0, 0.0, 0.0, -1.0}};
-    double MJ[3][6];
-    for (int r = 0; r < 3; r++)
-        for (int c = 0; c < 6; c++) MJ[r][c] = M[r][0] * J[0][c] + M[r][1] * J[1][c] + M[r][2] * J[2][c];
-    int h = 0;
-    for (int a = 0; a < 6; a++)
-        for (int b = a; b < 6; b++) acc[h++] += J[0][a] * MJ[0][b] + J[1][a] * MJ[1][b] + J[2][a] * MJ[2][b];
-    double Me[3];
-    for (int r = 0; r < 3; r++) Me[r] = M[r][0] * e[0] + M[r][1] * e[1] + M[r][2] * e[2];
-    for (int a = 0; a < 6; a++) acc[21 + a] += J[0][a] * Me[0] + J[1][a] * Me[1] + J[2][a] * Me[2];
-    acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+    const double* ctp = tcov + (size_t)6 * j;
+    const double ct[6] = {ctp[0], ctp[1], ctp[2], ctp[3], ctp[4], ctp[5]};
+    const double csa[6] = {cs[0], cs[1], cs[2], cs[3], cs[4], cs[5]};
+    const double Rm[3][3] = {{R[0][0], R[0][1], R[0][2]}, {R[1][0], R[1][1], R[1][2]}, {R[2][0], R[2][1], R[2][2]}};
+    const double qa[3] = {q[0], q[1], q[2]};
+    const double tj[3] = {(double)tgt[3 * (size_t)j + 0], (double)tgt[3 * (size_t)j + 1], (double)tgt[3 * (size_t)j + 2]};
+    double a28[28];
+    for (int v = 0; v < 28; v++) a28[v] = acc[v];
+    pcore::gicpm::contrib(Rm, qa, csa, tj, ct, a28);
+    for (int v = 0; v < 28; v++) acc[v] = a28[v];
     return true;
 }
 

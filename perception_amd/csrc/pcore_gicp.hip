@@ -15,6 +15,7 @@
 //                      J^T M e, wave shuffle-down tree, one-lane 6x6 LDLT and update, then
 //                      concatenate_transforms (renderer.cu:1412-1429).
 #include "pcore_internal.h"
+#include "pcore_gicp_math.h"
 
 #include <algorithm>
 #include <cfloat>
@@ -469,58 +470,20 @@ __device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6
     c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y; c[4] = d.x; c[5] = d.y;
 }
 
-// One point's Gauss-Newton contribution (orc gicp_contrib) given its transformed position q and its
-// correspondence tj / ct: acc[0..20] upper(H), [21..26] b, [27] error.
+// One point's Gauss-Newton contribution: the shared spec of pcore_gicp_math.h (the oracle calls the same
+// function), given the transformed point q, its correspondence tj and both covariances.
 __device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6],
                                              float4 tj, const double (&ct)[6], double (&acc)[28]) {
-    const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
-    const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
-    double RC[3][3], A[3][3];
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++) RC[r][c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++) A[r][c] = Ct[r][c] + (RC[r][0] * R[c][0] + RC[r][1] * R[c][1] + RC[r][2] * R[c][2]);
-    double m[3][3];
-    m[0][0] = A[1][1] * A[2][2] - A[1][2] * A[2][1];
-    m[0][1] = A[0][2] * A[2][1] - A[0][1] * A[2][2];
-    m[0][2] = A[0][1] * A[1][2] - A[0][2] * A[1][1];
-    m[1][0] = A[1][2] * A[2][0] - A[1][0] * A[2][2];
-    m[1][1] = A[0][0] * A[2][2] - A[0][2] * A[2][0];
-    m[1][2] = A[0][2] * A[1][0] - A[0][0] * A[1][2];
-    m[2][0] = A[1][0] * A[2][1] - A[1][1] * A[2][0];
-    m[2][1] = A[0][1] * A[2][0] - A[0][0] * A[2][1];
-    m[2][2] = A[0][0] * A[1][1] - A[0][1] * A[1][0];
-    const double det = A[0][0] * m[0][0] + A[0][1] * m[1][0] + A[0][2] * m[2][0];
-    const double inv = 1.0 / det;
-    double M[3][3];
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
-    const double e[3] = {(double)tj.x - q[0], (double)tj.y - q[1], (double)tj.z - q[2]};
-    const double J[3][6] = {{0.0, -q[2], q[1], -1.0, 0.0, 0.0},
-                            {q[2], 0.0, -q[0], 0.0, -1.0, 0.0},
-                            {-q[1], q[0], 0.0, 0.0, 0.0, -1.0}};
-    double MJ[3][6];
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int c = 0; c < 6; c++) MJ[r][c] = M[r][0] * J[0][c] + M[r][1] * J[1][c] + M[r][2] * J[2][c];
-    int h = 0;
-#pragma unroll
-    for (int a = 0; a < 6; a++)
-#pragma unroll
-        for (int b = a; b < 6; b++) { acc[h] += J[0][a] * MJ[0][b] + J[1][a] * MJ[1][b] + J[2][a] * MJ[2][b]; h++; }
-    double Me[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) Me[r] = M[r][0] * e[0] + M[r][1] * e[1] + M[r][2] * e[2];
-#pragma unroll
-    for (int a = 0; a < 6; a++) acc[21 + a] += J[0][a] * Me[0] + J[1][a] * Me[1] + J[2][a] * Me[2];
-    acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+    const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
+    gicpm::contrib(R, q, cs, t3, ct, acc);
+}
+
+// a wave-uniform double moved to SGPRs (R, t of the pose being refined)
+__device__ __forceinline__ double uniform_d(double x) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
 // 6x6 LDLT without pivoting (orc ldlt_solve6).  Single lane.
@@ -574,7 +537,7 @@ __device__ __forceinline__ void group_sync() {
 // The per-pose iteration chain is latency-bound, so the slowest pose sets a chunk's tail; WPP > 1
 // splits each iteration's scan over more lanes.
 #ifndef PCORE_GICP_WAVES_PER_EU
-#define PCORE_GICP_WAVES_PER_EU 2
+#define PCORE_GICP_WAVES_PER_EU 3
 #endif
 #ifndef PCORE_GICP_WPP
 #define PCORE_GICP_WPP 1
@@ -625,27 +588,17 @@ gicp_kernel(GicpArgs g, int num_poses) {
 #pragma unroll
             for (int r = 0; r < 3; r++) {
 #pragma unroll
-                for (int c = 0; c < 3; c++) R[r][c] = RT[3 * r + c];
-                t[r] = RT[9 + r];
+                for (int c = 0; c < 3; c++) R[r][c] = uniform_d(RT[3 * r + c]);
+                t[r] = uniform_d(RT[9 + r]);
             }
             double acc[28];
 #pragma unroll
             for (int v = 0; v < 28; v++) acc[v] = 0.0;
-            // rounds of NT source points, software-pipelined: round r's nearest-target scan runs while
-            // round r-1's target covariance (a gather) and round r+1's source point are in flight, then
-            // round r-1's contribution is added; per lane the contributions keep their point order
-            float4 sp_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (tid < ns) sp_n = src[tid];
-            bool p_ok = false;  // previous round's pending contribution
-            double p_q[3] = {0.0, 0.0, 0.0}, p_cs[6], p_ct[6];
-            float4 p_tj = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            // rounds of NT source points: point i -> thread i % NT, contributions added in point order
             for (int i0 = 0; i0 < ns; i0 += NT) {
                 const int i = i0 + tid;
                 const bool act = i < ns;
-                const float4 sp = sp_n;
-                double cs[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // consumed after the next round's scan
-                if (act) load_cov(scov, i, cs);
-                if (i + NT < ns) sp_n = src[i + NT];
+                const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
                 double q[3];
 #pragma unroll
@@ -659,19 +612,13 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 } else {
                     scan_quads(tquads, (nt + 3) >> 2, qx, qy, qz, best, j);
                 }
-                if (p_ok) gicp_contrib(R, p_q, p_cs, p_tj, p_ct, acc);
-                p_ok = act && j >= 0;
-                if (p_ok) {
-                    // a selected target is finite, so the staged copy equals the original
-                    p_tj = tgt[j];
-                    load_cov(tcov, j, p_ct);
-#pragma unroll
-                    for (int k = 0; k < 3; k++) p_q[k] = q[k];
-#pragma unroll
-                    for (int k = 0; k < 6; k++) p_cs[k] = cs[k];
+                if (act && j >= 0) {
+                    double cs[6], ct[6];
+                    load_cov(scov, i, cs);
+                    load_cov(tcov, j, ct);
+                    gicp_contrib(R, q, cs, tgt[j], ct, acc);
                 }
             }
-            if (p_ok) gicp_contrib(R, p_q, p_cs, p_tj, p_ct, acc);
             GPROF_T(t_b);
 #pragma unroll
             for (int v = 0; v < 28; v++) {

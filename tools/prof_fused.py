@@ -17,8 +17,11 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--poses", type=int, default=10000)
     ap.add_argument("--icp", action="store_true")
+    ap.add_argument("--c3", action="store_true", help="the 5-object C3 scene")
     a = ap.parse_args()
-    w = workloads.build(poses_per_model=a.poses)
+    names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can",
+             "024_bowl"] if a.c3 else ["003_cracker_box"]
+    w = workloads.build(names=names, poses_per_model=a.poses)
     n = int(w.poses.shape[0])
     for _ in range(a.iters):
         if a.icp:
