@@ -264,10 +264,19 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
 
+// Meshlet header through the scalar cache (the index is wave-uniform; a constant-address-space load is an
+// s_load, which the compiler cannot prove safe for a plain global pointer in a kernel that also stores)
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const i4v ci4v;
+__device__ __forceinline__ Meshlet load_meshlet(const Meshlet* p, int m) {
+    const i4v v = ((const ci4v*)p)[m];
+    return Meshlet{v.x, v.y, v.z, v.w};
+}
+
 template <int STRIDE, bool IDPASS = false>
 __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, int32_t* cid = nullptr) {
     const int tid = threadIdx.x;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of meshlet headers
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int W = a.width, H = a.height, ws = a.ws;
@@ -318,7 +327,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t pk0 = 0, pk1 = 0, id0 = 0, id1 = 0;
     if (m < ml_hi) {
-        ml = a.meshlets[m];
+        ml = load_meshlet(a.meshlets, m);
         if (lane < ml.nv) v = a.mverts[ml.vbase + lane];
         if (lane < ml.nt) pk0 = a.mtris[ml.tbase + lane];
         if (kWave + lane < ml.nt) pk1 = a.mtris[ml.tbase + kWave + lane];
@@ -334,7 +343,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         float4 vn = make_float4(0.f, 0.f, 0.f, 0.f);
         uint32_t pn0 = 0, pn1 = 0, in0 = 0, in1 = 0;
         if (mn < ml_hi) {
-            mln = a.meshlets[mn];
+            mln = load_meshlet(a.meshlets, mn);
             if (lane < mln.nv) vn = a.mverts[mln.vbase + lane];
             if (lane < mln.nt) pn0 = a.mtris[mln.tbase + lane];
             if (kWave + lane < mln.nt) pn1 = a.mtris[mln.tbase + kWave + lane];
@@ -404,15 +413,22 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             while (big) {
                 const int j = __ffsll((unsigned long long)big) - 1;
                 big &= big - 1;
+                // j is wave-uniform: v_readlane into SGPRs (no LDS round trip)
+                auto rl = [&](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j)); };
                 TriRec rb;
-                rb.a0 = __shfl(r.a0, j); rb.a1 = __shfl(r.a1, j);
-                rb.b0 = __shfl(r.b0, j); rb.b1 = __shfl(r.b1, j);
-                rb.c0 = __shfl(r.c0, j); rb.c1 = __shfl(r.c1, j);
-                rb.z0 = __shfl(r.z0, j); rb.z1 = __shfl(r.z1, j); rb.z2 = __shfl(r.z2, j);
-                const int bkx0 = __shfl(kx0, j), bky0 = __shfl(ky0, j), bnx = __shfl(nx, j), bnk = __shfl(nk, j);
-                const uint32_t bid = IDPASS ? (uint32_t)__shfl((int)oid, j) : 0u;
+                rb.a0 = rl(r.a0); rb.a1 = rl(r.a1);
+                rb.b0 = rl(r.b0); rb.b1 = rl(r.b1);
+                rb.c0 = rl(r.c0); rb.c1 = rl(r.c1);
+                rb.z0 = rl(r.z0); rb.z1 = rl(r.z1); rb.z2 = rl(r.z2);
+                const int bkx0 = __builtin_amdgcn_readlane(kx0, j), bky0 = __builtin_amdgcn_readlane(ky0, j);
+                const int bnx = __builtin_amdgcn_readlane(nx, j), bnk = __builtin_amdgcn_readlane(nk, j);
+                const uint32_t bid = IDPASS ? (uint32_t)__builtin_amdgcn_readlane((int)oid, j) : 0u;
+                // q / bnx without an integer division: the float quotient is within 1e-3 of q / bnx (q / bnx
+                // is at most the sample rows), so one correction step gives the exact row
+                const float inv_nx = 1.0f / (float)bnx;
                 for (int q = lane; q < bnk; q += kWave) {
-                    const int iy = q / bnx, ix = q - iy * bnx;
+                    int iy = (int)(((float)q + 0.5f) * inv_nx), ix = q - iy * bnx;
+                    if (ix < 0) { iy--; ix += bnx; } else if (ix >= bnx) { iy++; ix -= bnx; }
                     raster_sample<IDPASS>(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf, cid, bid);
                 }
             }
@@ -446,7 +462,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int pose = blockIdx.x;
     const int tid = threadIdx.x;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of meshlet headers
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int ws = a.ws, hs = a.hs;
