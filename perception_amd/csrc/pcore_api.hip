@@ -191,7 +191,7 @@ void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std:
             }
         };
         add_tri(next_seed);
-        while ((int)mt.size() < kMeshletMaxTris) {
+        while ((int)mt.size() < kMeshletBuildTris) {
             int best = -1, best_score = -1;
             for (size_t i = 0; i < mv.size(); i++)
                 for (int t : adj[mv[i]]) {

@@ -11,6 +11,10 @@ namespace pcore {
 // packed local indices i0 | i1 << 8 | i2 << 16.
 constexpr int kMeshletMaxVerts = 64;
 constexpr int kMeshletMaxTris = 128;
+// The builder stops at 64 triangles: one vertex pass + one 64-lane triangle batch per meshlet.  With 128,
+// meshlets of 65..95 triangles cost a second, mostly empty batch (the 003_cracker_box proxy: 191 meshlets
+// and 264 batches vs 197 and 197).
+constexpr int kMeshletBuildTris = 64;
 struct Meshlet {
     int32_t vbase;  // first vertex in mverts
     int32_t tbase;  // first triangle in mtris
