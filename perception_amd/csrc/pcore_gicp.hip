@@ -18,6 +18,7 @@
 #include "pcore_gicp_math.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cfloat>
 #include <climits>
 
@@ -522,6 +523,54 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
     return true;
 }
 
+// Lane-0 step of an iteration: LDLT of the reduced normal equations, the left update of (R, t) into RT and
+// fast_gicp's convergence test.  Returns 0 continue, 1 stop without update (H not positive definite),
+// 2 stop after the update.
+__device__ __forceinline__ int solve_update(const double (&acc)[28], const double (&R)[3][3], const double (&t)[3],
+                                        double* RT, double rot_eps, double trans_eps) {
+    double d[6];
+    if (!ldlt_solve6(acc, acc + 21, d)) return 1;
+    double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
+    const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+    const double inv = 1.0 / nrm;
+    qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
+    const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
+    const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
+    const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
+                             {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
+                             {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
+    double dr = 0.0, dt = 0.0;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) {
+            RT[3 * r + c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
+            const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
+            dr = v > dr ? v : dr;
+        }
+        RT[9 + r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
+        const double v = fabs(d[3 + r]);
+        dt = v > dt ? v : dt;
+    }
+    return (dr < rot_eps && dt < trans_eps) ? 2 : 0;
+}
+
+// concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
+__device__ __forceinline__ void write_pose(const GicpArgs& g, int gp, const double* RT, int iters) {
+    const float* pin = g.poses_in + (size_t)16 * gp;
+    float A[4][4], Tf[4][4];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
+            Tf[r][c] = r < 3 ? (float)(c < 3 ? RT[3 * r + c] : RT[9 + r]) : (c == 3 ? 1.0f : 0.0f);
+        }
+    float* pout = g.poses_out + (size_t)16 * gp;
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            const float p = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
+            pout[4 * r + c] = r < 3 ? (float)((double)p * 100) : p;
+        }
+    if (g.iters_out) g.iters_out[gp] = iters;
+}
+
 // Synchronise the WPP waves that share one pose: LDS writes of any lane visible to all of them.
 template <int WPP>
 __device__ __forceinline__ void group_sync() {
@@ -643,36 +692,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 }
             }
             GPROF_T(t_c);
-            if (tid == 0) {
-                int flag = 0;  // 0 continue, 1 stop (no update), 2 stop after update
-                double d[6];
-                if (!ldlt_solve6(acc, acc + 21, d)) {
-                    flag = 1;
-                } else {
-                    double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
-                    const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
-                    const double inv = 1.0 / nrm;
-                    qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
-                    const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
-                    const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
-                    const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
-                                             {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
-                                             {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
-                    double dr = 0.0, dt = 0.0;
-                    for (int r = 0; r < 3; r++) {
-                        for (int c = 0; c < 3; c++) {
-                            RT[3 * r + c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
-                            const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
-                            dr = v > dr ? v : dr;
-                        }
-                        RT[9 + r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
-                        const double v = fabs(d[3 + r]);
-                        dt = v > dt ? v : dt;
-                    }
-                    flag = (dr < g.rot_eps && dt < g.trans_eps) ? 2 : 0;
-                }
-                sFlag = flag;
-            }
+            if (tid == 0) sFlag = solve_update(acc, R, t, RT, g.rot_eps, g.trans_eps);
             group_sync<WPP>();
             const int flag = __builtin_amdgcn_readfirstlane(sFlag);
             GPROF_T(t_d);
@@ -683,25 +703,121 @@ gicp_kernel(GicpArgs g, int num_poses) {
             done = flag != 0;
         }
         group_sync<WPP>();
-        if (tid == 0) {
-            // concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
-            const float* pin = g.poses_in + (size_t)16 * gp;
-            float A[4][4], Tf[4][4];
-            for (int r = 0; r < 4; r++)
-                for (int c = 0; c < 4; c++) {
-                    A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
-                    Tf[r][c] = r < 3 ? (float)(c < 3 ? RT[3 * r + c] : RT[9 + r]) : (c == 3 ? 1.0f : 0.0f);
-                }
-            float* pout = g.poses_out + (size_t)16 * gp;
-            for (int r = 0; r < 4; r++)
-                for (int c = 0; c < 4; c++) {
-                    const float p = Tf[r][0] * A[0][c] + Tf[r][1] * A[1][c] + Tf[r][2] * A[2][c] + Tf[r][3] * A[3][c];
-                    pout[4 * r + c] = r < 3 ? (float)((double)p * 100) : p;
-                }
-            if (g.iters_out) g.iters_out[gp] = iters;
-        }
+        if (tid == 0) write_pose(g, gp, RT, iters);
     }
 }
+
+
+// Small batches (C1: 128 poses fill 128 of 1024 SIMDs) with large target segments: WPP waves per pose.
+// All waves search the correspondences of the iteration's source points (round r -> wave r % WPP), the
+// indices go to LDS, and wave 0 then adds the contributions exactly as gicp_kernel<1> does -- point i on
+// lane i % 64, in point order -- so the refined poses are bit-identical; only the nearest-target
+// searches, the expensive part against a whole-scene target, run in parallel.
+template <int WPP>
+__global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num_poses) {
+    constexpr int NT = 64 * WPP;
+    extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
+    __shared__ double RT[12];
+    __shared__ int sPose, sFlag;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) sPose = atomicAdd(g.work_counter, 1);
+        __syncthreads();
+        const int pose = __builtin_amdgcn_readfirstlane(sPose);
+        if (pose >= num_poses) break;
+        const int gp = g.pose_base + pose;
+        const int ns = g.src_count[pose];
+        const float4* src = g.src + (size_t)pose * g.src_cap;
+        const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
+        int seg = g.whole_seg;
+        if (g.pose_label) {
+            const int pl = g.pose_label[gp];
+            seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
+        }
+        seg = __builtin_amdgcn_readfirstlane(seg);
+        const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
+        const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
+        const double* tcov = g.tgt_cov + (size_t)6 * lo;
+        const float4* tgt = g.tgt + lo;
+        const float* tquads = g.tgt_quads + (seg >= 0 ? (size_t)16 * g.seg_qoff[seg] : 0);
+        const bool use_grid = nt > kGridNNMin && g.grids != nullptr && seg >= 0;
+        LabelGrid G{};
+        if (use_grid) G = g.grids[seg];
+        if (tid == 0) {
+            for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
+        }
+        int iters = 0;
+        bool done = ns <= 0 || nt <= 0;
+        for (int it = 0; it < g.max_iter && !done; it++) {
+            __syncthreads();
+            double R[3][3], t[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) R[r][c] = uniform_d(RT[3 * r + c]);
+                t[r] = uniform_d(RT[9 + r]);
+            }
+            // correspondences, all waves
+            for (int i0 = wave * 64; i0 < ns; i0 += NT) {
+                const int i = i0 + lane;
+                const bool act = i < ns;
+                const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+                double q[3];
+#pragma unroll
+                for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
+                const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
+                int j = -1;
+                float best = INFINITY;
+                if (use_grid) {
+                    if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qx, qy, qz, best, j);
+                } else {
+                    scan_quads(tquads, (nt + 3) >> 2, qx, qy, qz, best, j);
+                }
+                if (act) jbuf[i] = j;
+            }
+            __syncthreads();
+            if (wave == 0) {
+                double acc[28];
+#pragma unroll
+                for (int v = 0; v < 28; v++) acc[v] = 0.0;
+                for (int i0 = 0; i0 < ns; i0 += 64) {
+                    const int i = i0 + lane;
+                    const int j = i < ns ? jbuf[i] : -1;
+                    if (j >= 0) {
+                        const float4 sp = src[i];
+                        const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+                        double q[3];
+#pragma unroll
+                        for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
+                        double cs[6], ct[6];
+                        load_cov(scov, i, cs);
+                        load_cov(tcov, j, ct);
+                        gicp_contrib(R, q, cs, tgt[j], ct, acc);
+                    }
+                }
+#pragma unroll
+                for (int v = 0; v < 28; v++) {
+                    double x = acc[v];
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
+                    acc[v] = x;
+                }
+                if (tid == 0) sFlag = solve_update(acc, R, t, RT, g.rot_eps, g.trans_eps);
+            }
+            __syncthreads();
+            const int flag = __builtin_amdgcn_readfirstlane(sFlag);
+            if (flag != 1) iters++;
+            done = flag != 0;
+        }
+        __syncthreads();
+        if (tid == 0) write_pose(g, gp, RT, iters);
+    }
+}
+
+constexpr int kGicpWideWpp = 8;
+constexpr size_t kGicpWideMaxLds = 96 * 1024;  // correspondence buffer: src_cap <= 24576
 
 #ifdef PCORE_GICP_PROFILE
 extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
@@ -717,6 +833,7 @@ extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;
     static int resident_wgs = 0;  // workgroups the whole device holds at once (occupancy x CUs)
+    static int num_cus = 0;
     if (resident_wgs == 0) {
         int dev = 0, per_cu = 0;
         hipDeviceProp_t prop;
@@ -726,10 +843,24 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gicp_kernel<kGicpWpp>, 64 * kGicpWpp, 0);
         if (e != hipSuccess) return e;
         resident_wgs = std::max(1, per_cu) * prop.multiProcessorCount;
+        num_cus = prop.multiProcessorCount;
     }
-    const int wgs = std::min(resident_wgs, num_poses);
     hipError_t e = hipMemsetAsync(g.work_counter, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
+    // a batch too small to give every SIMD a pose: spread each pose's searches over kGicpWideWpp waves
+    const size_t wide_lds = (size_t)g.src_cap * sizeof(int32_t);
+    bool wide = num_poses <= num_cus * 2 && wide_lds <= kGicpWideMaxLds;
+    if (const char* e = getenv("PCORE_GICP_KERNEL")) {  // tests pin either kernel (same results)
+        if (e[0] == 'n') wide = false;
+        else if (e[0] == 'w' && wide_lds <= kGicpWideMaxLds) wide = true;
+    }
+    if (wide) {
+        const int wgs = std::min(num_poses, num_cus * 2);
+        hipLaunchKernelGGL(gicp_wide_kernel<kGicpWideWpp>, dim3(wgs), dim3(64 * kGicpWideWpp), wide_lds, s, g,
+                           num_poses);
+        return hipGetLastError();
+    }
+    const int wgs = std::min(resident_wgs, num_poses);
     hipLaunchKernelGGL(gicp_kernel<kGicpWpp>, dim3(wgs), dim3(64 * kGicpWpp), 0, s, g, num_poses);
     return hipGetLastError();
 }

@@ -252,11 +252,15 @@ def _label_covs(case, six=True):
     return cov
 
 
+@pytest.mark.parametrize("kernel", ["narrow", "wide"])
 @pytest.mark.parametrize("fixture", ["one_object", "three_objects"])
-def test_evaluate_icp_matches_oracle(fixture, request):
+def test_evaluate_icp_matches_oracle(fixture, kernel, request, monkeypatch):
+    """Both GICP kernels -- one wave per pose (large batches) and eight waves per pose (small batches) --
+    against the oracle; PCORE_GICP_KERNEL pins the choice launch_gicp otherwise makes by batch size."""
     case, core, t = request.getfixturevalue(fixture)
     sc = case.scene
     n = min(48, len(case.poses))
+    monkeypatch.setenv("PCORE_GICP_KERNEL", kernel)
     adj, iters, rc, oc, df = core.evaluate_icp(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n],
                                                cost_type=2, stride=case.stride)
     oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
@@ -352,7 +356,8 @@ def test_observed_cloud_bounded_matches_oracle(one_object):
     assert torch.equal(xyz, ref)
 
 
-def test_evaluate_icp_3dof_whole_scene_targets_matches_oracle():
+@pytest.mark.parametrize("kernel", ["narrow", "wide"])
+def test_evaluate_icp_3dof_whole_scene_targets_matches_oracle(kernel, monkeypatch):
     """C1's table-top scene with the WHOLE observed cloud as the GICP target (~19k points at stride 4, no
     labels): correspondences and target covariances take the exact grid shell search; the result must equal
     the oracle's brute-force scans bit for bit."""
@@ -369,6 +374,7 @@ def test_evaluate_icp_3dof_whole_scene_targets_matches_oracle():
     core.set_observation(torch.from_numpy(c1.src_depth_cm).to(dev), None, xyz, None, 0.0075)
     idx = np.array([c1.gt_index, 3, 70], np.int64)
     n = len(idx)
+    monkeypatch.setenv("PCORE_GICP_KERNEL", kernel)
     poses = c1.poses[idx]
     tot = np.full(n, xyz.shape[0], np.float32)
     adj, iters, rc, oc, df = core.evaluate_icp(torch.from_numpy(poses).to(dev), torch.zeros(n, dtype=torch.int32,
