@@ -118,12 +118,14 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
 // Exact neighbour search over a segment's grid (segments above kGridNNMin points)
 // ------------------------------------------------------------------------------------------------
 //
-// Cells are visited in shells of growing Chebyshev radius r around the query's cell.  A point in an
-// unvisited cell has |floor(fp) - floor(fq)| >= r + 1 on some axis, hence |fp - fq| > r in the grid's
-// float cell coordinates, hence a true axis distance above (r - eps) * cell and a float squared distance
-// above B^2 (1 - 3e-7) with B = (r - 0.01 - 1e-6 |fq|) * cell.  Once the caller's limit (the best
-// distance, or the k-th best once k are held) is below 0.99999 B^2, no unvisited point can reach or tie
-// it, so the result equals the brute-force scan's lexicographic minimum of (float distance, index).
+// Cells are visited in shells of growing Chebyshev radius r around the query's cell.  A point binned in
+// cell i has its float cell coordinate fp in [i, i + 1) (the grid spans the points' own bounds, so no
+// clamping), so along each axis |fp - fq| is at least the gap between fq and that interval, and the true
+// distance at least (gap - eps) * cell; a cell whose bound exceeds the caller's limit (the best distance,
+// or the k-th best once k are held) is skipped without loading it, and the search stops once the limit is
+// below the bound of the nearest face of the visited box that still has cells beyond it.  Every skipped
+// point is strictly farther than the limit, so the result equals the brute-force scan's lexicographic
+// minimum of (float distance, index).
 // Returns false when the cell budget runs out first (or the query is far outside the grid): the caller
 // then scans the whole segment.  Non-finite queries are the caller's business.
 constexpr int kShellBudget = 343;  // cells, r <= 3 around an in-grid query
@@ -135,6 +137,20 @@ __device__ __forceinline__ bool grid_shells(const LabelGrid& g, const int32_t* c
     const float fm = fmaxf(fabsf(fx), fmaxf(fabsf(fy), fabsf(fz)));
     if (!(fm < 65536.0f)) return false;
     const int cx = (int)floorf(fx), cy = (int)floorf(fy), cz = (int)floorf(fz);
+    const float e = 0.01f + 1e-6f * fm;  // cell-unit slack for the rounding of fp, fq and inv_c
+    const float c2 = g.cell * g.cell * 0.99999f;
+    // lower bound of the float squared distance from q to any point binned in cell (ix, iy, iz): a point's
+    // cell coordinate fp lies in [i, i + 1), so |fp - fq| >= gap along each axis
+    auto cell_lb = [&](int ix, int iy, int iz) {
+        const float gx = fmaxf(fmaxf((float)ix - fx, fx - (float)(ix + 1)) - e, 0.0f);
+        const float gy = fmaxf(fmaxf((float)iy - fy, fy - (float)(iy + 1)) - e, 0.0f);
+        const float gz = fmaxf(fmaxf((float)iz - fz, fz - (float)(iz + 1)) - e, 0.0f);
+        return (gx * gx + gy * gy + gz * gz) * c2;
+    };
+    auto try_cell = [&](int row, int ix, int iy, int iz) {
+        if (cell_lb(ix, iy, iz) > limit()) return;  // every point of the cell is strictly farther
+        visit(cell_start[row + ix], cell_start[row + ix + 1]);
+    };
     int visited = 0;
     for (int r = 0;; r++) {
         const int z0 = max(0, cz - r), z1 = min(g.nz - 1, cz + r);
@@ -145,24 +161,31 @@ __device__ __forceinline__ bool grid_shells(const LabelGrid& g, const int32_t* c
                 const int row = g.cell_base + (iz * g.ny + iy) * g.nx;
                 const bool face = iz == cz - r || iz == cz + r || iy == cy - r || iy == cy + r;
                 if (face) {
-                    for (int ix = x0; ix <= x1; ix++) visit(cell_start[row + ix], cell_start[row + ix + 1]);
+                    for (int ix = x0; ix <= x1; ix++) try_cell(row, ix, iy, iz);
                     visited += x1 >= x0 ? x1 - x0 + 1 : 0;
                 } else {
                     if (cx - r >= 0 && cx - r < g.nx) {
-                        visit(cell_start[row + cx - r], cell_start[row + cx - r + 1]);
+                        try_cell(row, cx - r, iy, iz);
                         visited++;
                     }
                     if (r > 0 && cx + r >= 0 && cx + r < g.nx) {
-                        visit(cell_start[row + cx + r], cell_start[row + cx + r + 1]);
+                        try_cell(row, cx + r, iy, iz);
                         visited++;
                     }
                 }
             }
-        if (cx - r <= 0 && cx + r >= g.nx - 1 && cy - r <= 0 && cy + r >= g.ny - 1 && cz - r <= 0 &&
-            cz + r >= g.nz - 1)
-            return true;  // every cell visited
-        const float B = ((float)r - 0.01f - 1e-6f * fm) * g.cell;
-        if (B > 0.0f && limit() < B * B * 0.99999f) return true;
+        // unvisited cells lie beyond the faces of the box [c - r, c + r + 1) that are inside the grid; the
+        // distance from fq to the nearest such face bounds every unvisited point
+        float B = INFINITY;
+        if (cx - r > 0) B = fminf(B, fx - (float)(cx - r));
+        if (cx + r < g.nx - 1) B = fminf(B, (float)(cx + r + 1) - fx);
+        if (cy - r > 0) B = fminf(B, fy - (float)(cy - r));
+        if (cy + r < g.ny - 1) B = fminf(B, (float)(cy + r + 1) - fy);
+        if (cz - r > 0) B = fminf(B, fz - (float)(cz - r));
+        if (cz + r < g.nz - 1) B = fminf(B, (float)(cz + r + 1) - fz);
+        if (B == INFINITY) return true;  // every cell visited
+        B -= e;
+        if (B > 0.0f && limit() < B * B * c2) return true;
         if (visited >= kShellBudget) return false;
     }
 }
