@@ -178,6 +178,21 @@ def main():
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    # the secondary (binding) roof of an on-chip design, SURVEY.md 7 "roofline honesty": VALU issue rate of
+    # the same kernel from the SQ counters of tools/sq_counters.sh (a separate counters-only pass)
+    valu = None
+    sq_path = os.path.join(ROOT, "profiles", "r01_sq_counters.json")
+    if os.path.exists(sq_path):
+        try:
+            with open(sq_path) as f:
+                sq = json.load(f)
+            if sq.get("fused_cost_poses_per_launch") == n:
+                fc = sq["fused_cost"]
+                valu = {"issue_frac": fc["derived_valu_issue_frac_at_2cyc"],
+                        "instr_per_pose": fc["derived_valu_instr_per_pose"],
+                        "source": "profiles/r01_sq_counters.json: 2 * SQ_INSTS_VALU / (1024 SIMDs * GRBM_GUI_ACTIVE/8)"}
+        except (OSError, ValueError, KeyError):
+            valu = None
     line = {
         "metric": "candidate poses rendered+scored/sec @640x480",
         "value": value,
@@ -197,7 +212,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_BPS, "traffic": traffic,
                      "kernel": "fused_cost_kernel", "kernel_ms": kern_ms,
-                     "bytes_per_pose": bpp, "p_r_mean": p_r_mean},
+                     "bytes_per_pose": bpp, "p_r_mean": p_r_mean, "valu": valu},
         "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},
     }
     if world == 1 and not args.no_cpu:
