@@ -98,3 +98,19 @@ def test_localize_objects_greedy_render_matches_oracle_pipeline(tmp_path, icp):
     rec.write_outputs(res, str(tmp_path / "out"))
     back = io.read_output_poses(str(tmp_path / "out" / "output_poses.txt"))
     assert [b.name for b in back] == names
+    # ADD-S AUC (north star: within 0.1 of the reference): the GPU pipeline's selected poses, scored with the
+    # GPU ADD-S kernel, against the oracle pipeline's selected poses scored with the f64 CPU ADD-S
+    from perception_amd import metrics
+    from perception_amd.model import to_eigen
+    g_err, o_err = [], []
+    for k, i in enumerate(bi):
+        pts = np.unique(sc.bank.models[k].tris.reshape(-1, 3), axis=0)
+        est_gpu = np.asarray(res.object_transforms[k], np.float64)
+        est_orc = to_eigen(np.asarray(adj[i], np.float32)).astype(np.float64)
+        _, s_gpu = metrics.pose_distances(rec.core, pts, gts[k][None], est_gpu[None])
+        _, s_orc = oracle.pose_distances(pts, gts[k][None], est_orc[None])
+        g_err.append(float(s_gpu[0].item()))
+        o_err.append(float(s_orc[0]))
+    auc_gpu = metrics.compute_pose_metrics(np.array(g_err))["auc"]
+    auc_orc = metrics.compute_pose_metrics(np.array(o_err))["auc"]
+    assert abs(auc_gpu - auc_orc) <= 0.1, (auc_gpu, auc_orc)
