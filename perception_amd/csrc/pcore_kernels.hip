@@ -556,13 +556,16 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
         wave_sync();
     };
 
+    int wave_pts = 0;  // wave-uniform
     for (int base = wave * kWave; base < nsamp; base += kThreads) {
         const int k = base + lane;
         bool valid = false;
         if (k < nsamp && !(a.dbg_skip & 4)) {
             const int32_t z = sm.zbuf[k];
-            const int32_t zf = occlusion_rule(z, a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg, pl,
-                                              a.occlusion_threshold);
+            // no fragment: Z = 0 whatever the source (the sampled source is read only under a fragment)
+            const int32_t zf = z == INT_MAX ? 0
+                                            : occlusion_rule(z, a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg,
+                                                             pl, a.occlusion_threshold);
             if (zf != z) sm.zbuf[k] = zf;
             if (a.dbg_zs) a.dbg_zs[(size_t)pose * nsamp + k] = zf;
             valid = zf > 0;  // depth_to_mask, compute_point_clouds.cuh:64
@@ -570,6 +573,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
         const uint64_t bv = __ballot(valid);
         if (valid) queue[qcount + mbcnt64(bv)] = k;
         qcount += __popcll(bv);
+        wave_pts += __popcll(bv);
         if (qcount >= kWave) {
             process_points(qcount);
             qcount = 0;
@@ -581,17 +585,13 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     for (int off = 32; off > 0; off >>= 1) wave_bad += __shfl_xor(wave_bad, off);
     __syncthreads();  // all points counted / marked
     if (lane == 0) atomicAdd(&sm.counters[0], wave_bad);
-    // number of points = number of valid samples, counted again cheaply from the final z-buffer
-    int my_pts = 0, my_expl = 0;
-    for (int k = tid; k < nsamp; k += kThreads) my_pts += sm.zbuf[k] > 0 ? 1 : 0;
+    // number of points = number of valid samples (counted per wave above)
+    int my_expl = 0;
     for (int w = tid; w < a.bitmap_words; w += kThreads) my_expl += __popc(sm.bitmap[w]);
-    for (int off = 32; off > 0; off >>= 1) {
-        my_pts += __shfl_xor(my_pts, off);
-        my_expl += __shfl_xor(my_expl, off);
-    }
+    for (int off = 32; off > 0; off >>= 1) my_expl += __shfl_xor(my_expl, off);
     if (lane == 0) {
         atomicAdd(&sm.counters[1], my_expl);
-        atomicAdd(&sm.counters[2], my_pts);
+        atomicAdd(&sm.counters[2], wave_pts);
     }
     __syncthreads();
 
