@@ -520,19 +520,35 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
                         const int ix0 = (int)floorf(fmaxf(lx, 0.0f)), ix1 = min(g.nx - 1, (int)floorf(hx));
                         const int iy0 = (int)floorf(fmaxf(ly, 0.0f)), iy1 = min(g.ny - 1, (int)floorf(hy));
                         const int iz0 = (int)floorf(fmaxf(lz, 0.0f)), iz1 = min(g.nz - 1, (int)floorf(hz));
-                        for (int iz = iz0; iz <= iz1; iz++)
-                            for (int iy = iy0; iy <= iy1; iy++)
-                                for (int ix = ix0; ix <= ix1; ix++) {
-                                    const int c = g.cell_base + (iz * g.ny + iy) * g.nx + ix;
-                                    const int pe = a.cell_start[c + 1];
-                                    for (int pi = a.cell_start[c]; pi < pe; pi++) {
-                                        const float4 o = a.grid_pts[pi];
-                                        const float dx = xp - o.x, dy = yp - o.y, dz = zp - o.z;
-                                        const float d = dx * dx + dy * dy + dz * dz;
-                                        const int oi = __float_as_int(o.w);
-                                        if (d < best || (d == best && oi < bidx)) { best = d; bidx = oi; }
-                                    }
+                        // the radius box spans <= 2 cells per axis (cell >= 2 r): fetch the <= 8 cell ranges
+                        // with independent loads, then each cell's points four at a time (clamped loads
+                        // issued together) -- the (distance, index) minimum does not depend on the order
+                        int cb[8], ce[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const int ix = ix0 + (q & 1), iy = iy0 + ((q >> 1) & 1), iz = iz0 + (q >> 2);
+                            const bool ok = ix <= ix1 && iy <= iy1 && iz <= iz1;
+                            const int c = g.cell_base + (iz * g.ny + iy) * g.nx + ix;
+                            cb[q] = ok ? a.cell_start[c] : 0;
+                            ce[q] = ok ? a.cell_start[c + 1] : 0;
+                        }
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            for (int pi = cb[q]; pi < ce[q]; pi += 4) {
+                                float4 o[4];
+#pragma unroll
+                                for (int u = 0; u < 4; u++) o[u] = a.grid_pts[min(pi + u, ce[q] - 1)];
+#pragma unroll
+                                for (int u = 0; u < 4; u++) {
+                                    const float dx = xp - o[u].x, dy = yp - o[u].y, dz = zp - o[u].z;
+                                    const float d = dx * dx + dy * dy + dz * dz;
+                                    const int oi = __float_as_int(o[u].w);
+                                    const bool take = pi + u < ce[q] && (d < best || (d == best && oi < bidx));
+                                    best = take ? d : best;
+                                    bidx = take ? oi : bidx;
                                 }
+                            }
+                        }
                     }
                 }
                 // compute_costs.cuh:201-270 (cost types 0 / 2: explained marking; type 1: colour gate first)
