@@ -40,6 +40,7 @@ struct pcore_ctx {
     DevBuf<uint32_t> mtris;
     DevBuf<Meshlet> meshlets;
     DevBuf<int32_t> model_ml_lo, model_ml_hi;
+    DevBuf<float4> model_box;  // FusedArgs::model_box
     bool have_mesh = false;
     // camera
     pcore_camera cam{};
@@ -78,6 +79,17 @@ struct pcore_ctx {
     DevBuf<float4> tri_lab;       // Lab per original triangle
     DevBuf<float4> obs_lab;       // Lab per observed point, label-sorted
     DevBuf<int32_t> colour_id;    // N x nsamp scratch of the fused kernel's colour id pass
+    DevBuf<int32_t> ovf_list;     // poses deferred to the fused overflow launch
+    DevBuf<int32_t> ovf_ctr;      // two list counters, used by alternate calls (FusedArgs::ovf_slot)
+    DevBuf<int32_t> win_hist;     // FusedArgs::win_hist
+    int32_t* fb_host = nullptr;   // mapped host memory (FusedArgs::fb_host), host view
+    int32_t* fb_dev = nullptr;    // the same, device view
+    int ovf_slot = 0;
+    int32_t fb_seq = 0;           // sequence number of the last fused launch
+    int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
+    long long tile_key = -1;      // ws, hs, bitmap words, colour of the current tile configuration
+    int tile_tier = 0;
+    double ovf_frac = 1.0;        // fraction of the poses the chosen tier defers (last histogram)
     std::vector<int> obs_order;   // label-sorted position -> caller's observed index
     bool have_obs_colours = false;
     DevBuf<double> metric_part;  // ADD / ADD-S per-block partial sums
@@ -314,7 +326,9 @@ void pcore_destroy(pcore_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)dev_free(c->tris); (void)dev_free(c->tri_lo); (void)dev_free(c->tri_hi);
     (void)dev_free(c->mverts); (void)dev_free(c->mtris); (void)dev_free(c->meshlets);
-    (void)dev_free(c->model_ml_lo); (void)dev_free(c->model_ml_hi); (void)dev_free(c->proj);
+    (void)dev_free(c->model_ml_lo); (void)dev_free(c->model_ml_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
+    (void)dev_free(c->ovf_list); (void)dev_free(c->ovf_ctr); (void)dev_free(c->win_hist);
+    if (c->fb_host) (void)hipHostFree(c->fb_host);
     (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
     (void)dev_free(c->grids); (void)dev_free(c->cell_start); (void)dev_free(c->grid_pts);
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
@@ -344,6 +358,7 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     std::vector<float4> mv;
     std::vector<uint32_t> mt, mo;
     std::vector<Meshlet> ml;
+    std::vector<float4> box;
     std::vector<int32_t> mlo(num_models), mhi(num_models), tlo(num_models), thi(num_models);
     int t0 = 0;
     for (int m = 0; m < num_models; m++) {
@@ -375,6 +390,17 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
                 }
                 tv[(size_t)3 * t + k] = id;
             }
+        // bounding box of the model's vertices (pose windows); w = 1 when every coordinate is finite
+        float4 bmin = make_float4(INFINITY, INFINITY, INFINITY, 1.0f), bmax = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+        for (size_t i = 0; i < vxyz.size(); i += 3) {
+            if (!std::isfinite(vxyz[i]) || !std::isfinite(vxyz[i + 1]) || !std::isfinite(vxyz[i + 2])) bmin.w = 0.0f;
+            bmin.x = std::min(bmin.x, vxyz[i]); bmax.x = std::max(bmax.x, vxyz[i]);
+            bmin.y = std::min(bmin.y, vxyz[i + 1]); bmax.y = std::max(bmax.y, vxyz[i + 1]);
+            bmin.z = std::min(bmin.z, vxyz[i + 2]); bmax.z = std::max(bmax.z, vxyz[i + 2]);
+        }
+        if (vxyz.empty()) bmin = bmax = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        box.push_back(bmin);
+        box.push_back(bmax);
         mlo[m] = (int)ml.size();
         build_meshlets(tv, (int)(vxyz.size() / 3), vxyz, t0, mv, mt, mo, ml);
         mhi[m] = (int)ml.size();
@@ -397,6 +423,7 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     HIPC(c, dev_upload(c->tri_lab, tl));
     HIPC(c, dev_upload(c->model_ml_lo, mlo));
     HIPC(c, dev_upload(c->model_ml_hi, mhi));
+    HIPC(c, dev_upload(c->model_box, box));
     c->num_models = num_models;
     c->num_tris = num_tris;
     c->have_mesh = true;
@@ -608,6 +635,73 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
     return PCORE_OK;
 }
 
+// Tile of the fused window launch ("Pose windows"): the tier with the most workgroups per CU
+// whose tile holds the windows of >= 99 % of the poses of the last finished call with the same sampled
+// image; tier 0 until one is known.  Only the speed depends on the choice, never the results.
+static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
+    const size_t lds_cu = c->prop.maxSharedMemoryPerMultiProcessor ? c->prop.maxSharedMemoryPerMultiProcessor
+                                                                   : (size_t)160 * 1024;
+    const bool colour = a.cid != nullptr;
+    const int nsamp = a.ws * a.hs;
+    hipError_t e;
+    if (!c->fb_host) {
+        if ((e = hipHostMalloc((void**)&c->fb_host, 16 * sizeof(int32_t), hipHostMallocMapped)) != hipSuccess) return e;
+        std::memset(c->fb_host, 0, 16 * sizeof(int32_t));
+        c->fb_host[kTileTiers + 2] = -1;
+        if ((e = hipHostGetDevicePointer((void**)&c->fb_dev, c->fb_host, 0)) != hipSuccess) return e;
+        if ((e = dev_reserve(c->ovf_ctr, 2)) != hipSuccess) return e;
+        if ((e = dev_reserve(c->win_hist, kTileTiers + 1)) != hipSuccess) return e;
+        if ((e = hipMemset(c->ovf_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
+        if ((e = hipMemset(c->win_hist.p, 0, (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
+    }
+    if ((e = dev_reserve(c->ovf_list, (size_t)num_poses)) != hipSuccess) return e;
+    int edge[kTileTiers];
+    for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, lds_cu);
+    const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);
+    if (key != c->tile_key) {
+        c->tile_key = key;
+        c->tile_key_seq = c->fb_seq + 1;
+        c->tile_tier = 0;
+        c->ovf_frac = 1.0;
+    } else {
+        volatile int32_t* fb = c->fb_host;
+        const int32_t seq = fb[kTileTiers + 2];
+        if (seq >= c->tile_key_seq && seq <= c->fb_seq) {
+            int32_t h[kTileTiers + 1];
+            long long tot = 0;
+            for (int b = 0; b <= kTileTiers; b++) tot += (h[b] = fb[b]);
+            if (tot > 0) {
+                int tier = kTileTiers - 1;
+                long long over = tot;  // windows above edge[t]
+                for (int t = 0; t < kTileTiers; t++) {
+                    over -= h[t];
+                    if (edge[t] > 0 && over * 100 <= tot) { tier = t; break; }
+                }
+                c->tile_tier = tier;
+                c->ovf_frac = (double)over / (double)tot;
+            }
+        }
+    }
+    if (const char* env = getenv("PCORE_FUSED_TIER")) {
+        c->tile_tier = std::min(std::max(atoi(env), 0), kTileTiers);
+        c->ovf_frac = 1.0;
+    }
+    // overflow launch: twice the predicted deferred poses + 16 workgroups (any count is still covered by the
+    // grid-stride loop); the whole 1024 until a histogram is known
+    a.ovf_grid = (int)std::min<double>(kOvfGrid, 2.0 * c->ovf_frac * num_poses + 16.0);
+    // tier kTileTiers (A/B knob only): the whole image
+    a.tcap = c->tile_tier < kTileTiers && edge[c->tile_tier] > 0 ? edge[c->tile_tier] : nsamp;
+    for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
+    a.ovf_list = c->ovf_list.p;
+    a.ovf_ctr = c->ovf_ctr.p;
+    a.ovf_slot = c->ovf_slot;
+    c->ovf_slot ^= 1;
+    a.win_hist = c->win_hist.p;
+    a.fb_host = c->fb_dev;
+    a.fb_seq = ++c->fb_seq;
+    return hipSuccess;
+}
+
 static int ensure_sampled(pcore_ctx* c, int stride, hipStream_t s) {
     if (c->sampled_stride == stride) return PCORE_OK;
     const int ws = (c->cam.width + stride - 1) / stride, hs = (c->cam.height + stride - 1) / stride;
@@ -643,7 +737,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
         return fail(c, PCORE_E_INVALID_ARG, "evaluate: width must be a multiple of stride");
     const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
     if (ws > 4095 || hs > 4095) return fail(c, PCORE_E_INVALID_ARG, "evaluate: sampled image too large");
-    const size_t lds = fused_lds_bytes(ws, hs, c->bitmap_words, p->cost_type == PCORE_COST_RGBD_3DOF);
+    const size_t lds = fused_lds_bytes(ws * hs, c->bitmap_words, p->cost_type == PCORE_COST_RGBD_3DOF);
     if (lds > (size_t)c->prop.sharedMemPerBlock)
         return fail(c, PCORE_E_INVALID_ARG,
                     "evaluate: sampled z-buffer does not fit in LDS (use a larger stride); need " +
@@ -665,6 +759,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.meshlets = c->meshlets.p;
     a.model_ml_lo = c->model_ml_lo.p;
     a.model_ml_hi = c->model_ml_hi.p;
+    a.model_box = c->model_box.p;
     a.num_models = c->num_models;
     const float* pj = c->cam.proj;
     a.p00 = pj[0]; a.p01 = pj[1]; a.p02 = pj[2]; a.p03 = pj[3];
@@ -699,6 +794,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
         a.cid = c->colour_id.p;
     }
     if (const char* e = getenv("PCORE_DEBUG_SKIP")) a.dbg_skip = atoi(e);
+    HIPC(c, set_fused_tiles(c, num_poses, a));
     HIPC(c, launch_fused_cost(a, s));
     return PCORE_OK;
 }
@@ -712,6 +808,7 @@ static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& 
     a.meshlets = c->meshlets.p;
     a.model_ml_lo = c->model_ml_lo.p;
     a.model_ml_hi = c->model_ml_hi.p;
+    a.model_box = c->model_box.p;
     a.num_models = c->num_models;
     const float* pj = c->cam.proj;
     a.p00 = pj[0]; a.p01 = pj[1]; a.p02 = pj[2]; a.p03 = pj[3];

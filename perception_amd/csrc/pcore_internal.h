@@ -35,6 +35,11 @@ struct LabelGrid {
     int32_t pad1, pad2;
 };
 
+// tile tiers of the fused window launch: workgroups per CU 6, 5, 4, 3, 2 (the LDS tile that leaves room
+// for that many workgroups); the host picks the tier from the previous call's window histogram
+constexpr int kTileTiers = 5;
+constexpr int kTierWGs[kTileTiers] = {6, 5, 4, 3, 2};
+
 struct FusedArgs {
     // batch
     const float* poses;
@@ -48,6 +53,7 @@ struct FusedArgs {
     const Meshlet* meshlets;
     const int32_t* model_ml_lo;
     const int32_t* model_ml_hi;
+    const float4* model_box;  // 2 per model: (min x, y, z, 1 if every vertex is finite), (max x, y, z, 0)
     int32_t num_models;
     // camera
     float p00, p01, p02, p03, p10, p11, p12, p13;  // rows 0 and 1 of proj
@@ -79,6 +85,20 @@ struct FusedArgs {
     const float4* obs_lab;      // Lab of every observed point, label-sorted order
     int32_t* cid;               // N x nsamp scratch: original triangle of each sample's nearest fragment
     float colour_thr;           // color_distance_threshold
+    // sample windows ("Pose windows"): the z-sample tile in LDS holds `tcap` samples; a pose
+    // whose window is larger is appended to ovf_list and scored by the overflow launch (tile = ws * hs).
+    // ovf_ctr[ovf_slot] counts the list; the overflow launch zeroes ovf_ctr[1 - ovf_slot] for the next call.
+    int32_t tcap;
+    int32_t* ovf_list;
+    int32_t* ovf_ctr;
+    int32_t ovf_slot;
+    // window-size histogram (bin b: windows of at most hist_edge[b] samples, the last bin the rest),
+    // published by the overflow launch to fb_host (mapped host memory) and reset there
+    int32_t hist_edge[kTileTiers];
+    int32_t* win_hist;  // kTileTiers + 1 bins
+    int32_t* fb_host;   // kTileTiers + 1 bins + 1 overflow count + 1 sequence number
+    int32_t fb_seq;
+    int32_t ovf_grid;   // workgroups of the overflow launch (from the predicted overflow count)
     // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
     // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
     int32_t dbg_skip;
@@ -135,7 +155,12 @@ int pose_dist_blocks(int n);
 hipError_t launch_pose_distances(const float* pts, int n, const double* T_gt, const double* T_est, int pairs,
                                  double* part, double* out_add, double* out_adds, hipStream_t s);
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
-size_t fused_lds_bytes(int ws, int hs, int bitmap_words, bool colour = false);
+// LDS of one fused / cloud workgroup whose z-sample tile holds `tile_samples` samples
+size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour = false);
+// tile capacity (samples) of tier t: the largest tile that leaves room for kTierWGs[t] workgroups per CU
+// (capped at the whole sampled image)
+int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, size_t lds_per_cu);
+constexpr int kOvfGrid = 1024;  // most workgroups of the overflow launch (grid-stride over the list)
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
                               const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
                               const float* proj, int32_t* depth, hipStream_t s);

@@ -18,8 +18,10 @@
 #include "pcore_internal.h"
 #include "pcore_colour.h"
 
+#include <algorithm>
 #include <climits>
 #include <cfloat>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -185,14 +187,20 @@ struct FusedSmem {
 // IDPASS = false: depth pass (atomicMin of the fragment depth).  IDPASS = true: colour id pass over the
 // final depths: the fragments whose depth equals the sample's minimum leave the lowest original triangle
 // index -- the colour the reference's serial z-test (strict <) keeps.
+// Sample window of a pose: samples kx in [x0, x0 + nx), ky in [y0, y0 + ny); the LDS z-sample tile stores
+// them row-major, sample (kx, ky) at (ky - y0) * nx + (kx - x0).
+struct SampleWin {
+    int x0, y0, nx, ny;
+};
+
 template <bool IDPASS = false>
-__device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, int s, int H, int ws, int32_t* zbuf,
-                                              int32_t* cid = nullptr, uint32_t id = 0) {
+__device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, int s, int H, const SampleWin& w,
+                                              int32_t* zbuf, int32_t* cid = nullptr, uint32_t id = 0) {
     const float P0 = (float)(kx * s);
     const float P1 = (float)(H - 1 - ky * s);
     int32_t d;
     if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d)) {
-        const int k = ky * ws + kx;
+        const int k = (ky - w.y0) * w.nx + (kx - w.x0);
         if constexpr (IDPASS) {
             if (d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
         } else {
@@ -201,9 +209,9 @@ __device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, i
     }
 }
 
-size_t fused_lds_bytes(int ws, int hs, int bitmap_words, bool colour) {
+size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-    size_t b = al((size_t)ws * hs * 4);
+    size_t b = al((size_t)tile_samples * 4);
     b += al((size_t)kWaves * kWave * 4) * 3;
     b += al((size_t)kWaves * kWave * 8);
     b += al((size_t)kWaves * kRecCap * sizeof(TriRec));
@@ -274,12 +282,13 @@ __device__ __forceinline__ Meshlet load_meshlet(const Meshlet* p, int m) {
 }
 
 template <int STRIDE, bool IDPASS = false>
-__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, int32_t* cid = nullptr) {
+__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw,
+                                             int32_t* cid = nullptr) {
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of meshlet headers
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
-    const int W = a.width, H = a.height, ws = a.ws;
+    const int W = a.width, H = a.height;
     // pose (wave-uniform -> scalar loads)
     const float* P = a.poses + (size_t)16 * pose;
     const float m00 = P[0], m01 = P[1], m02 = P[2], m03 = P[3];
@@ -297,8 +306,10 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     uint2* vwin = sm.vwin + wave * kWave;
     TriRec* ring = sm.ring + wave * kRecCap;
     uint32_t* ring_id = IDPASS ? sm.ring_id + wave * kRecCap : nullptr;
-    const short2v wzero = {0, 0};
-    const short2v wlim = {(short)(ws - 1), (short)(a.hs - 1)};
+    // every triangle window is clipped to the pose window (a no-op when the window is conservative, and the
+    // bound that keeps the tile indexing in range whatever the input)
+    const short2v wzero = {(short)sw.x0, (short)sw.y0};
+    const short2v wlim = {(short)(sw.x0 + sw.nx - 1), (short)(sw.y0 + sw.ny - 1)};
     int rec_count = 0;  // wave-uniform
 
     const int dbg = a.dbg_skip;
@@ -314,7 +325,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 const int nx = ((r.meta >> 24) & 0xf) + 1, ny = ((r.meta >> 28) & 0xf) + 1;
                 for (int iy = 0; iy < ny; iy++)
                     for (int ix = 0; ix < nx; ix++)
-                        raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, ws, sm.zbuf, cid, id);
+                        raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
             }
         }
         wave_sync();
@@ -399,6 +410,14 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     float bmin[2], bmax[2];
                     bbox_ref(p, cmax0, cmax1, bmin, bmax);
                     nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
+                    if (nk > 0) {  // clip to the pose window
+                        const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
+                        kx0 = max(kx0, sw.x0);
+                        ky0 = max(ky0, sw.y0);
+                        nx = kx1 - kx0;
+                        ny = ky1 - ky0;
+                        nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+                    }
                 }
             }
             TriRec r;
@@ -429,7 +448,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 for (int q = lane; q < bnk; q += kWave) {
                     int iy = (int)(((float)q + 0.5f) * inv_nx), ix = q - iy * bnx;
                     if (ix < 0) { iy--; ix += bnx; } else if (ix >= bnx) { iy++; ix -= bnx; }
-                    raster_sample<IDPASS>(rb, bkx0 + ix, bky0 + iy, s, H, ws, sm.zbuf, cid, bid);
+                    raster_sample<IDPASS>(rb, bkx0 + ix, bky0 + iy, s, H, sw, sm.zbuf, cid, bid);
                 }
             }
             // small triangles: queue into the wave's ring
@@ -457,37 +476,92 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     if (rec_count > 0) flush(rec_count);
 }
 
-template <int STRIDE, bool COLOUR = false>
-__global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int pose = blockIdx.x;
+// Conservative sample window of a pose ("Pose windows").  Lanes 0-7 of every wave project the
+// corners of the model's bounding box with the vertex stage's own arithmetic; the window is their screen
+// box widened by a bound on the float error of any vertex's projection, mapped to samples through the
+// bounds of vertex_window (every triangle window lies inside).  The whole sampled image when the box is
+// not finite or comes within 5 % of its depth magnitude of the camera plane.  Wave-uniform; every wave of
+// the workgroup computes the same window.
+__device__ SampleWin pose_window(const FusedArgs& a, int model, const float (&m)[12], int s) {
+    const SampleWin whole = {0, 0, a.ws, a.hs};
+    const float4 lo = a.model_box[2 * model], hi = a.model_box[2 * model + 1];
+    const int c = lane_id() & 7;
+    const float x = (c & 1) ? hi.x : lo.x, y = (c & 2) ? hi.y : lo.y, z = (c & 4) ? hi.z : lo.z;
+    const float Wf = (float)a.width, Hf = (float)a.height;
+    const float lx = row4(m[0], m[1], m[2], m[3], x, y, z);
+    const float ly = row4(m[4], m[5], m[6], m[7], x, y, z);
+    const float lz = row4(m[8], m[9], m[10], m[11], x, y, z);
+    const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
+    const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
+    const float sx = px / lz * Wf / 2.0f + Wf / 2.0f;
+    const float sy = py / lz * Hf / 2.0f + Hf / 2.0f;
+    const bool bad = !(fabsf(sx) < 1.0e7f) || !(fabsf(sy) < 1.0e7f) || !(lz > 0.0f);  // also NaN
+    float lzmin = lz, sx0 = sx, sx1 = sx, sy0 = sy, sy1 = sy;
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+        lzmin = fminf(lzmin, __shfl_xor(lzmin, off));
+        sx0 = fminf(sx0, __shfl_xor(sx0, off));
+        sx1 = fmaxf(sx1, __shfl_xor(sx1, off));
+        sy0 = fminf(sy0, __shfl_xor(sy0, off));
+        sy1 = fmaxf(sy1, __shfl_xor(sy1, off));
+    }
+    auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    lzmin = uni(lzmin); sx0 = uni(sx0); sx1 = uni(sx1); sy0 = uni(sy0); sy1 = uni(sy1);
+    if ((__ballot(bad) & 0xffull) || lo.w == 0.0f) return whole;
+    // magnitude of the terms of each camera row over the box (bounds the rounding of any vertex's row)
+    const float ax = fmaxf(fabsf(lo.x), fabsf(hi.x)), ay = fmaxf(fabsf(lo.y), fabsf(hi.y));
+    const float az = fmaxf(fabsf(lo.z), fabsf(hi.z));
+    const float Bx = fabsf(m[0]) * ax + fabsf(m[1]) * ay + fabsf(m[2]) * az + fabsf(m[3]);
+    const float By = fabsf(m[4]) * ax + fabsf(m[5]) * ay + fabsf(m[6]) * az + fabsf(m[7]);
+    const float Bz = fabsf(m[8]) * ax + fabsf(m[9]) * ay + fabsf(m[10]) * az + fabsf(m[11]);
+    if (!(lzmin > 0.05f * Bz)) return whole;
+    // |error of sx| <= (W/2) (Pbx / lzmin) eps (8 + 4 Bz / lzmin) + 4 eps (|sx| + W), Bz / lzmin <= 20
+    const float eps = 5.9604645e-8f;
+    const float Pbx = fabsf(a.p00) * Bx + fabsf(a.p01) * By + fabsf(a.p02) * Bz + fabsf(a.p03);
+    const float Pby = fabsf(a.p10) * Bx + fabsf(a.p11) * By + fabsf(a.p12) * Bz + fabsf(a.p13);
+    const float mgx = 2.0f + 256.0f * eps * (0.5f * Wf) * Pbx / lzmin + 8.0f * eps * (fmaxf(fabsf(sx0), fabsf(sx1)) + Wf);
+    const float mgy = 2.0f + 256.0f * eps * (0.5f * Hf) * Pby / lzmin + 8.0f * eps * (fmaxf(fabsf(sy0), fabsf(sy1)) + Hf);
+    if (!(mgx < 1.0e6f) || !(mgy < 1.0e6f)) return whole;
+    const float xlo = sx0 - mgx, xhi = sx1 + mgx, ylo = sy0 - mgy, yhi = sy1 + mgy;
+    // vertex_window: lo.x >= (sx - 0.5) / s, hi.x <= sx / s; lo.y >= (H - 1 - sy) / s, hi.y <= (H - 0.5 - sy) / s
+    const float sf = (float)s;
+    const int X0 = max(0, (int)floorf((xlo - 1.0f) / sf)), X1 = min(a.ws - 1, (int)floorf(xhi / sf));
+    const int Y0 = max(0, (int)floorf((Hf - 1.0f - yhi) / sf)), Y1 = min(a.hs - 1, (int)floorf((Hf - ylo) / sf));
+    return SampleWin{X0, Y0, max(0, X1 - X0 + 1), max(0, Y1 - Y0 + 1)};
+}
+
+// One pose of stage COST on the workgroup's LDS tile (sw.nx * sw.ny <= tile capacity).
+template <int STRIDE, bool COLOUR>
+__device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw) {
     const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of meshlet headers
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
-    const int ws = a.ws, hs = a.hs;
-    const int nsamp = ws * hs;
+    const int ws = a.ws, nsamp = a.ws * a.hs;
+    const int tn = sw.nx * sw.ny;  // samples of the window (tile)
 
-    const FusedSmem sm = carve_smem(smem_raw, nsamp, a.bitmap_words, COLOUR);
-    for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
+    for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
     for (int i = tid; i < a.bitmap_words; i += kThreads) sm.bitmap[i] = 0u;
     if (tid < 4) sm.counters[tid] = 0;
+    if (a.dbg_zs)  // debug z-samples: the samples outside the window stay 0
+        for (int i = tid; i < nsamp; i += kThreads) a.dbg_zs[(size_t)pose * nsamp + i] = 0;
 
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
-    raster_phase<STRIDE>(a, sm, pose);
+    raster_phase<STRIDE>(a, sm, pose, sw);
     __syncthreads();
     int32_t* cid = nullptr;
     if constexpr (COLOUR) {
-        // colour id pass (cost_type 1): which triangle left each sample's minimum depth
+        // colour id pass (cost_type 1): which triangle left each sample's minimum depth (tile-local index)
         cid = a.cid + (size_t)pose * nsamp;
-        for (int i = tid; i < nsamp; i += kThreads) cid[i] = INT_MAX;
+        for (int i = tid; i < tn; i += kThreads) cid[i] = INT_MAX;
         __syncthreads();
-        raster_phase<STRIDE, true>(a, sm, pose, cid);
+        raster_phase<STRIDE, true>(a, sm, pose, sw, cid);
         __syncthreads();
     }
 
     // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
+    // per-wave point queue in the (now free) triangle ring: (tile index, kx | ky << 16) pairs
     int32_t* queue = reinterpret_cast<int32_t*>(sm.ring) + wave * (kRecCap * (int)sizeof(TriRec) / 4);
     int qcount = 0;
     const int grid_id = use_seg ? pl : a.num_grids;
@@ -503,9 +577,10 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
             const int j = base + lane;
             bool is_bad = false;
             if (j < count) {
-                const int k = queue[j];
+                const int k = queue[2 * j];
+                const int kxy = queue[2 * j + 1];
                 const int32_t Z = sm.zbuf[k];
-                const int ky = k / ws, kx = k - ky * ws;
+                const int kx = kxy & 0xffff, ky = kxy >> 16;
                 // compute_point_clouds.cuh:14-22 with depth_factor (cm -> m)
                 const float zp = (float)Z / a.depth_factor;
                 const float xp = ((float)(kx * s) - a.cx) / a.fx * zp;
@@ -573,21 +648,34 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     };
 
     int wave_pts = 0;  // wave-uniform
-    for (int base = wave * kWave; base < nsamp; base += kThreads) {
+    // tile index k -> (ix, iy) without an integer division: (k + 0.5) / nx in float is within 1e-3 of the
+    // quotient (k < 2^14), so one correction step gives the exact row
+    const float inv_nx = tn > 0 ? 1.0f / (float)sw.nx : 0.0f;
+    for (int base = wave * kWave; base < tn; base += kThreads) {
         const int k = base + lane;
         bool valid = false;
-        if (k < nsamp && !(a.dbg_skip & 4)) {
+        int kx = 0, ky = 0;
+        if (k < tn && !(a.dbg_skip & 4)) {
+            int iy = (int)(((float)k + 0.5f) * inv_nx), ix = k - iy * sw.nx;
+            if (ix < 0) { iy--; ix += sw.nx; } else if (ix >= sw.nx) { iy++; ix -= sw.nx; }
+            kx = sw.x0 + ix;
+            ky = sw.y0 + iy;
+            const int gk = ky * ws + kx;
             const int32_t z = sm.zbuf[k];
             // no fragment: Z = 0 whatever the source (the sampled source is read only under a fragment)
             const int32_t zf = z == INT_MAX ? 0
-                                            : occlusion_rule(z, a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg,
+                                            : occlusion_rule(z, a.src_s[gk], use_seg ? (int)a.lab_s[gk] : 0, use_seg,
                                                              pl, a.occlusion_threshold);
             if (zf != z) sm.zbuf[k] = zf;
-            if (a.dbg_zs) a.dbg_zs[(size_t)pose * nsamp + k] = zf;
+            if (a.dbg_zs) a.dbg_zs[(size_t)pose * nsamp + gk] = zf;
             valid = zf > 0;  // depth_to_mask, compute_point_clouds.cuh:64
         }
         const uint64_t bv = __ballot(valid);
-        if (valid) queue[qcount + mbcnt64(bv)] = k;
+        if (valid) {
+            const int q = qcount + mbcnt64(bv);
+            queue[2 * q] = k;
+            queue[2 * q + 1] = kx | (ky << 16);
+        }
         qcount += __popcll(bv);
         wave_pts += __popcll(bv);
         if (qcount >= kWave) {
@@ -633,6 +721,69 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
     }
 }
 
+__device__ __forceinline__ void load_pose_rows(const float* poses, int pose, float (&m)[12]) {
+    const float* P = poses + (size_t)16 * pose;
+#pragma unroll
+    for (int i = 0; i < 12; i++) m[i] = P[i];
+}
+
+// Window launch: one workgroup per pose, LDS tile of a.tcap samples.  A pose whose window exceeds the tile
+// goes to the overflow list (its outputs are written by fused_cost_ovf_kernel, launched next).
+template <int STRIDE, bool COLOUR = false>
+__global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int pose = blockIdx.x;
+    const FusedSmem sm = carve_smem(smem_raw, a.tcap, a.bitmap_words, COLOUR);
+    const int model = a.pose_model[pose];
+    SampleWin sw = {0, 0, 0, 0};  // invalid model: nothing is rendered
+    if (model >= 0 && model < a.num_models) {
+        float m[12];
+        load_pose_rows(a.poses, pose, m);
+        sw = pose_window(a, model, m, STRIDE > 0 ? STRIDE : a.stride);
+    }
+    const int tn = sw.nx * sw.ny;
+    if (threadIdx.x == 0) {
+        int b = 0;
+#pragma unroll
+        for (int t = 0; t < kTileTiers; t++) b += tn > a.hist_edge[t] ? 1 : 0;
+        atomicAdd(&a.win_hist[b], 1);
+        if (tn > a.tcap) a.ovf_list[atomicAdd(&a.ovf_ctr[a.ovf_slot], 1)] = pose;
+    }
+    if (tn > a.tcap) return;
+    fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
+}
+
+// Overflow launch: the poses fused_cost_kernel deferred, grid-stride over the list, LDS tile of the whole
+// sampled image.  Workgroup 0 also publishes the window histogram to the host, resets it, and zeroes the
+// other list counter (the one the next call counts with).
+template <int STRIDE, bool COLOUR = false>
+__global__ void __launch_bounds__(kThreads) fused_cost_ovf_kernel(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const FusedSmem sm = carve_smem(smem_raw, a.ws * a.hs, a.bitmap_words, COLOUR);
+    const int n = min(__builtin_amdgcn_readfirstlane(a.ovf_ctr[a.ovf_slot]), a.num_poses);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int b = 0; b <= kTileTiers; b++) {
+            a.fb_host[b] = a.win_hist[b];
+            a.win_hist[b] = 0;
+        }
+        a.fb_host[kTileTiers + 1] = n;
+        // no system fence: the host may read a torn set, which only steers the next tile choice
+        a.fb_host[kTileTiers + 2] = a.fb_seq;
+        a.ovf_ctr[1 - a.ovf_slot] = 0;
+    }
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int pose = __builtin_amdgcn_readfirstlane(a.ovf_list[i]);
+        if (pose < 0 || pose >= a.num_poses) continue;
+        const int model = a.pose_model[pose];
+        float m[12];
+        load_pose_rows(a.poses, pose, m);
+        const SampleWin sw = (model >= 0 && model < a.num_models) ? pose_window(a, model, m, STRIDE > 0 ? STRIDE : a.stride)
+                                                                  : SampleWin{0, 0, 0, 0};
+        fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
+        __syncthreads();  // the next pose re-initialises the LDS
+    }
+}
+
 // Stage CLOUD into per-pose scratch slots (the GICP source clouds): sampled raster, source occlusion,
 // then the reference's compaction order (row-major samples, compute_point_clouds.cuh:290-346).
 template <int STRIDE>
@@ -645,19 +796,36 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int ws = a.ws, nsamp = a.ws * a.hs;
     const FusedSmem sm = carve_smem(smem_raw, nsamp, 0);
-    for (int i = tid; i < nsamp; i += kThreads) sm.zbuf[i] = INT_MAX;
+    const int model = a.pose_model[pose];
+    SampleWin sw = {0, 0, 0, 0};
+    if (model >= 0 && model < a.num_models) {
+        float m[12];
+        load_pose_rows(a.poses, pose, m);
+        sw = pose_window(a, model, m, s);
+    }
+    const int tn = sw.nx * sw.ny;  // <= nsamp: the tile is the whole image here
+    for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
     if (tid == 0) carry_s = 0;
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
-    raster_phase<STRIDE>(a, sm, pose);
+    raster_phase<STRIDE>(a, sm, pose, sw);
     __syncthreads();
     float4* out = a.cloud_out + (size_t)pose * a.cloud_cap;
-    for (int base = 0; base < nsamp; base += kThreads) {
+    // row-major over the window = the reference's row-major compaction order (no valid sample lies outside)
+    const float inv_nx = tn > 0 ? 1.0f / (float)sw.nx : 0.0f;
+    for (int base = 0; base < tn; base += kThreads) {
         const int k = base + tid;
         int32_t zf = 0;
-        if (k < nsamp)
-            zf = occlusion_rule(sm.zbuf[k], a.src_s[k], use_seg ? (int)a.lab_s[k] : 0, use_seg, pl,
+        int kx = 0, ky = 0;
+        if (k < tn) {
+            int iy = (int)(((float)k + 0.5f) * inv_nx), ix = k - iy * sw.nx;
+            if (ix < 0) { iy--; ix += sw.nx; } else if (ix >= sw.nx) { iy++; ix -= sw.nx; }
+            kx = sw.x0 + ix;
+            ky = sw.y0 + iy;
+            const int gk = ky * ws + kx;
+            zf = occlusion_rule(sm.zbuf[k], a.src_s[gk], use_seg ? (int)a.lab_s[gk] : 0, use_seg, pl,
                                 a.occlusion_threshold);
+        }
         const bool valid = zf > 0;
         const uint64_t b = __ballot(valid);
         if (lane == 0) wsum[wave] = __popcll(b);
@@ -670,7 +838,6 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
         const int carry = carry_s;
         if (valid) {
             const int o = carry + woff + mbcnt64(b);
-            const int ky = k / ws, kx = k - ky * ws;
             const float zp = (float)zf / a.depth_factor;
             const float xp = ((float)(kx * s) - a.cx) / a.fx * zp;
             const float yp = ((float)(ky * s) - a.cy) / a.fy * zp;
@@ -684,7 +851,7 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
 }
 
 hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
-    const size_t lds = fused_lds_bytes(a.ws, a.hs, 0);
+    const size_t lds = fused_lds_bytes(a.ws * a.hs, 0);
     if (a.num_poses <= 0) return hipSuccess;
     if (a.stride == 8)
         hipLaunchKernelGGL(render_cloud_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
@@ -693,16 +860,39 @@ hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s) {
-    const bool colour = a.cid != nullptr;
-    const size_t lds = fused_lds_bytes(a.ws, a.hs, a.bitmap_words, colour);
-    if (a.num_poses <= 0) return hipSuccess;
+int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, size_t lds_per_cu) {
+    const int nsamp = ws * hs;
+    const size_t per_wg = (lds_per_cu / kTierWGs[t]) & ~size_t(511);  // LDS is allocated in 512-byte blocks
+    const size_t fixed = fused_lds_bytes(0, bitmap_words, colour);
+    if (per_wg <= fixed + 64) return 0;
+    const int cap = (int)((per_wg - fixed) / 4) & ~3;
+    return cap >= nsamp ? nsamp : cap;
+}
+
+hipError_t launch_fused_cost(const FusedArgs& a0, hipStream_t s) {
+    if (a0.num_poses <= 0) return hipSuccess;
+    const bool colour = a0.cid != nullptr;
+    const int nsamp = a0.ws * a0.hs;
+    FusedArgs a = a0;
+    if (a.tcap <= 0 || a.tcap > nsamp) a.tcap = nsamp;
+    const size_t lds = fused_lds_bytes(a.tcap, a.bitmap_words, colour);
     if (colour)
         hipLaunchKernelGGL((fused_cost_kernel<0, true>), dim3(a.num_poses), dim3(kThreads), lds, s, a);
     else if (a.stride == 8)
         hipLaunchKernelGGL(fused_cost_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
     else
         hipLaunchKernelGGL(fused_cost_kernel<0>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // one workgroup (the feedback) when no pose can overflow a whole-image tile
+    const size_t lds_full = fused_lds_bytes(nsamp, a.bitmap_words, colour);
+    const dim3 grid(a.tcap == nsamp ? 1 : std::max(1, std::min({a.num_poses, kOvfGrid, a.ovf_grid})));
+    if (colour)
+        hipLaunchKernelGGL((fused_cost_ovf_kernel<0, true>), grid, dim3(kThreads), lds_full, s, a);
+    else if (a.stride == 8)
+        hipLaunchKernelGGL(fused_cost_ovf_kernel<8>, grid, dim3(kThreads), lds_full, s, a);
+    else
+        hipLaunchKernelGGL(fused_cost_ovf_kernel<0>, grid, dim3(kThreads), lds_full, s, a);
     return hipGetLastError();
 }
 

@@ -194,6 +194,49 @@ def test_edge_poses(one_object):
     assert _bits_equal(df.cpu().numpy(), odf)
 
 
+def _edge_pose_batch():
+    P = []
+    for tz in (-0.5, 0.0, 0.02, 0.05, 0.12, 0.25, 3.0):
+        T = np.eye(4)
+        T[:3, 3] = (0.0, 0.0, tz)
+        P.append(T)
+    T = np.eye(4); T[:3, 3] = (2.0, 0.0, 0.8); P.append(T)       # out of view
+    T = np.eye(4); T[:3, 3] = (0.25, 0.1, 0.3); P.append(T)      # partly out of view
+    T = np.eye(4); T[:3, 3] = (0.0, 0.0, 0.10); T[:3, :3] = syn._rot_z(0.3); P.append(T)
+    return np.stack(P)
+
+
+@pytest.mark.parametrize("tier", [0, 2, 4, 5])
+def test_window_tiles_any_tier(one_object, tier, monkeypatch):
+    """Pose windows ("Pose windows"): the LDS tile tier only moves poses between the window and
+    the overflow launch.  A batch mixing ordinary and edge poses (huge / whole-image windows, poses behind
+    the camera) gives the oracle's costs and z-samples with every tier, 5 being the whole image."""
+    monkeypatch.setenv("PCORE_FUSED_TIER", str(tier))
+    case, core, t = one_object
+    sc = case.scene
+    s = case.stride
+    p16 = np.concatenate([case.poses[:40], init_from_eigen_batch(_edge_pose_batch()), case.poses[40:60]])
+    n = len(p16)
+    dev = t["poses"].device
+    poses = torch.from_numpy(p16).to(dev)
+    pm = torch.zeros(n, dtype=torch.int32, device=dev)
+    pl = torch.zeros(n, dtype=torch.int32, device=dev)
+    tot = torch.full((n,), float(case.pose_obs_total[0]), device=dev)
+    hs, ws = (sc.height + s - 1) // s, sc.width // s
+    dbg = torch.full((n, hs, ws), -7, dtype=torch.int32, device=dev)
+    for _ in range(2):  # the second call also runs with the tier the first call's histogram picks
+        rc, oc, df = core.evaluate(poses, pm, pl, tot, cost_type=2, stride=s, dbg_zs=dbg)
+    orc, ooc, odf = oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, p16, np.zeros(n, np.int32),
+                                    np.zeros(n, np.int32), sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask,
+                                    1.0, s, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz, case.label_start,
+                                    case.label_end, np.full(n, case.pose_obs_total[0], np.float32), 2, True, 0.01)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+    full = core.render(poses, pm, pl).cpu().numpy()
+    assert np.array_equal(dbg.cpu().numpy(), full[:, ::s, ::s])
+
+
 def test_empty_batch_and_errors(one_object):
     case, core, t = one_object
     dev = t["poses"].device

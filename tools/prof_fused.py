@@ -28,7 +28,7 @@ def main():
             w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
         else:
             w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()  # steady state: the next call sees this call's window histogram
     print("done", n)
 
 
