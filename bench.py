@@ -211,7 +211,7 @@ def main():
                    "height": w.scene.height, "stride": s, "parallelism": f"pose-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_BPS, "traffic": traffic,
-                     "kernel": "fused_cost_kernel", "kernel_ms": kern_ms,
+                     "kernel": "fused_cost_kernel (+ fused_cost_ovf_kernel: stage COST)", "kernel_ms": kern_ms,
                      "bytes_per_pose": bpp, "p_r_mean": p_r_mean, "valu": valu},
         "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},
     }
