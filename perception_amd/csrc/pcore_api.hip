@@ -88,7 +88,7 @@ struct pcore_ctx {
     int32_t fb_seq = 0;           // sequence number of the last fused launch
     int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
     long long tile_key = -1;      // ws, hs, bitmap words, colour of the current tile configuration
-    int tile_tier = 0;
+    int tile_tier = kDefaultTier;
     double ovf_frac = 1.0;        // fraction of the poses the chosen tier defers (last histogram)
     std::vector<int> obs_order;   // label-sorted position -> caller's observed index
     bool have_obs_colours = false;
@@ -637,7 +637,7 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
 
 // Tile of the fused window launch ("Pose windows"): the tier with the most workgroups per CU
 // whose tile holds the windows of >= 99 % of the poses of the last finished call with the same sampled
-// image; tier 0 until one is known.  Only the speed depends on the choice, never the results.
+// image; kDefaultTier until one is known.  Only the speed depends on the choice, never the results.
 static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
     const size_t lds_cu = c->prop.maxSharedMemoryPerMultiProcessor ? c->prop.maxSharedMemoryPerMultiProcessor
                                                                    : (size_t)160 * 1024;
@@ -661,7 +661,7 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
     if (key != c->tile_key) {
         c->tile_key = key;
         c->tile_key_seq = c->fb_seq + 1;
-        c->tile_tier = 0;
+        c->tile_tier = kDefaultTier;
         c->ovf_frac = 1.0;
     } else {
         volatile int32_t* fb = c->fb_host;
@@ -682,7 +682,7 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
             }
         }
     }
-    if (const char* env = getenv("PCORE_FUSED_TIER")) {
+    if (const char* env = getenv("PCORE_FUSED_TIER")) {  // A/B + test knob; >= kTileTiers: whole image
         c->tile_tier = std::min(std::max(atoi(env), 0), kTileTiers);
         c->ovf_frac = 1.0;
     }

@@ -39,6 +39,7 @@ struct LabelGrid {
 // for that many workgroups); the host picks the tier from the previous call's window histogram
 constexpr int kTileTiers = 5;
 constexpr int kTierWGs[kTileTiers] = {6, 5, 4, 3, 2};
+constexpr int kDefaultTier = 0;  // 6 workgroups per CU until a histogram is known
 
 struct FusedArgs {
     // batch

@@ -30,7 +30,10 @@ namespace pcore {
 constexpr int kWave = 64;
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr int kRecCap = 96;   // per-wave ring of queued triangle records (flush above kRecCap - 64)
+#ifndef PCORE_REC_CAP
+#define PCORE_REC_CAP 96
+#endif
+constexpr int kRecCap = PCORE_REC_CAP;  // per-wave ring of queued triangle records (flush above kRecCap - 64)
 constexpr int64_t PCORE_KEY_NONE_DEV = 0x7fffffffffffffffLL;
 constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queued; larger ones are
                               // processed cooperatively by the whole wave

@@ -206,11 +206,11 @@ def _edge_pose_batch():
     return np.stack(P)
 
 
-@pytest.mark.parametrize("tier", [0, 2, 4, 5])
+@pytest.mark.parametrize("tier", [0, 2, 4, 99])
 def test_window_tiles_any_tier(one_object, tier, monkeypatch):
     """Pose windows ("Pose windows"): the LDS tile tier only moves poses between the window and
     the overflow launch.  A batch mixing ordinary and edge poses (huge / whole-image windows, poses behind
-    the camera) gives the oracle's costs and z-samples with every tier, 5 being the whole image."""
+    the camera) gives the oracle's costs and z-samples with every tier, 99 being the whole image."""
     monkeypatch.setenv("PCORE_FUSED_TIER", str(tier))
     case, core, t = one_object
     sc = case.scene
