@@ -13,7 +13,9 @@
  *   - Plain C types only.  Large per-batch arrays are DEVICE pointers (e.g. tensor.data_ptr() of a
  *     PyTorch-ROCm tensor); mesh and camera setup take HOST pointers (copied once).
  *   - Every call is asynchronous on the caller's stream (`stream` may be NULL = default stream); the
- *     caller synchronises.  One context per (host thread, device); calls on a context are not re-entrant.
+ *     caller synchronises.  One context per (host thread, device); calls on a context are not re-entrant,
+ *     and its calls must all go to one stream (the context's device scratch -- GICP slots, the fused
+ *     kernel's overflow list and window histogram -- is reused by the next call in stream order).
  *   - Caller-allocated outputs.  The context owns persistent device scratch and never frees caller memory.
  *   - Return value: PCORE_OK or an error code; pcore_last_error() describes the last failure.
  *     The reference's in-band "invalid pose" convention (rendered cost -1, compute_costs.cuh:28-31) is kept.

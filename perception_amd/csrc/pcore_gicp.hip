@@ -30,15 +30,27 @@ namespace {
 
 constexpr int kGThreads = 256;
 constexpr int kMaxK = 16;
-// Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only).
+// Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only):
+// [0] nearest-target search, [1] covariance loads + contributions, [2] wave reduction, [3] lane-0 solve.
+// Each wave sums its clocks in registers and adds them once at exit (no atomics inside the loop); each
+// clock read is ordered after its phase's last result by an asm input dependency.
 #ifdef PCORE_GICP_PROFILE
 __device__ unsigned long long g_gicp_prof[4];
+#define GPROF_DECL unsigned long long gp_acc[4] = {0, 0, 0, 0}
 #define GPROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
-#define GPROF_ADD(k, a, b) \
-    if (lane == 0) atomicAdd(&g_gicp_prof[k], (unsigned long long)((b) - (a)))
+#define GPROF_TD(v, dep)                                                                   \
+    unsigned long long v;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "v"(dep) : "memory")
+#define GPROF_ADD(k, a, b) gp_acc[k] += (unsigned long long)((b) - (a))
+#define GPROF_FLUSH \
+    if (lane == 0)  \
+        for (int k_ = 0; k_ < 4; k_++) atomicAdd(&g_gicp_prof[k_], gp_acc[k_])
 #else
+#define GPROF_DECL
 #define GPROF_T(v)
+#define GPROF_TD(v, dep)
 #define GPROF_ADD(k, a, b)
+#define GPROF_FLUSH
 #endif
 
 constexpr int kTgtTile = 512;  // targets staged per wave in LDS, SoA (6 KiB)
@@ -624,6 +636,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ double sPart[WPP][28];
     __shared__ int sPose, sFlag;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    GPROF_DECL;
     for (;;) {
         group_sync<WPP>();  // the previous pose's reads of the shared state are done
         if (tid == 0) sPose = atomicAdd(g.work_counter, 1);
@@ -655,7 +668,6 @@ gicp_kernel(GicpArgs g, int num_poses) {
         bool done = ns <= 0 || nt <= 0;
         for (int it = 0; it < g.max_iter && !done; it++) {
             group_sync<WPP>();
-            GPROF_T(t_a);
             double R[3][3], t[3];
 #pragma unroll
             for (int r = 0; r < 3; r++) {
@@ -668,6 +680,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
             for (int v = 0; v < 28; v++) acc[v] = 0.0;
             // rounds of NT source points: point i -> thread i % NT, contributions added in point order
             for (int i0 = 0; i0 < ns; i0 += NT) {
+                GPROF_T(t_r0);
                 const int i = i0 + tid;
                 const bool act = i < ns;
                 const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -684,14 +697,18 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 } else {
                     scan_quads(tquads, (nt + 3) >> 2, qx, qy, qz, best, j);
                 }
+                GPROF_TD(t_r1, best);
                 if (act && j >= 0) {
                     double cs[6], ct[6];
                     load_cov(scov, i, cs);
                     load_cov(tcov, j, ct);
                     gicp_contrib(R, q, cs, tgt[j], ct, acc);
                 }
+                GPROF_TD(t_r2, acc[27]);
+                GPROF_ADD(0, t_r0, t_r1);
+                GPROF_ADD(1, t_r1, t_r2);
             }
-            GPROF_T(t_b);
+            GPROF_TD(t_b, acc[27]);
 #pragma unroll
             for (int v = 0; v < 28; v++) {
                 double x = acc[v];
@@ -714,20 +731,20 @@ gicp_kernel(GicpArgs g, int num_poses) {
                     }
                 }
             }
-            GPROF_T(t_c);
+            GPROF_TD(t_c, acc[27]);
             if (tid == 0) sFlag = solve_update(acc, R, t, RT, g.rot_eps, g.trans_eps);
             group_sync<WPP>();
             const int flag = __builtin_amdgcn_readfirstlane(sFlag);
-            GPROF_T(t_d);
-            GPROF_ADD(0, t_a, t_b);
-            GPROF_ADD(1, t_b, t_c);
-            GPROF_ADD(2, t_c, t_d);
+            GPROF_TD(t_d, flag);
+            GPROF_ADD(2, t_b, t_c);
+            GPROF_ADD(3, t_c, t_d);
             if (flag != 1) iters++;
             done = flag != 0;
         }
         group_sync<WPP>();
         if (tid == 0) write_pose(g, gp, RT, iters);
     }
+    GPROF_FLUSH;
 }
 
 

@@ -36,9 +36,9 @@ def main():
     fn(buf, 0)
     it = iters.cpu().numpy()
     total = int(it.sum()) + int((it < 150).sum())  # + the final non-updating solve
-    names = ["scan+contrib", "reduction", "solve"]
+    names = ["nn search", "contrib", "reduction", "solve"]
     print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())
-    for k in range(3):
+    for k in range(4):
         print(f"{names[k]:14s} {buf[k] / max(total, 1):10.0f} clk per pose-iteration")
 
 
