@@ -119,7 +119,17 @@ def main():
     w = workloads.build(poses_per_model=args.poses, device=local, rank=rank)
     n = int(w.poses.shape[0])
     out = tuple(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3))
-    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev)
+    # two key buffers: step i's all-reduce(MIN) overlaps step i + 1's kernels; a buffer is rewritten only
+    # after its previous exchange has completed (work.wait() orders the compute stream after it)
+    keys_ring = [torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev) for _ in range(2)]
+    works = [None, None]
+
+    def step_keys(i):
+        b = i % 2
+        if works[b] is not None:
+            works[b].wait()
+        keys_ring[b].fill_(PCORE_KEY_NONE)
+        return b, keys_ring[b]
 
     # rendered points per pose (for the algorithmic byte count), measured once outside the timed region
     # with one launch over the whole batch, so every fused-kernel launch of this process (and of its
@@ -131,10 +141,14 @@ def main():
     p_r_mean = int((dbg > 0).sum().item()) / max(n, 1)
     del dbg
 
-    for _ in range(args.warmup):
-        keys.fill_(PCORE_KEY_NONE)
+    for i in range(args.warmup):
+        b, keys = step_keys(i)
         workloads.step(w, out, keys)
-        pdist.allreduce_min_keys(keys)
+        works[b] = pdist.allreduce_min_keys_async(keys)
+    for b in range(2):
+        if works[b] is not None:
+            works[b].wait()
+            works[b] = None
     torch.cuda.synchronize()
 
     # per-launch duration of the dominant (fused) kernel, on the stream it runs on
@@ -145,12 +159,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        keys.fill_(PCORE_KEY_NONE)
+        b, keys = step_keys(i)
         ev[i][0].record(stream)
         w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=s, out=out)
         ev[i][1].record(stream)
         w.core.select(out[0], out[1], w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
-        pdist.allreduce_min_keys(keys)
+        works[b] = pdist.allreduce_min_keys_async(keys)
+    for wk in works:  # every exchange completes inside the timed region
+        if wk is not None:
+            wk.wait()
+    keys = keys_ring[(args.steps - 1) % 2]
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

@@ -9,7 +9,7 @@ exactly the reference's strict '<' first-index-wins scan (search_env.cpp:2560-25
 from __future__ import annotations
 
 import os
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -44,3 +44,12 @@ def allreduce_min_keys(keys: torch.Tensor) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(keys, op=dist.ReduceOp.MIN)
     return keys
+
+
+def allreduce_min_keys_async(keys: torch.Tensor) -> Optional["dist.Work"]:
+    """The same exchange, returned as a work handle (None on one process).  The caller waits on it before
+    reading or rewriting `keys`; meanwhile the next batch's kernels run beside the collective (RCCL runs on
+    its own stream, waiting only for the work already queued on the current one)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.all_reduce(keys, op=dist.ReduceOp.MIN, async_op=True)
+    return None
