@@ -53,14 +53,9 @@ __device__ unsigned long long g_gicp_prof[4];
 #define GPROF_FLUSH
 #endif
 
-constexpr int kTgtTile = 512;  // targets staged per wave in LDS, SoA (6 KiB)
-
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-struct TgtTile {
-    float x[kTgtTile], y[kTgtTile], z[kTgtTile];
-};
 constexpr double kPlaneScale = 1.0 - 1e-3;
 
 // LDS writes by some lanes of a wave visible to all its lanes (no block barrier: waves are independent)
@@ -364,66 +359,6 @@ hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_hos
 // GICP
 // ------------------------------------------------------------------------------------------------
 
-// Stage tn targets into a wave's SoA tile, padded to a multiple of 4 with +inf.  A non-finite target
-// (never the nearest in the oracle's scan: its distance is NaN or inf) is staged as +inf too, so no
-// distance in the packed scan is NaN for a finite query.
-template <int NT>
-__device__ __forceinline__ void stage_targets(TgtTile& T, const float4* tgt, int tn, int tid) {
-    const int tn4 = (tn + 3) & ~3;
-    for (int o = tid; o < tn4; o += NT) {
-        float4 p = o < tn ? tgt[o] : make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
-        if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) p = make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
-        T.x[o] = p.x;
-        T.y[o] = p.y;
-        T.z[o] = p.z;
-    }
-}
-
-// Nearest of a staged tile with packed f32 arithmetic (same IEEE operations, per element, as
-// sqdist3).  Four targets form a tournament that prefers the later target only when strictly nearer;
-// alternate quads feed two independent (best, index) chains, merged at the end by (distance, index):
-// together the lexicographic minimum of (distance, index), i.e. the oracle's first strict minimum.
-__device__ __forceinline__ void quad_min(const TgtTile& T, int o, f2v qx2, f2v qy2, f2v qz2, float& m, int& i) {
-    const f4v X = *reinterpret_cast<const f4v*>(&T.x[o]);
-    const f4v Y = *reinterpret_cast<const f4v*>(&T.y[o]);
-    const f4v Z = *reinterpret_cast<const f4v*>(&T.z[o]);
-    const f2v dxa = qx2 - X.xy, dya = qy2 - Y.xy, dza = qz2 - Z.xy;
-    const f2v dxb = qx2 - X.zw, dyb = qy2 - Y.zw, dzb = qz2 - Z.zw;
-    const f2v da = dxa * dxa + dya * dya + dza * dza;
-    const f2v db = dxb * dxb + dyb * dyb + dzb * dzb;
-    const bool c01 = da.y < da.x, c23 = db.y < db.x;
-    const float m01 = c01 ? da.y : da.x, m23 = c23 ? db.y : db.x;
-    const int i01 = c01 ? 1 : 0, i23 = c23 ? 3 : 2;
-    const bool c = m23 < m01;
-    m = c ? m23 : m01;
-    i = o + (c ? i23 : i01);
-}
-
-__device__ __forceinline__ void scan_targets(const TgtTile& T, int tn, int t0, float qx, float qy, float qz,
-                                             float& best, int& j) {
-    const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
-    float bA = INFINITY, bB = INFINITY;
-    int jA = -1, jB = -1;
-    int o = 0;
-#pragma unroll 2
-    for (; o + 8 <= tn; o += 8) {
-        float m;
-        int i;
-        quad_min(T, o, qx2, qy2, qz2, m, i);
-        if (m < bA) { bA = m; jA = i; }
-        quad_min(T, o + 4, qx2, qy2, qz2, m, i);
-        if (m < bB) { bB = m; jB = i; }
-    }
-    for (; o < tn; o += 4) {  // the last < 8 targets; tiles are padded to a multiple of 4
-        float m;
-        int i;
-        quad_min(T, o, qx2, qy2, qz2, m, i);
-        if (m < bA) { bA = m; jA = i; }
-    }
-    if (bB < bA || (bB == bA && jB >= 0 && jB < jA)) { bA = bB; jA = jB; }
-    if (bA < best) { best = bA; j = t0 + jA; }  // earlier tiles hold lower indices
-}
-
 // Nearest target by the segment's grid (segments above kGridNNMin): the lexicographic minimum of (float
 // squared distance, index) -- the brute-force scan's first strict minimum -- or j = -1 when no distance is
 // below +inf (a non-finite query).  Falls back to an in-order scan of the segment.
@@ -453,8 +388,11 @@ __device__ __forceinline__ void grid_nn(const LabelGrid& G, const int32_t* cell_
 // Nearest of a segment's targets read through the scalar cache: the segment is stored as quads of
 // 16 floats (x0..x3, y0..y3, z0..z3, 4 pad; non-finite and padding targets +inf), every lane scans the
 // same quads, so the loads are wave-uniform s_loads and the targets reach the VALU as SGPR operands --
-// no LDS traffic (an LDS broadcast read still moves 64 lanes x 16 B through the LDS pipe).  Same packed
-// arithmetic and tournament as quad_min, so the result is the oracle's first strict minimum.
+// no LDS traffic (an LDS broadcast read still moves 64 lanes x 16 B through the LDS pipe).  Packed f32
+// arithmetic with the same IEEE operations, per element, as sqdist3; four targets form a tournament that
+// prefers the later target only when strictly nearer; alternate quads feed two independent (best, index)
+// chains, merged at the end by (distance, index): together the lexicographic minimum of (distance, index),
+// i.e. the oracle's first strict minimum.
 typedef __attribute__((address_space(4))) const f4v cf4v;
 
 __device__ __forceinline__ void quad_min_s(f4v X, f4v Y, f4v Z, int o, f2v qx2, f2v qy2, f2v qz2, float& m,

@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(kMThreads) pose_dist_kernel(const float* pts, 
     red[1][threadIdx.x] = adds;
     __syncthreads();
     for (int s = kMThreads / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
+        if ((int)threadIdx.x < s) {
             red[0][threadIdx.x] += red[0][threadIdx.x + s];
             red[1][threadIdx.x] += red[1][threadIdx.x + s];
         }
