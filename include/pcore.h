@@ -151,7 +151,7 @@ typedef struct pcore_icp_params {
  * T * pose (concatenate_transforms, renderer.cu:1412-1429), re-render and re-score.  d_out_poses: N x 16
  * adjusted mat4x4 (the reference's adjusted_poses); d_out_iters (nullable): GICP iterations per pose.
  * Costs as pcore_evaluate, for the adjusted poses.  Device pointers; needs per-context scratch that
- * grows on first use (68 B per pose and stride sample; a batch is split into equal chunks that fit a
+ * grows on first use (64 B per pose and stride sample; a batch is split into equal chunks that fit a
  * budget of min(32 GiB, 40 % of the free device memory)). */
 int pcore_evaluate_icp(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model,
                        const int32_t* d_pose_label, const float* d_pose_obs_total, int32_t num_poses,
