@@ -165,6 +165,22 @@ class PoseCore:
             _ptr(df, torch.float32, "diff"), _ptr(dbg_zs, torch.int32, "dbg_zs"), _stream(stream)))
         return rc, oc, df
 
+    def capture_evaluate(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
+                         pose_obs_total: Optional[torch.Tensor], **kw):
+        """Stage COST of a fixed-size batch as a HIP graph (torch.cuda.CUDAGraph over the C-ABI launches).
+        One warm-up call reserves the scratch, samples the source and picks the LDS tile tier; then the
+        launches of one evaluate are captured.  Returns (replay, (rc, oc, diff)): replay() re-scores the batch
+        from the tensors' current contents (write new poses into `poses` in place).  For batches small enough
+        to be launch-bound (C1: 128 poses); the results equal evaluate()'s."""
+        n = int(poses.shape[0])
+        out = tuple(torch.empty(n, dtype=torch.float32, device=poses.device) for _ in range(3))
+        self.evaluate(poses, pose_model, pose_label, pose_obs_total, out=out, **kw)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            self.evaluate(poses, pose_model, pose_label, pose_obs_total, out=out, **kw)
+        return graph.replay, out
+
     def evaluate_icp(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
                      pose_obs_total: Optional[torch.Tensor], cost_type: int = _native.COST_DEPTH_6DOF,
                      calc_obs_cost: bool = True, stride: int = 8, depth_factor: float = 100.0,

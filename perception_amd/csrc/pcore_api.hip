@@ -80,11 +80,10 @@ struct pcore_ctx {
     DevBuf<float4> obs_lab;       // Lab per observed point, label-sorted
     DevBuf<int32_t> colour_id;    // N x nsamp scratch of the fused kernel's colour id pass
     DevBuf<int32_t> ovf_list;     // poses deferred to the fused overflow launch
-    DevBuf<int32_t> ovf_ctr;      // two list counters, used by alternate calls (FusedArgs::ovf_slot)
+    DevBuf<int32_t> ovf_ctr;      // FusedArgs::ovf_ctr
     DevBuf<int32_t> win_hist;     // FusedArgs::win_hist
     int32_t* fb_host = nullptr;   // mapped host memory (FusedArgs::fb_host), host view
     int32_t* fb_dev = nullptr;    // the same, device view
-    int ovf_slot = 0;
     int32_t fb_seq = 0;           // sequence number of the last fused launch
     int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
     long long tile_key = -1;      // ws, hs, bitmap words, colour of the current tile configuration
@@ -694,8 +693,6 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
     for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
     a.ovf_list = c->ovf_list.p;
     a.ovf_ctr = c->ovf_ctr.p;
-    a.ovf_slot = c->ovf_slot;
-    c->ovf_slot ^= 1;
     a.win_hist = c->win_hist.p;
     a.fb_host = c->fb_dev;
     a.fb_seq = ++c->fb_seq;

@@ -88,11 +88,11 @@ struct FusedArgs {
     float colour_thr;           // color_distance_threshold
     // sample windows ("Pose windows"): the z-sample tile in LDS holds `tcap` samples; a pose
     // whose window is larger is appended to ovf_list and scored by the overflow launch (tile = ws * hs).
-    // ovf_ctr[ovf_slot] counts the list; the overflow launch zeroes ovf_ctr[1 - ovf_slot] for the next call.
+    // ovf_ctr[0] counts the list, ovf_ctr[1] the finished overflow workgroups; the overflow launch returns
+    // both to 0
     int32_t tcap;
     int32_t* ovf_list;
     int32_t* ovf_ctr;
-    int32_t ovf_slot;
     // window-size histogram (bin b: windows of at most hist_edge[b] samples, the last bin the rest),
     // published by the overflow launch to fb_host (mapped host memory) and reset there
     int32_t hist_edge[kTileTiers];

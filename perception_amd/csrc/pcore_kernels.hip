@@ -750,20 +750,24 @@ __global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
 #pragma unroll
         for (int t = 0; t < kTileTiers; t++) b += tn > a.hist_edge[t] ? 1 : 0;
         atomicAdd(&a.win_hist[b], 1);
-        if (tn > a.tcap) a.ovf_list[atomicAdd(&a.ovf_ctr[a.ovf_slot], 1)] = pose;
+        if (tn > a.tcap) {
+            const int at = atomicAdd(&a.ovf_ctr[0], 1);
+            if (at < a.num_poses) a.ovf_list[at] = pose;
+        }
     }
     if (tn > a.tcap) return;
     fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
 }
 
 // Overflow launch: the poses fused_cost_kernel deferred, grid-stride over the list, LDS tile of the whole
-// sampled image.  Workgroup 0 also publishes the window histogram to the host, resets it, and zeroes the
-// other list counter (the one the next call counts with).
+// sampled image.  Workgroup 0 also publishes the window histogram to the host and resets it; the last
+// workgroup to finish returns the list counter to 0 (every workgroup has read it by then), so consecutive
+// launches -- and replays of a captured graph -- start from an empty list.
 template <int STRIDE, bool COLOUR = false>
 __global__ void __launch_bounds__(kThreads) fused_cost_ovf_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const FusedSmem sm = carve_smem(smem_raw, a.ws * a.hs, a.bitmap_words, COLOUR);
-    const int n = min(__builtin_amdgcn_readfirstlane(a.ovf_ctr[a.ovf_slot]), a.num_poses);
+    const int n = min(__builtin_amdgcn_readfirstlane(a.ovf_ctr[0]), a.num_poses);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int b = 0; b <= kTileTiers; b++) {
             a.fb_host[b] = a.win_hist[b];
@@ -772,7 +776,6 @@ __global__ void __launch_bounds__(kThreads) fused_cost_ovf_kernel(FusedArgs a) {
         a.fb_host[kTileTiers + 1] = n;
         // no system fence: the host may read a torn set, which only steers the next tile choice
         a.fb_host[kTileTiers + 2] = a.fb_seq;
-        a.ovf_ctr[1 - a.ovf_slot] = 0;
     }
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int pose = __builtin_amdgcn_readfirstlane(a.ovf_list[i]);
@@ -784,6 +787,13 @@ __global__ void __launch_bounds__(kThreads) fused_cost_ovf_kernel(FusedArgs a) {
                                                                   : SampleWin{0, 0, 0, 0};
         fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
         __syncthreads();  // the next pose re-initialises the LDS
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&a.ovf_ctr[1], 1) == (int)gridDim.x - 1) {
+            a.ovf_ctr[0] = 0;
+            a.ovf_ctr[1] = 0;
+        }
     }
 }
 

@@ -237,6 +237,36 @@ def test_window_tiles_any_tier(one_object, tier, monkeypatch):
     assert np.array_equal(dbg.cpu().numpy(), full[:, ::s, ::s])
 
 
+def test_graph_replay_matches_oracle(one_object):
+    """PoseCore.capture_evaluate: the captured launches (window + overflow kernels, HIP graph) re-score new
+    poses written in place into the captured tensor, with the oracle's costs, replay after replay (the
+    overflow list counter returns to 0 inside the graph)."""
+    case, core, t = one_object
+    sc = case.scene
+    s = case.stride
+    n = 32
+    dev = t["poses"].device
+    edge = init_from_eigen_batch(_edge_pose_batch())
+    batches = [case.poses[:n], np.concatenate([edge, case.poses[40:40 + n - len(edge)]]), case.poses[n:2 * n]]
+    poses = torch.from_numpy(batches[0]).to(dev).clone()
+    pm = torch.zeros(n, dtype=torch.int32, device=dev)
+    pl = torch.zeros(n, dtype=torch.int32, device=dev)
+    tot = torch.full((n,), float(case.pose_obs_total[0]), device=dev)
+    replay, (rc, oc, df) = core.capture_evaluate(poses, pm, pl, tot, cost_type=2, stride=s)
+    for p16 in batches + batches[::-1]:
+        poses.copy_(torch.from_numpy(p16))
+        replay()
+        torch.cuda.synchronize()
+        orc, ooc, odf = oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, p16, np.zeros(n, np.int32),
+                                        np.zeros(n, np.int32), sc.width, sc.height, sc.proj, sc.src_depth_cm,
+                                        sc.mask, 1.0, s, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz,
+                                        case.label_start, case.label_end,
+                                        np.full(n, case.pose_obs_total[0], np.float32), 2, True, 0.01)
+        assert _bits_equal(rc.cpu().numpy(), orc)
+        assert _bits_equal(oc.cpu().numpy(), ooc)
+        assert _bits_equal(df.cpu().numpy(), odf)
+
+
 def test_empty_batch_and_errors(one_object):
     case, core, t = one_object
     dev = t["poses"].device

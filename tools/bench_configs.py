@@ -128,6 +128,12 @@ def run_c1(steps, warmup, stride=4):
         print(json.dumps({"config": "C1", "poses": n, "models": 1, "width": W, "height": H, "stride": stride,
                           "icp": icp, "s_per_step": dt, "poses_per_s": n / dt, "observed_points": int(xyz.shape[0])}),
               flush=True)
+    # the launch-bound render + score as a captured HIP graph (PoseCore.capture_evaluate)
+    replay, _ = core.capture_evaluate(poses, pm, None, tot, cost_type=0, stride=stride, sensor_resolution=0.0075)
+    dt = timed(replay, steps, warmup)
+    print(json.dumps({"config": "C1", "poses": n, "models": 1, "width": W, "height": H, "stride": stride,
+                      "icp": False, "graph": True, "s_per_step": dt, "poses_per_s": n / dt,
+                      "observed_points": int(xyz.shape[0])}), flush=True)
 
 
 def main():
