@@ -37,6 +37,41 @@ def _bits(a):
     return np.asarray(a, np.float32).view(np.uint32)
 
 
+def _oracle_poses(w, poses, pm, tot):
+    """The oracle's costs of arbitrary poses (16-float rows) against the workload's scene."""
+    sc = w.scene
+    xyz = w.obs_xyz.cpu().numpy()
+    lab = w.obs_label.cpu().numpy()
+    order = np.argsort(lab, kind="stable")
+    oxyz, olab = xyz[order], lab[order]
+    nl = int(olab.max()) + 1
+    ls = np.array([np.searchsorted(olab, L, "left") for L in range(nl)], np.int32)
+    le = np.array([np.searchsorted(olab, L, "right") for L in range(nl)], np.int32)
+    return oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, poses, pm, pm, sc.width, sc.height, sc.proj,
+                           sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, ls, le,
+                           tot, 2, True, 0.01)
+
+
+def _random_poses(rng, n):
+    """Uniform random rotations; translations spread from behind the camera through the near plane to far
+    away and off screen, with a quarter of them close to the camera (big or whole-image windows)."""
+    q = rng.standard_normal((n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    w_, x, y, z = q.T
+    R = np.stack([np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w_ * z), 2 * (x * z + w_ * y)], -1),
+                  np.stack([2 * (x * y + w_ * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w_ * x)], -1),
+                  np.stack([2 * (x * z - w_ * y), 2 * (y * z + w_ * x), 1 - 2 * (x * x + y * y)], -1)], 1)
+    T = np.zeros((n, 4, 4))
+    T[:, :3, :3] = R
+    T[:, 3, 3] = 1.0
+    t = np.stack([rng.uniform(-0.6, 0.6, n), rng.uniform(-0.45, 0.45, n), rng.uniform(-0.3, 2.5, n)], -1)
+    near = rng.random(n) < 0.25
+    t[near, 2] = rng.uniform(-0.05, 0.2, near.sum())
+    t[near, :2] *= 0.2
+    T[:, :3, 3] = t
+    return T
+
+
 @pytest.fixture(scope="module")
 def c2():
     w = workloads.build(poses_per_model=10000)
@@ -84,7 +119,8 @@ def test_c2_gt_pose_wins_and_selection_matches_oracle_rule(c2):
 
 
 def test_c5_1280x720_subset_bit_exact_vs_oracle():
-    """C5's camera (1280x720, 57.6 KB LDS z-samples per pose) on a 2,000-pose batch."""
+    """C5's camera (1280x720: 57.6 KB of whole-image z-samples, windows of ~1,600 samples) on a 2,000-pose
+    batch."""
     w = workloads.build(poses_per_model=2000, cam=syn.CAM_1280)
     rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
     rc, oc, df = rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy()
@@ -112,3 +148,38 @@ def test_c4_21_models_selection_bit_exact_vs_oracle():
     orc, ooc, _ = _oracle_subset(w, sub)
     assert np.array_equal(_bits(rc[sub]), _bits(orc))
     assert np.array_equal(_bits(oc[sub]), _bits(ooc))
+
+
+@pytest.mark.parametrize("cam,tier", [("640", "auto"), ("640", "0"), ("640", "99"), ("1280", "auto")])
+def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, monkeypatch):
+    """3,000 random poses of three models (random rotations; behind, across and near the camera plane, off
+    screen, far): every pose's costs bit-exact against the oracle with the tile tier chosen from the window
+    histogram, forced to the smallest tile (most poses overflow to the whole-image launch) and forced to the
+    whole image -- the conservative pose windows never drop a fragment; at 640x480 and at C5's 1280x720.
+    For 200 of them the sampled z-buffers equal the full-frame render."""
+    from perception_amd.model import init_from_eigen_batch
+    if tier != "auto":
+        monkeypatch.setenv("PCORE_FUSED_TIER", tier)
+    w = workloads.build(names=["003_cracker_box", "005_tomato_soup_can", "024_bowl"], poses_per_model=10,
+                        cam=syn.CAM_640 if cam == "640" else syn.CAM_1280)
+    rng = np.random.default_rng(11)
+    n = 3000
+    p16 = init_from_eigen_batch(_random_poses(rng, n))
+    pm = rng.integers(0, w.num_models, n).astype(np.int32)
+    tot = np.bincount(w.obs_label.cpu().numpy(), minlength=w.num_models).astype(np.float32)[pm]
+    dev = w.poses.device
+    poses, pmt, tott = torch.from_numpy(p16).to(dev), torch.from_numpy(pm).to(dev), torch.from_numpy(tot).to(dev)
+    for _ in range(2):  # the second call runs with the tier the first call's histogram picks
+        rc, oc, df = w.core.evaluate(poses, pmt, pmt, tott, stride=w.stride)
+    orc, ooc, odf = _oracle_poses(w, p16, pm, tot)
+    rc, oc, df = rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy()
+    bad = np.nonzero((_bits(rc) != _bits(orc)) | (_bits(oc) != _bits(ooc)) | (_bits(df) != _bits(odf)))[0]
+    assert len(bad) == 0, f"{len(bad)} poses differ, e.g. {bad[:5]}"
+    assert (rc >= 0).sum() > 100 and (rc < 0).sum() > 100  # both visible and empty renders are exercised
+    m = 200
+    s = w.stride
+    hs, ws = (w.scene.height + s - 1) // s, w.scene.width // s
+    dbg = torch.full((m, hs, ws), -7, dtype=torch.int32, device=dev)
+    w.core.evaluate(poses[:m], pmt[:m], pmt[:m], tott[:m], stride=s, dbg_zs=dbg)
+    full = w.core.render(poses[:m], pmt[:m], pmt[:m]).cpu().numpy()
+    assert np.array_equal(dbg.cpu().numpy(), full[:, ::s, ::s])
