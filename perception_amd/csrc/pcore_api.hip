@@ -690,6 +690,8 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
     a.ovf_grid = (int)std::min<double>(kOvfGrid, 2.0 * c->ovf_frac * num_poses + 16.0);
     // tier kTileTiers (A/B knob only): the whole image
     a.tcap = c->tile_tier < kTileTiers && edge[c->tile_tier] > 0 ? edge[c->tile_tier] : nsamp;
+    if (const char* env = getenv("PCORE_FUSED_TCAP"))  // test knob: a tile of this many samples (most poses overflow)
+        a.tcap = std::min(std::max(atoi(env), 1), nsamp);
     for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
     a.ovf_list = c->ovf_list.p;
     a.ovf_ctr = c->ovf_ctr.p;

@@ -150,15 +150,18 @@ def test_c4_21_models_selection_bit_exact_vs_oracle():
     assert np.array_equal(_bits(oc[sub]), _bits(ooc))
 
 
-@pytest.mark.parametrize("cam,tier", [("640", "auto"), ("640", "0"), ("640", "99"), ("1280", "auto")])
+@pytest.mark.parametrize("cam,tier", [("640", "auto"), ("640", "0"), ("640", "99"), ("640", "tcap64"),
+                                      ("1280", "auto")])
 def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, monkeypatch):
     """3,000 random poses of three models (random rotations; behind, across and near the camera plane, off
     screen, far): every pose's costs bit-exact against the oracle with the tile tier chosen from the window
-    histogram, forced to the smallest tile (most poses overflow to the whole-image launch) and forced to the
-    whole image -- the conservative pose windows never drop a fragment; at 640x480 and at C5's 1280x720.
+    histogram, forced to the smallest tier, to a 64-sample tile (nearly every pose overflows to the
+    whole-image launch) and to the whole image -- the conservative pose windows never drop a fragment; at 640x480 and at C5's 1280x720.
     For 200 of them the sampled z-buffers equal the full-frame render."""
     from perception_amd.model import init_from_eigen_batch
-    if tier != "auto":
+    if tier == "tcap64":
+        monkeypatch.setenv("PCORE_FUSED_TCAP", "64")  # nearly every pose takes the overflow launch
+    elif tier != "auto":
         monkeypatch.setenv("PCORE_FUSED_TIER", tier)
     w = workloads.build(names=["003_cracker_box", "005_tomato_soup_can", "024_bowl"], poses_per_model=10,
                         cam=syn.CAM_640 if cam == "640" else syn.CAM_1280)

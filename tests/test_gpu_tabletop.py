@@ -63,8 +63,13 @@ def test_tabletop_localization_matches_oracle(cylinder):
     assert len(res) >= 1
 
 
-def test_tabletop_colour_cost_matches_oracle():
-    """cost_type 1: the colour id pass (nearest fragment's triangle) and the CIEDE2000 gate, bit-exact."""
+@pytest.mark.parametrize("tile", ["auto", "tcap64"])
+def test_tabletop_colour_cost_matches_oracle(tile, monkeypatch):
+    """cost_type 1: the colour id pass (nearest fragment's triangle) and the CIEDE2000 gate, bit-exact -- with
+    the chosen LDS tile and with a 64-sample tile that sends nearly every pose through the overflow launch
+    (the colour ids are indexed within the pose's tile)."""
+    if tile == "tcap64":
+        monkeypatch.setenv("PCORE_FUSED_TCAP", "64")
     names, placements, sc = _scene(colors=[(200, 40, 30), (30, 60, 190)])
     table = TableParams(x_min=0.52, x_max=0.68, y_min=-0.16, y_max=0.16, table_height=0.7, res=0.04)
     bank = {n: ModelMetaData(n, model=sc.bank.models[i]) for i, n in enumerate(names)}
@@ -87,14 +92,16 @@ def test_tabletop_colour_cost_matches_oracle():
     assert np.array_equal(g_rc.view(np.uint32), rc.view(np.uint32))
     assert np.array_equal(g_oc.view(np.uint32), oc.view(np.uint32))
     assert np.array_equal(g_df.view(np.uint32), df.view(np.uint32))
+    bc, bi = oracle.select(rc, oc, pm, len(names))
+    got = {m: (cost, idx) for m, cost, idx, _ in res}
+    for m in range(len(names)):
+        if bi[m] >= 0:
+            assert got[m] == (int(bc[m]), int(bi[m]))
+    if tile != "auto":
+        return
     # the colour gate matters: a wrongly coloured model explains nothing near the red box
     rc_depth, _, _ = oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, mats, pm, None, sc.width, sc.height,
                                      sc.proj, src_cm, None, rec.params.gpu_occlusion_threshold, rec.params.gpu_stride,
                                      sc.cx, sc.cy, sc.fx, sc.fy, 100.0, rec.obs_xyz_host, None, None, tot, 0, True,
                                      rec.params.sensor_resolution)
     assert (rc > rc_depth).any()
-    bc, bi = oracle.select(rc, oc, pm, len(names))
-    got = {m: (cost, idx) for m, cost, idx, _ in res}
-    for m in range(len(names)):
-        if bi[m] >= 0:
-            assert got[m] == (int(bc[m]), int(bi[m]))
