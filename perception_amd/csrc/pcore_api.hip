@@ -74,6 +74,9 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_count;
     DevBuf<double> icp_cov;
     DevBuf<int32_t> icp_counter;
+    DevBuf<uint32_t> icp_order_keys;  // 2 x chunk keys (in, out)
+    DevBuf<int32_t> icp_order_idx;    // 2 x chunk indices (in, out = GicpArgs::pose_order)
+    DevBuf<unsigned char> icp_order_temp;
     // colour gate (cost_type 1)
     DevBuf<uint32_t> mtri_orig;   // original triangle of every meshlet triangle
     DevBuf<float4> tri_lab;       // Lab per original triangle
@@ -333,7 +336,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->mtri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part);
     delete c;
@@ -901,6 +904,10 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, dev_reserve(c->icp_count, (size_t)chunk));
     HIPC(c, dev_reserve(c->icp_cov, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 1));
+    HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
+    HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
+    const size_t order_temp = gicp_order_temp_bytes(chunk);
+    HIPC(c, dev_reserve(c->icp_order_temp, order_temp));
     FusedArgs a;
     fill_fused_args(c, p, a);
     GicpArgs g{};
@@ -939,6 +946,12 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         HIPC(c, launch_render_cloud(a, s));
         HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
         g.pose_base = base;
+        g.pose_order = nullptr;
+        if (!getenv("PCORE_GICP_INDEX_ORDER")) {  // A/B knob: the queue in index order
+            HIPC(c, launch_gicp_order(g, n, c->icp_order_keys.p, c->icp_order_keys.p + chunk, c->icp_order_idx.p,
+                                      c->icp_order_idx.p + chunk, c->icp_order_temp.p, order_temp, s));
+            g.pose_order = c->icp_order_idx.p + chunk;
+        }
         HIPC(c, launch_gicp(g, n, s));
     }
     // re-render and re-score the adjusted poses (renderer.cu:1757-1907)

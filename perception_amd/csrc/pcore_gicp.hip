@@ -15,6 +15,8 @@
 //                      J^T M e, wave shuffle-down tree, one-lane 6x6 LDLT and update, then
 //                      concatenate_transforms (renderer.cu:1412-1429).
 #include "pcore_internal.h"
+
+#include <hipcub/hipcub.hpp>
 #include "pcore_gicp_math.h"
 
 #include <algorithm>
@@ -577,7 +579,10 @@ gicp_kernel(GicpArgs g, int num_poses) {
     GPROF_DECL;
     for (;;) {
         group_sync<WPP>();  // the previous pose's reads of the shared state are done
-        if (tid == 0) sPose = atomicAdd(g.work_counter, 1);
+        if (tid == 0) {
+            const int q = atomicAdd(g.work_counter, 1);
+            sPose = (g.pose_order && q < num_poses) ? g.pose_order[q] : q;
+        }
         group_sync<WPP>();
         const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
         if (pose >= num_poses) break;
@@ -700,7 +705,10 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     for (;;) {
         __syncthreads();
-        if (tid == 0) sPose = atomicAdd(g.work_counter, 1);
+        if (tid == 0) {
+            const int q = atomicAdd(g.work_counter, 1);
+            sPose = (g.pose_order && q < num_poses) ? g.pose_order[q] : q;
+        }
         __syncthreads();
         const int pose = __builtin_amdgcn_readfirstlane(sPose);
         if (pose >= num_poses) break;
@@ -807,6 +815,38 @@ extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
     return e == hipSuccess ? 0 : 1;
 }
 #endif
+
+// predicted cost of one GICP iteration of a pose: source points x targets of its segment (the scan)
+__global__ void gicp_cost_key_kernel(GicpArgs g, int n, uint32_t* keys, int32_t* idx) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int seg = g.whole_seg;
+    if (g.pose_label) {
+        const int pl = g.pose_label[g.pose_base + i];
+        seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
+    }
+    const unsigned long long nt = seg >= 0 ? (unsigned long long)(g.seg_hi[seg] - g.seg_lo[seg]) : 0ull;
+    const unsigned long long c = (unsigned long long)max(g.src_count[i], 0) * nt;
+    keys[i] = (uint32_t)min(c >> 4, 0xffffffffull);
+    idx[i] = i;
+}
+
+size_t gicp_order_temp_bytes(int n) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                       (const int32_t*)nullptr, (int32_t*)nullptr, n);
+    return bytes;
+}
+
+hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32_t* keys_out, int32_t* idx_in,
+                             int32_t* order_out, void* temp, size_t temp_bytes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gicp_cost_key_kernel, dim3((n + 255) / 256), dim3(256), 0, s, g, n, keys_in, idx_in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, keys_in, keys_out, idx_in, order_out, n, 0,
+                                                        32, s);
+}
 
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;

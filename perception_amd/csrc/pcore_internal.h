@@ -125,6 +125,9 @@ struct GicpArgs {
     int32_t max_iter;
     double rot_eps, trans_eps;
     int32_t* work_counter;    // device int, zeroed by launch_gicp (persistent-wave pose queue)
+    // queue order (chunk-local pose indices, nullable = index order): longest first, by the predicted cost of
+    // an iteration (source points x segment targets), so the long serial chains start early
+    const int32_t* pose_order;
     // neighbour grids of the segments (grids[seg], same indices as seg_lo / seg_hi): segments larger than
     // kGridNNMin targets take the exact grid search instead of the LDS scan
     const LabelGrid* grids;
@@ -151,6 +154,12 @@ hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_hos
                                    int num_segs, int first_grid, const LabelGrid* grids, const int32_t* cell_start,
                                    const float4* grid_pts, int k, double* cov_out, hipStream_t s);
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s);
+// scratch of launch_gicp_order: 4 arrays of n 32-bit words + the radix sort's temporary storage
+size_t gicp_order_temp_bytes(int n);
+// g.pose_order for a chunk of n poses whose clouds are rendered (g.src_count): chunk-local indices sorted by
+// descending src_count x segment size
+hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32_t* keys_out, int32_t* idx_in,
+                             int32_t* order_out, void* temp, size_t temp_bytes, hipStream_t s);
 // pcore_metrics.hip
 int pose_dist_blocks(int n);
 hipError_t launch_pose_distances(const float* pts, int n, const double* T_gt, const double* T_est, int pairs,
