@@ -188,14 +188,19 @@ def write_poses_txt(path: str, poses_xyz_qxyzw: np.ndarray, decimals: int = 4):
 
 
 def read_poses_txt(path: str) -> np.ndarray:
-    """GenerateSuccessorStates (search_env.cpp:7098-7130): split on ' ', std::stod each field."""
-    rows = []
+    """GenerateSuccessorStates (search_env.cpp:7098-7130): split on ' ', std::stod each field; the first 7
+    fields of each line, up to the first empty line.  Files of exactly 7 single-space-separated fields per
+    line (what write_poses_txt and the reference's scripts produce) are parsed in one pass; anything else
+    line by line."""
     with open(path) as f:
-        for line in f:
-            line = line.rstrip("\n")
-            if not line:
-                break  # getline() stops producing poses at the end; an empty line would fail stod
-            rows.append([float(v) for v in line.split(" ")[:7]])
+        text = f.read()
+    lines = text.split("\n")
+    end = next((i for i, ln in enumerate(lines) if not ln), len(lines))
+    lines = lines[:end]
+    fields = " ".join(lines).split(" ")
+    if lines and len(fields) == 7 * len(lines) and all(ln.count(" ") == 6 for ln in lines):
+        return np.array(fields, dtype=np.float64).reshape(-1, 7)
+    rows = [[float(v) for v in ln.split(" ")[:7]] for ln in lines]
     return np.asarray(rows, np.float64).reshape(-1, 7)
 
 

@@ -101,6 +101,44 @@ def matrix_to_quat_xyzw(R: np.ndarray) -> np.ndarray:
     return np.array([x, y, z, w])
 
 
+def quat_xyzw_to_matrix_batch(q: np.ndarray) -> np.ndarray:
+    """quat_xyzw_to_matrix over (N, 4) quaternions: the same float64 operations per element."""
+    q = np.asarray(q, dtype=np.float64).reshape(-1, 4)
+    x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    n = np.sqrt(x * x + y * y + z * z + w * w)
+    x, y, z, w = x / n, y / n, z / n, w / n
+    R = np.empty((len(q), 3, 3))
+    R[:, 0, 0] = 1 - 2 * (y * y + z * z)
+    R[:, 0, 1] = 2 * (x * y - z * w)
+    R[:, 0, 2] = 2 * (x * z + y * w)
+    R[:, 1, 0] = 2 * (x * y + z * w)
+    R[:, 1, 1] = 1 - 2 * (x * x + z * z)
+    R[:, 1, 2] = 2 * (y * z - x * w)
+    R[:, 2, 0] = 2 * (x * z - y * w)
+    R[:, 2, 1] = 2 * (y * z + x * w)
+    R[:, 2, 2] = 1 - 2 * (x * x + y * y)
+    return R
+
+
+def pose_matrix_batch(translations: np.ndarray, quats_xyzw: np.ndarray) -> np.ndarray:
+    """pose_matrix over N poses: (N, 4, 4)."""
+    t = np.asarray(translations, dtype=np.float64).reshape(-1, 3)
+    T = np.zeros((len(t), 4, 4))
+    T[:, :3, :3] = quat_xyzw_to_matrix_batch(quats_xyzw)
+    T[:, :3, 3] = t
+    T[:, 3, 3] = 1.0
+    return T
+
+
+def chain_matmul_batch(A: np.ndarray, T: np.ndarray, B: np.ndarray) -> np.ndarray:
+    """A @ T[i] @ B[i] for every i, each product summed over k in index order as a plain 4x4 matmul loop
+    ((a0 b0 + a1 b1) + a2 b2) + a3 b3, independent of BLAS blocking and thread count."""
+    def mm(X, Y):
+        return (((X[..., :, 0, None] * Y[..., None, 0, :] + X[..., :, 1, None] * Y[..., None, 1, :])
+                 + X[..., :, 2, None] * Y[..., None, 2, :]) + X[..., :, 3, None] * Y[..., None, 3, :])
+    return mm(mm(np.broadcast_to(A, T.shape), T), B)
+
+
 def pose_matrix(translation: Sequence[float], quat_xyzw: Sequence[float]) -> np.ndarray:
     """ContPose::GetTransform (object_state.cpp:83-97): Translation3d(x,y,z) * normalised quaternion."""
     T = np.eye(4)

@@ -28,7 +28,8 @@ from . import io as pio
 from ._native import COST_DEPTH_6DOF, ICP_K, ICP_MAX_ITER, ICP_ROT_EPS, ICP_TRANS_EPS, PCORE_KEY_NONE
 from .core import PoseCore, decode_keys
 from .distributed import allreduce_min_keys, shard_range
-from .model import Model, compute_proj, init_from_eigen_batch, matrix_to_quat_xyzw, pose_matrix, to_eigen
+from .model import (Model, chain_matmul_batch, compute_proj, init_from_eigen_batch, matrix_to_quat_xyzw, pose_matrix,
+                    pose_matrix_batch, to_eigen)
 
 # cam_to_body (search_env.cpp:1536-1539)
 CAM_TO_BODY = np.array([[0, 0, 1, 0], [-1, 0, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1]], np.float64)
@@ -133,10 +134,12 @@ def preprocessing_transform(model: Model, flipped: bool = False, mesh_in_mm: boo
 
 
 def _dims(model: Model):
-    v = model.vertices()
+    """Bounding-box extents of the model's vertices (min / max over the triangle corners: the same as over
+    the unique vertices, without sorting them)."""
+    v = model.tris.reshape(-1, 3)
     if len(v) == 0:
         return np.zeros(3)
-    return v.max(0) - v.min(0)
+    return v.max(0).astype(np.float64) - v.min(0).astype(np.float64)
 
 
 class ObjectRecognizer:
@@ -209,11 +212,22 @@ class ObjectRecognizer:
         need = self.params.min_neighbor_points_for_valid_pose
         if len(seg) < need:
             return np.zeros(len(translations), bool)
+        # float64 squared distances (dx^2 + dy^2) + dz^2 on the device, chunked -- elementwise eager ops,
+        # the same IEEE operations in the same order as a host evaluation
         out = np.zeros(len(translations), bool)
-        for a in range(0, len(translations), 4096):
-            t = translations[a:a + 4096]
-            d2 = ((t[:, None, :] - seg[None, :, :]) ** 2).sum(-1)
-            out[a:a + 4096] = (d2 <= rad * rad).sum(1) >= need
+        sg = torch.from_numpy(np.ascontiguousarray(seg)).to(self.device)
+        tt = torch.from_numpy(np.ascontiguousarray(translations, dtype=np.float64)).to(self.device)
+        r2 = rad * rad
+        step = max(1, (1 << 24) // max(len(seg), 1))
+        for a in range(0, len(translations), step):
+            t = tt[a:a + step]
+            dx = t[:, 0:1] - sg[None, :, 0]
+            d2 = dx * dx
+            dy = t[:, 1:2] - sg[None, :, 1]
+            d2 = d2 + dy * dy
+            dz = t[:, 2:3] - sg[None, :, 2]
+            d2 = d2 + dz * dz
+            out[a:a + step] = ((d2 <= r2).sum(1) >= need).cpu().numpy()
         return out
 
     def generate_successor_states(self, inp: RecognitionInput):
@@ -247,12 +261,16 @@ class ObjectRecognizer:
         return np.array([seg[min(s[1], len(seg) - 1)] for s in states], np.float32)
 
     def _pose_in_cam(self, states) -> np.ndarray:
-        """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576)."""
+        """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576): inv(cam_z_front) * T(state) *
+        preprocess, vectorised over the states (model.chain_matmul_batch: index-order 4x4 products)."""
         cam_z_front = self.camera_pose @ CAM_TO_BODY
         cam_matrix = np.linalg.inv(cam_z_front)
-        mats = np.empty((len(states), 4, 4))
-        for i, (mid, _, p) in enumerate(states):
-            mats[i] = cam_matrix @ pose_matrix(p[:3], p[3:7]) @ self.preprocess[mid]
+        if not states:
+            return init_from_eigen_batch(np.zeros((0, 4, 4)), 100)
+        P = np.stack([s[2] for s in states]).astype(np.float64)
+        mids = np.fromiter((s[0] for s in states), dtype=np.int64, count=len(states))
+        pre = np.stack(self.preprocess)[mids]
+        mats = chain_matmul_batch(cam_matrix, pose_matrix_batch(P[:, :3], P[:, 3:7]), pre)
         return init_from_eigen_batch(mats, 100)
 
     # -- ComputeGreedyRenderPoses (search_env.cpp:2462-2651) ----------------------------------------

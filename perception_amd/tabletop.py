@@ -196,11 +196,17 @@ class TabletopRecognizer(ObjectRecognizer):
         return out
 
     def _pose_in_cam(self, states) -> np.ndarray:
-        from .model import init_from_eigen_batch
+        """The 3-DoF states' poses in the camera, vectorised (yaw quaternions with math.sin / math.cos per
+        state, as yaw_pose_matrix; index-order 4x4 products, model.chain_matmul_batch)."""
+        from .model import chain_matmul_batch, init_from_eigen_batch, pose_matrix_batch
         cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
-        mats = np.empty((len(states), 4, 4))
-        for i, (mid, _, p) in enumerate(states):
-            mats[i] = cam_matrix @ yaw_pose_matrix(p[0], p[1], p[2], p[3]) @ self.preprocess[mid]
+        if not states:
+            return init_from_eigen_batch(np.zeros((0, 4, 4)), 100)
+        xyzy = np.array([(p[0], p[1], p[2], p[3]) for _, _, p in states], dtype=np.float64)
+        yaws = [normalize_angle_positive(float(y)) for y in xyzy[:, 3]]
+        q = np.array([(0.0, 0.0, math.sin(y / 2.0), math.cos(y / 2.0)) for y in yaws])
+        mids = np.fromiter((s[0] for s in states), dtype=np.int64, count=len(states))
+        mats = chain_matmul_batch(cam_matrix, pose_matrix_batch(xyzy[:, :3], q), np.stack(self.preprocess)[mids])
         return init_from_eigen_batch(mats, 100)
 
     def localize(self, model_names: Sequence[str], depth: np.ndarray, camera_pose: np.ndarray,

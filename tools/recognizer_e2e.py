@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""End-to-end ObjectRecognizer.localize_objects_greedy_render on a C3-sized input (5 objects, 10,000
+candidate poses each read from poses.txt), with and without GICP: wall time of the whole call (host state
+generation, pose building, observation setup, GPU search) next to the GPU-only stage times.  --loop-poses
+times the per-state Python pose building the recognizer used before (A/B)."""
+import argparse
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from perception_amd import io, synthetic as syn  # noqa: E402
+from perception_amd.model import init_from_eigen_batch, matrix_to_quat_xyzw, pose_matrix  # noqa: E402
+from perception_amd.recognizer import (CAM_TO_BODY, CameraIntrinsics, ModelMetaData, ObjectRecognizer,  # noqa: E402
+                                       PerchParams, RecognitionInput)
+
+
+def loop_pose_in_cam(self, states):
+    cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
+    mats = np.empty((len(states), 4, 4))
+    for i, (mid, _, p) in enumerate(states):
+        mats[i] = cam_matrix @ pose_matrix(p[:3], p[3:7]) @ self.preprocess[mid]
+    return init_from_eigen_batch(mats, 100)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--poses", type=int, default=10000)
+    ap.add_argument("--loop-poses", action="store_true")
+    a = ap.parse_args()
+    names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
+    rng = np.random.default_rng(syn.SEED)
+    from perception_amd import workloads
+    centers = workloads.object_centers(len(names))
+    gts = np.stack([syn.default_gt_pose(rng, c) for c in centers])
+    from tests.helpers import oracle_render_fn
+    sc = syn.make_scene(names, gts, oracle_render_fn, rng=rng)
+    root = tempfile.mkdtemp()
+    for k, name in enumerate(names):
+        P = syn.candidate_poses(gts[k][:3, 3], a.poses, rng, include=gts[k])
+        rows = np.array([np.concatenate([T[:3, 3], matrix_to_quat_xyzw(T[:3, :3])]) for T in P])
+        os.makedirs(os.path.join(root, name), exist_ok=True)
+        io.write_poses_txt(os.path.join(root, name, "poses.txt"), rows, decimals=6)
+    bank = {n: ModelMetaData(n, model=sc.bank.models[i]) for i, n in enumerate(names)}
+    cam = CameraIntrinsics(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy)
+    if a.loop_poses:
+        ObjectRecognizer._pose_in_cam = loop_pose_in_cam
+    for icp in (0, 1):
+        rec = ObjectRecognizer(bank, cam, PerchParams(icp_type=3 if icp else 0, gpu_batch_size=100000))
+        inp = RecognitionInput(names, sc.depth_raw, sc.mask, depth_factor=sc.depth_factor, rendered_root_dir=root,
+                               use_icp=icp)
+        rec.localize_objects_greedy_render(inp)  # warm-up (scratch, tiers)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = rec.localize_objects_greedy_render(inp)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        states = rec.generate_successor_states(inp)
+        t1 = time.perf_counter()
+        rec._pose_in_cam(states)
+        dp = time.perf_counter() - t1
+        print({"icp": icp, "states": len(states), "localize_s": round(dt, 4), "search_s": round(rec.last_stats.time, 4),
+               "icp_s": round(rec.last_stats.icp_time, 4), "pose_building_s": round(dp, 4),
+               "loop_poses": a.loop_poses, "found": len(res.model_names)}, flush=True)
+
+
+if __name__ == "__main__":
+    main()
