@@ -90,3 +90,28 @@ def test_reference_demo_depth_png_unprojects():
     sub = d[::8, ::8]
     assert len(xyz) == int((sub > 0).sum())
     assert np.allclose(np.sort(xyz[:, 2]), np.sort(sub[sub > 0].astype(np.float32) / np.float32(10000.0)))
+
+
+def test_read_poses_txt_edge_cases(tmp_path):
+    """One-pass parse for regular files, line-by-line otherwise: the first 7 fields of each line up to the
+    first empty line (search_env.cpp:7098-7130 getline + stod), CRLF endings, trailing spaces, extra fields."""
+    import numpy as np
+    from perception_amd import io
+
+    rng = np.random.default_rng(2)
+    R = rng.normal(size=(6, 7))
+    row = lambda r: " ".join(repr(float(v)) for v in r)  # noqa: E731
+    cases = {
+        "regular": ("\n".join(row(r) for r in R) + "\n", R),
+        "crlf": ("\r\n".join(row(r) for r in R) + "\r\n", R),
+        "trailing_space": ("\n".join(row(r) + " " for r in R) + "\n", R),
+        "extra_fields": ("\n".join(row(np.append(r, 9.0)) for r in R) + "\n", R),
+        "stops_at_empty_line": ("\n".join(row(r) for r in R[:3]) + "\n\n" + row(R[4]) + "\n", R[:3]),
+        "no_final_newline": ("\n".join(row(r) for r in R), R),
+        "empty": ("", np.zeros((0, 7))),
+    }
+    for name, (text, want) in cases.items():
+        p = tmp_path / f"{name}.txt"
+        p.write_text(text)
+        got = io.read_poses_txt(str(p))
+        assert got.shape == want.shape and np.array_equal(got, want), name
