@@ -510,7 +510,7 @@ void covariance_one(const float* xyz, int n, int i, int k, double* out6) {
 
 // per-point Gauss-Newton contribution: acc[0..20] = upper(H) row-major, [21..26] = b, [27] = error
 bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const double* cs, const float* tgt,
-                  const double* tcov, int nt, double acc[28]) {
+                  const double* tcov, int nt, double acc[pcore::gicpm::kTerms]) {
     const double s0 = (double)s[0], s1 = (double)s[1], s2 = (double)s[2];
     double q[3];
     for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
@@ -528,10 +528,10 @@ bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const
     const double Rm[3][3] = {{R[0][0], R[0][1], R[0][2]}, {R[1][0], R[1][1], R[1][2]}, {R[2][0], R[2][1], R[2][2]}};
     const double qa[3] = {q[0], q[1], q[2]};
     const double tj[3] = {(double)tgt[3 * (size_t)j + 0], (double)tgt[3 * (size_t)j + 1], (double)tgt[3 * (size_t)j + 2]};
-    double a28[28];
-    for (int v = 0; v < 28; v++) a28[v] = acc[v];
-    pcore::gicpm::contrib(Rm, qa, csa, tj, ct, a28);
-    for (int v = 0; v < 28; v++) acc[v] = a28[v];
+    double a27[pcore::gicpm::kTerms];
+    for (int v = 0; v < pcore::gicpm::kTerms; v++) a27[v] = acc[v];
+    pcore::gicpm::contrib(Rm, qa, csa, tj, ct, a27);
+    for (int v = 0; v < pcore::gicpm::kTerms; v++) acc[v] = a27[v];
     return true;
 }
 
@@ -585,19 +585,19 @@ int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* t
     double t[3] = {0.0, 0.0, 0.0};
     int it = 0;
     if (ns > 0 && nt > 0) {
-        std::vector<double> part((size_t)kGicpThreads * 28);
+        std::vector<double> part((size_t)kGicpThreads * pcore::gicpm::kTerms);
         for (it = 0; it < max_iter;) {
             std::fill(part.begin(), part.end(), 0.0);
             for (int i = 0; i < ns; i++)
                 gicp_contrib(R, t, src_xyz + (size_t)3 * i, src_cov + (size_t)6 * i, tgt_xyz, tgt_cov, nt,
-                             part.data() + (size_t)28 * (i % kGicpThreads));
+                             part.data() + (size_t)pcore::gicpm::kTerms * (i % kGicpThreads));
             // fixed reduction: per wave shuffle-down tree to lane 0, then the 4 waves in order
-            double tot[28];
-            for (int v = 0; v < 28; v++) {
+            double tot[pcore::gicpm::kTerms];
+            for (int v = 0; v < pcore::gicpm::kTerms; v++) {
                 double wsum[kGicpThreads / 64];
                 for (int w = 0; w < kGicpThreads / 64; w++) {
                     double lane[64];
-                    for (int l = 0; l < 64; l++) lane[l] = part[(size_t)28 * (w * 64 + l) + v];
+                    for (int l = 0; l < 64; l++) lane[l] = part[(size_t)pcore::gicpm::kTerms * (w * 64 + l) + v];
                     for (int off = 32; off > 0; off >>= 1)
                         for (int l = 0; l < off; l++) lane[l] = lane[l] + lane[l + off];
                     wsum[w] = lane[0];

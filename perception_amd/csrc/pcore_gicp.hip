@@ -449,7 +449,7 @@ __device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6
 // One point's Gauss-Newton contribution: the shared spec of pcore_gicp_math.h (the oracle calls the same
 // function), given the transformed point q, its correspondence tj and both covariances.
 __device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6],
-                                             float4 tj, const double (&ct)[6], double (&acc)[28]) {
+                                             float4 tj, const double (&ct)[6], double (&acc)[gicpm::kTerms]) {
     const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
     gicpm::contrib(R, q, cs, t3, ct, acc);
 }
@@ -501,7 +501,7 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
 // Lane-0 step of an iteration: LDLT of the reduced normal equations, the left update of (R, t) into RT and
 // fast_gicp's convergence test.  Returns 0 continue, 1 stop without update (H not positive definite),
 // 2 stop after the update.
-__device__ __forceinline__ int solve_update(const double (&acc)[28], const double (&R)[3][3], const double (&t)[3],
+__device__ __forceinline__ int solve_update(const double (&acc)[gicpm::kTerms], const double (&R)[3][3], const double (&t)[3],
                                         double* RT, double rot_eps, double trans_eps) {
     double d[6];
     if (!ldlt_solve6(acc, acc + 21, d)) return 1;
@@ -573,7 +573,7 @@ __global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(P
 gicp_kernel(GicpArgs g, int num_poses) {
     constexpr int NT = 64 * WPP;
     __shared__ double RT[12];
-    __shared__ double sPart[WPP][28];
+    __shared__ double sPart[WPP][gicpm::kTerms];
     __shared__ int sPose, sFlag;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     GPROF_DECL;
@@ -618,9 +618,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 for (int c = 0; c < 3; c++) R[r][c] = uniform_d(RT[3 * r + c]);
                 t[r] = uniform_d(RT[9 + r]);
             }
-            double acc[28];
+            double acc[gicpm::kTerms];
 #pragma unroll
-            for (int v = 0; v < 28; v++) acc[v] = 0.0;
+            for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
             // rounds of NT source points: point i -> thread i % NT, contributions added in point order
             for (int i0 = 0; i0 < ns; i0 += NT) {
                 GPROF_T(t_r0);
@@ -647,13 +647,13 @@ gicp_kernel(GicpArgs g, int num_poses) {
                     load_cov(tcov, j, ct);
                     gicp_contrib(R, q, cs, tgt[j], ct, acc);
                 }
-                GPROF_TD(t_r2, acc[27]);
+                GPROF_TD(t_r2, acc[gicpm::kTerms - 1]);
                 GPROF_ADD(0, t_r0, t_r1);
                 GPROF_ADD(1, t_r1, t_r2);
             }
-            GPROF_TD(t_b, acc[27]);
+            GPROF_TD(t_b, acc[gicpm::kTerms - 1]);
 #pragma unroll
-            for (int v = 0; v < 28; v++) {
+            for (int v = 0; v < gicpm::kTerms; v++) {
                 double x = acc[v];
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
@@ -662,19 +662,19 @@ gicp_kernel(GicpArgs g, int num_poses) {
             if constexpr (WPP > 1) {
                 if (lane == 0) {
 #pragma unroll
-                    for (int v = 0; v < 28; v++) sPart[wave][v] = acc[v];
+                    for (int v = 0; v < gicpm::kTerms; v++) sPart[wave][v] = acc[v];
                 }
                 __syncthreads();
                 if (tid == 0) {
 #pragma unroll
-                    for (int v = 0; v < 28; v++) {
+                    for (int v = 0; v < gicpm::kTerms; v++) {
                         double x = sPart[0][v];
                         for (int w = 1; w < WPP; w++) x = x + sPart[w][v];
                         acc[v] = x;
                     }
                 }
             }
-            GPROF_TD(t_c, acc[27]);
+            GPROF_TD(t_c, acc[gicpm::kTerms - 1]);
             if (tid == 0) sFlag = solve_update(acc, R, t, RT, g.rot_eps, g.trans_eps);
             group_sync<WPP>();
             const int flag = __builtin_amdgcn_readfirstlane(sFlag);
@@ -765,9 +765,9 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
             }
             __syncthreads();
             if (wave == 0) {
-                double acc[28];
+                double acc[gicpm::kTerms];
 #pragma unroll
-                for (int v = 0; v < 28; v++) acc[v] = 0.0;
+                for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
                 for (int i0 = 0; i0 < ns; i0 += 64) {
                     const int i = i0 + lane;
                     const int j = i < ns ? jbuf[i] : -1;
@@ -784,7 +784,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                     }
                 }
 #pragma unroll
-                for (int v = 0; v < 28; v++) {
+                for (int v = 0; v < gicpm::kTerms; v++) {
                     double x = acc[v];
 #pragma unroll
                     for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);

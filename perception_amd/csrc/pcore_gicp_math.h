@@ -32,10 +32,14 @@ PCORE_GHD void jt_mul(const double (&q)[3], const double (&v)[3], double (&o)[6]
     o[5] = -v[2];
 }
 
-// acc[0..20] += upper(J^T M J) row-major, acc[21..26] += J^T M e, acc[27] += e^T M e, for the point q with
-// correspondence tj, source covariance cs and target covariance ct (xx, xy, xz, yy, yz, zz).
+// Terms of the normal equations a point adds: the upper triangle of J^T M J and J^T M e.  (fast_gicp also
+// sums the error e^T M e; nothing in the step or the convergence test reads it, so it is not accumulated.)
+constexpr int kTerms = 27;
+
+// acc[0..20] += upper(J^T M J) row-major, acc[21..26] += J^T M e, for the point q with correspondence tj,
+// source covariance cs and target covariance ct (xx, xy, xz, yy, yz, zz).
 PCORE_GHD void contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6], const double (&tj)[3],
-                       const double (&ct)[6], double (&acc)[28]) {
+                       const double (&ct)[6], double (&acc)[kTerms]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
     double RC[3][3], A[3][3];
@@ -101,7 +105,6 @@ PCORE_UNROLL
     jt_mul(q, Me, g);
 PCORE_UNROLL
     for (int a = 0; a < 6; a++) acc[21 + a] += g[a];
-    acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
 }
 
 }  // namespace gicpm
