@@ -35,11 +35,14 @@ struct LabelGrid {
     int32_t pad1, pad2;
 };
 
-// tile tiers of the fused window launch: workgroups per CU 6, 5, 4, 3, 2 (the LDS tile that leaves room
-// for that many workgroups); the host picks the tier from the previous call's window histogram
-constexpr int kTileTiers = 5;
-constexpr int kTierWGs[kTileTiers] = {6, 5, 4, 3, 2};
-constexpr int kDefaultTier = 0;  // 6 workgroups per CU until a histogram is known
+// tile tiers of the fused window launch: workgroups per CU PCORE_TIER_MAX, ..., 3, 2 (the LDS tile that
+// leaves room for that many workgroups); the host picks the tier from the previous call's window histogram
+#ifndef PCORE_TIER_MAX
+#define PCORE_TIER_MAX 6
+#endif
+constexpr int kTileTiers = PCORE_TIER_MAX - 1;
+constexpr int tier_wgs(int t) { return PCORE_TIER_MAX - t; }
+constexpr int kDefaultTier = 0;  // the most workgroups per CU until a histogram is known
 
 struct FusedArgs {
     // batch
@@ -167,7 +170,7 @@ hipError_t launch_pose_distances(const float* pts, int n, const double* T_gt, co
 hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
 // LDS of one fused / cloud workgroup whose z-sample tile holds `tile_samples` samples
 size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour = false);
-// tile capacity (samples) of tier t: the largest tile that leaves room for kTierWGs[t] workgroups per CU
+// tile capacity (samples) of tier t: the largest tile that leaves room for tier_wgs(t) workgroups per CU
 // (capped at the whole sampled image)
 int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, size_t lds_per_cu);
 constexpr int kOvfGrid = 1024;  // most workgroups of the overflow launch (grid-stride over the list)

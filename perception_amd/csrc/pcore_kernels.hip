@@ -732,10 +732,34 @@ __device__ __forceinline__ void load_pose_rows(const float* poses, int pose, flo
 
 // Window launch: one workgroup per pose, LDS tile of a.tcap samples.  A pose whose window exceeds the tile
 // goes to the overflow list (its outputs are written by fused_cost_ovf_kernel, launched next).
+#ifdef PCORE_WG_TIMING
+// measurement build only (tools/wg_timeline.py): wall clock (100 MHz) at the start and end of every
+// fused_cost_kernel workgroup, indexed by pose
+__device__ unsigned long long pcore_wg_clock[2 * 1048576];
+extern "C" int pcore_debug_wg_clock(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcore_wg_clock), sizeof(unsigned long long) * 2 * (size_t)n);
+}
+#endif
+
+// register budget of the fused kernel: 7 waves per SIMD (72 VGPRs, 94 SGPRs) when a 7-workgroup tier exists
+#ifndef PCORE_FUSED_WAVES_PER_EU
+#define PCORE_FUSED_WAVES_PER_EU (PCORE_TIER_MAX > 6 ? PCORE_TIER_MAX : 1)
+#endif
 template <int STRIDE, bool COLOUR = false>
-__global__ void __launch_bounds__(kThreads) fused_cost_kernel(FusedArgs a) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PCORE_FUSED_WAVES_PER_EU)))
+fused_cost_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int pose = blockIdx.x;
+#ifdef PCORE_WG_TIMING
+    if (threadIdx.x == 0) pcore_wg_clock[2 * pose] = wall_clock64();
+    struct End {
+        int pose;
+        __device__ ~End() {
+            __syncthreads();
+            if (threadIdx.x == 0) pcore_wg_clock[2 * pose + 1] = wall_clock64();
+        }
+    } end_clock{pose};
+#endif
     const FusedSmem sm = carve_smem(smem_raw, a.tcap, a.bitmap_words, COLOUR);
     const int model = a.pose_model[pose];
     SampleWin sw = {0, 0, 0, 0};  // invalid model: nothing is rendered
@@ -873,9 +897,19 @@ hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// gfx950 allocates a workgroup's LDS in 1,280-byte granules (160 KiB = 128 of them), not the 512 bytes of
+// earlier CDNA parts: a census of resident fused_cost_kernel workgroups (tools/wg_timeline.py,
+// tools/lds_census.sh) found 27,136-byte tiles at 5 per CU and 32,768-byte ones at 4, but 26,880 and 32,000
+// bytes at 6 and 5.  PCORE_LDS_GRANULE overrides it (A/B only).
+constexpr size_t kLdsGranule = 1280;
+
 int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, size_t lds_per_cu) {
     const int nsamp = ws * hs;
-    const size_t per_wg = (lds_per_cu / kTierWGs[t]) & ~size_t(511);  // LDS is allocated in 512-byte blocks
+    static const size_t granule = [] {
+        const char* e = getenv("PCORE_LDS_GRANULE");
+        return (size_t)(e ? std::max(atoi(e), 4) : kLdsGranule);
+    }();
+    const size_t per_wg = (lds_per_cu / tier_wgs(t)) / granule * granule;
     const size_t fixed = fused_lds_bytes(0, bitmap_words, colour);
     if (per_wg <= fixed + 64) return 0;
     const int cap = (int)((per_wg - fixed) / 4) & ~3;
