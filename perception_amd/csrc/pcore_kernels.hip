@@ -33,7 +33,7 @@ constexpr int kWaves = kThreads / kWave;
 #ifndef PCORE_REC_CAP
 #define PCORE_REC_CAP 96
 #endif
-constexpr int kRecCap = PCORE_REC_CAP;  // per-wave ring of queued triangle records (flush above kRecCap - 64)
+constexpr int kRecCap = PCORE_REC_CAP;  // per-wave circular ring of queued triangle records (flushed 64 at a time)
 constexpr int64_t PCORE_KEY_NONE_DEV = 0x7fffffffffffffffLL;
 constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queued; larger ones are
                               // processed cooperatively by the whole wave
@@ -284,6 +284,14 @@ __device__ __forceinline__ Meshlet load_meshlet(const Meshlet* p, int m) {
     return Meshlet{v.x, v.y, v.z, v.w};
 }
 
+#ifdef PCORE_FLUSH_STATS
+// measurement build only: small-triangle flush batches, records, fragment tests, loop trips
+__device__ unsigned long long pcore_flush_stats[8];
+extern "C" int pcore_debug_flush_stats(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcore_flush_stats), sizeof(unsigned long long) * 8);
+}
+#endif
+
 template <int STRIDE, bool IDPASS = false>
 __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw,
                                              int32_t* cid = nullptr) {
@@ -313,15 +321,40 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     // bound that keeps the tile indexing in range whatever the input)
     const short2v wzero = {(short)sw.x0, (short)sw.y0};
     const short2v wlim = {(short)(sw.x0 + sw.nx - 1), (short)(sw.y0 + sw.ny - 1)};
-    int rec_count = 0;  // wave-uniform
+    // circular ring of queued small triangles: records [rec_head, rec_head + rec_count) modulo kRecCap;
+    // flushed 64 at a time, so that every fragment-test batch fills the wave (a partial batch only when an
+    // append would overflow the ring, and at the end)
+    int rec_head = 0, rec_count = 0;  // wave-uniform
 
     const int dbg = a.dbg_skip;
-    auto flush = [&](int count) {
+    auto ring_slot = [&](int i) { return i >= kRecCap ? i - kRecCap : i; };  // i < 2 kRecCap
+    auto flush = [&](int head, int count) {
         wave_sync();
         if (dbg & 1) return;
         for (int base = 0; base < count; base += kWave) {
-            const int j = base + lane;
-            if (j < count) {
+            const int j = ring_slot(head + min(base + lane, count - 1));
+#ifdef PCORE_FLUSH_STATS
+            {
+                const bool in = base + lane < count;
+                const TriRec rs = ring[j];
+                const int nxs = ((rs.meta >> 24) & 0xf) + 1, nys = ((rs.meta >> 28) & 0xf) + 1;
+                const int nks = in ? nxs * nys : 0;
+                int mx_ny = in ? nys : 0, mx_nx = in ? nxs : 0;
+                int sum = nks;
+                for (int o = 32; o > 0; o >>= 1) {
+                    mx_ny = max(mx_ny, __shfl_xor(mx_ny, o));
+                    mx_nx = max(mx_nx, __shfl_xor(mx_nx, o));
+                    sum += __shfl_xor(sum, o);
+                }
+                if (lane == 0) {
+                    atomicAdd(&pcore_flush_stats[0], 1ull);                             // 64-lane batches
+                    atomicAdd(&pcore_flush_stats[1], (unsigned long long)min(count - base, kWave));  // records
+                    atomicAdd(&pcore_flush_stats[2], (unsigned long long)sum);          // fragment tests
+                    atomicAdd(&pcore_flush_stats[3], (unsigned long long)(mx_ny * mx_nx));  // loop trips (upper)
+                }
+            }
+#endif
+            if (base + lane < count) {
                 const TriRec r = ring[j];
                 const uint32_t id = IDPASS ? ring_id[j] : 0u;
                 const int kx0 = r.meta & 0xfff, ky0 = (r.meta >> 12) & 0xfff;
@@ -432,6 +465,17 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             }
             // large triangles: whole-wave cooperative
             uint64_t big = __ballot(nk > kSmallK);
+#ifdef PCORE_FLUSH_STATS
+            {
+                const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(t < ml.nt);
+                if (lane == 0) {
+                    atomicAdd(&pcore_flush_stats[4], (unsigned long long)__popcll(big));
+                    atomicAdd(&pcore_flush_stats[5], (unsigned long long)__popcll(btouch));
+                    atomicAdd(&pcore_flush_stats[6], (unsigned long long)__popcll(blanes));
+                    atomicAdd(&pcore_flush_stats[7], 1ull);
+                }
+            }
+#endif
             while (big) {
                 const int j = __ffsll((unsigned long long)big) - 1;
                 big &= big - 1;
@@ -457,15 +501,23 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             // small triangles: queue into the wave's ring
             const bool qd = nk > 0 && nk <= kSmallK;
             const uint64_t bq = __ballot(qd);
+            const int nq = __popcll(bq);
+            if (rec_count + nq > kRecCap) {  // rare: more queued than the ring holds -> partial batch first
+                flush(rec_head, rec_count);
+                rec_head = 0;
+                rec_count = 0;
+            }
             if (qd) {
                 r.meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) | ((uint32_t)(ny - 1) << 28);
-                ring[rec_count + mbcnt64(bq)] = r;
-                if (IDPASS) ring_id[rec_count + mbcnt64(bq)] = oid;
+                const int slot = ring_slot(rec_head + rec_count + mbcnt64(bq));
+                ring[slot] = r;
+                if (IDPASS) ring_id[slot] = oid;
             }
-            rec_count += __popcll(bq);
-            if (rec_count > kRecCap - kWave) {
-                flush(rec_count);
-                rec_count = 0;
+            rec_count += nq;
+            while (rec_count >= kWave) {  // full batches only
+                flush(rec_head, kWave);
+                rec_head = ring_slot(rec_head + kWave);
+                rec_count -= kWave;
             }
         }
         wave_sync();  // vertex slots are rewritten by the next meshlet
@@ -476,7 +528,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         id0 = in0;
         id1 = in1;
     }
-    if (rec_count > 0) flush(rec_count);
+    if (rec_count > 0) flush(rec_head, rec_count);
 }
 
 // Conservative sample window of a pose ("Pose windows").  Lanes 0-7 of every wave project the
