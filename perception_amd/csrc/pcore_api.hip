@@ -908,7 +908,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
     const size_t order_temp = gicp_order_temp_bytes(chunk);
     HIPC(c, dev_reserve(c->icp_order_temp, order_temp));
-    FusedArgs a;
+    FusedArgs a{};
     fill_fused_args(c, p, a);
     GicpArgs g{};
     g.src = c->icp_cloud.p;
