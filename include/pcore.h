@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PCORE_ABI_VERSION 2
+#define PCORE_ABI_VERSION 3
 
 enum pcore_status {
     PCORE_OK = 0,
@@ -73,6 +73,15 @@ int pcore_create(int device, pcore_ctx** out_ctx);
 void pcore_destroy(pcore_ctx* ctx);
 const char* pcore_last_error(const pcore_ctx* ctx);
 int pcore_abi_version(void);
+
+/* Generation of the context's device state.  A captured HIP graph of pcore_evaluate bakes in the kernel
+ * arguments and the scratch pointers of the call it captured (sampled source, neighbour grids, overflow
+ * list, colour scratch, tile size); the counter changes whenever any of them may have changed:
+ * pcore_upload_meshes, pcore_set_camera, pcore_set_observation, pcore_set_observation_colors, a new
+ * sampling stride, and every reallocation of per-batch scratch.  A replay is valid only while the
+ * generation equals the one read right after the capture (no reference counterpart: the reference
+ * re-uploads everything per call, renderer.cu:1532-1544).  0 for a NULL context. */
+uint64_t pcore_generation(const pcore_ctx* ctx);
 
 /* ---- static inputs ----------------------------------------------------------------------------- */
 /* Triangles of all models concatenated + triangles per model: the `tris` and `tris_model_count`

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_evaluate_icp",
     "pcore_render",
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
-    "pcore_observed_cloud_bounded", "pcore_set_observation_colors",
+    "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation",
 )
 
 
@@ -108,8 +108,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     L.pcore_set_observation_colors.argtypes = [vp, vp, i32, vp]
     L.pcore_observed_cloud_bounded.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, vp, vp, vp, i32,
                                                ctypes.POINTER(i32), vp]
+    L.pcore_generation.argtypes = [vp]
     for name in EXPORTED_SYMBOLS:
-        if name not in ("pcore_destroy", "pcore_last_error"):
+        if name not in ("pcore_destroy", "pcore_last_error", "pcore_generation"):
             getattr(L, name).restype = ctypes.c_int
+    L.pcore_generation.restype = ctypes.c_uint64
     _lib = L
     return L

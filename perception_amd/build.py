@@ -30,6 +30,18 @@ def flags() -> list:
             "-fno-fast-math", "-Wall", "-Wno-unused-function"]
 
 
+def kernel_source_digest() -> str:
+    """SHA-256 (16 hex) of the sources that define the fused COST kernel: ties a committed counter profile
+    (profiles/sq_counters.json) to the code it measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h"):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True

@@ -171,7 +171,13 @@ class PoseCore:
         One warm-up call reserves the scratch, samples the source and picks the LDS tile tier; then the
         launches of one evaluate are captured.  Returns (replay, (rc, oc, diff)): replay() re-scores the batch
         from the tensors' current contents (write new poses into `poses` in place).  For batches small enough
-        to be launch-bound (C1: 128 poses); the results equal evaluate()'s."""
+        to be launch-bound (C1: 128 poses); the results equal evaluate()'s.
+
+        The graph bakes in the context state of the capture (sampled source, neighbour grids, scratch
+        pointers, tile size).  Any later setup call (upload_meshes, set_camera, set_observation,
+        set_observation_colors), a new stride or a larger batch that reallocates scratch changes the
+        context's generation (pcore_generation), and replay() then raises PcoreError(PCORE_E_STATE)
+        instead of running stale launches: capture again."""
         n = int(poses.shape[0])
         out = tuple(torch.empty(n, dtype=torch.float32, device=poses.device) for _ in range(3))
         self.evaluate(poses, pose_model, pose_label, pose_obs_total, out=out, **kw)
@@ -179,7 +185,19 @@ class PoseCore:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             self.evaluate(poses, pose_model, pose_label, pose_obs_total, out=out, **kw)
-        return graph.replay, out
+        gen = self.generation()
+
+        def replay():
+            if self.generation() != gen:
+                raise PcoreError(_native.PCORE_E_STATE, "captured evaluate graph is stale: the context changed "
+                                 "(setup call, new stride or scratch reallocation) since the capture")
+            graph.replay()
+
+        return replay, out
+
+    def generation(self) -> int:
+        """pcore_generation: changes whenever state a captured evaluate graph depends on may have changed."""
+        return int(self.lib.pcore_generation(self._h))
 
     def evaluate_icp(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
                      pose_obs_total: Optional[torch.Tensor], cost_type: int = _native.COST_DEPTH_6DOF,

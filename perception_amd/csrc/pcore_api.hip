@@ -31,6 +31,8 @@ struct pcore_ctx {
     int device = 0;
     std::string err;
     hipDeviceProp_t prop{};
+    DeviceInfo dinfo{};       // per-device launch constants, filled once in pcore_create
+    uint64_t generation = 1;  // pcore_generation: bumped whenever captured state may change
     // mesh
     int num_models = 0;
     int num_tris = 0;
@@ -131,6 +133,14 @@ hipError_t dev_reserve(DevBuf<T>& b, size_t n) {
     e = hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(T));
     if (e == hipSuccess) b.n = n;
     return e;
+}
+
+// dev_reserve for scratch a captured evaluate graph points into: a reallocation invalidates such graphs
+template <typename T>
+hipError_t reserve_gen(pcore_ctx* c, DevBuf<T>& b, size_t n) {
+    if (b.n >= n && b.p) return hipSuccess;
+    c->generation++;
+    return dev_reserve(b, n);
 }
 
 template <typename T>
@@ -319,9 +329,25 @@ int pcore_create(int device, pcore_ctx** out_ctx) {
         delete c;
         return PCORE_E_HIP;
     }
+    // per-context (not function-static) launch constants: contexts on other devices or threads never share
+    // or race on them
+    DeviceInfo& d = c->dinfo;
+    d.num_cus = std::max(1, c->prop.multiProcessorCount);
+    d.lds_per_cu = c->prop.maxSharedMemoryPerMultiProcessor ? (size_t)c->prop.maxSharedMemoryPerMultiProcessor
+                                                            : (size_t)160 * 1024;
+    d.lds_granule = kLdsGranule;
+    if (const char* e = getenv("PCORE_LDS_GRANULE")) d.lds_granule = (size_t)std::max(atoi(e), 4);  // A/B only
+    int per_cu = 0;
+    if (gicp_occupancy_per_cu(&per_cu) != hipSuccess) {
+        delete c;
+        return PCORE_E_HIP;
+    }
+    d.gicp_resident_wgs = std::max(1, per_cu) * d.num_cus;
     *out_ctx = c;
     return PCORE_OK;
 }
+
+uint64_t pcore_generation(const pcore_ctx* c) { return c ? c->generation : 0; }
 
 void pcore_destroy(pcore_ctx* c) {
     if (!c) return;
@@ -356,6 +382,7 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     }
     if (acc != num_tris) return fail(c, PCORE_E_INVALID_ARG, "upload_meshes: sum(tris_model_count) != num_tris");
     HIPC(c, hipSetDevice(c->device));
+    c->generation++;
 
     std::vector<float4> mv;
     std::vector<uint32_t> mt, mo;
@@ -437,6 +464,7 @@ int pcore_set_camera(pcore_ctx* c, const pcore_camera* cam) {
     if (cam->width <= 0 || cam->height <= 0 || cam->width > 16384 || cam->height > 16384)
         return fail(c, PCORE_E_INVALID_ARG, "set_camera: bad image size");
     HIPC(c, hipSetDevice(c->device));
+    c->generation++;
     c->cam = *cam;
     std::vector<float> pj(cam->proj, cam->proj + 16);
     HIPC(c, dev_upload(c->proj, pj));
@@ -500,6 +528,7 @@ int pcore_set_observation_colors(pcore_ctx* c, const uint8_t* d_obs_rgb, int32_t
     if (num_obs != (int)c->obs_order.size() || (num_obs > 0 && !d_obs_rgb))
         return fail(c, PCORE_E_INVALID_ARG, "set_observation_colors: num_obs differs from the observation");
     HIPC(c, hipSetDevice(c->device));
+    c->generation++;
     hipStream_t s = (hipStream_t)stream;
     std::vector<uint8_t> rgb((size_t)num_obs * 3);
     if (num_obs > 0) HIPC(c, hipMemcpyAsync(rgb.data(), d_obs_rgb, rgb.size(), hipMemcpyDeviceToHost, s));
@@ -520,6 +549,7 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
         return fail(c, PCORE_E_INVALID_ARG, "set_observation: bad arguments");
     if (!(sensor_resolution >= 0.0f)) return fail(c, PCORE_E_INVALID_ARG, "set_observation: bad sensor_resolution");
     HIPC(c, hipSetDevice(c->device));
+    c->generation++;
     hipStream_t s = (hipStream_t)stream;
     const size_t npx = (size_t)c->cam.width * c->cam.height;
     HIPC(c, dev_reserve(c->src_depth, npx));
@@ -641,8 +671,6 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
 // whose tile holds the windows of >= 99 % of the poses of the last finished call with the same sampled
 // image; kDefaultTier until one is known.  Only the speed depends on the choice, never the results.
 static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
-    const size_t lds_cu = c->prop.maxSharedMemoryPerMultiProcessor ? c->prop.maxSharedMemoryPerMultiProcessor
-                                                                   : (size_t)160 * 1024;
     const bool colour = a.cid != nullptr;
     const int nsamp = a.ws * a.hs;
     hipError_t e;
@@ -656,9 +684,9 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
         if ((e = hipMemset(c->ovf_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
         if ((e = hipMemset(c->win_hist.p, 0, (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
     }
-    if ((e = dev_reserve(c->ovf_list, (size_t)num_poses)) != hipSuccess) return e;
+    if ((e = reserve_gen(c, c->ovf_list, (size_t)num_poses)) != hipSuccess) return e;
     int edge[kTileTiers];
-    for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, lds_cu);
+    for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, c->dinfo);
     const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);
     if (key != c->tile_key) {
         c->tile_key = key;
@@ -706,6 +734,7 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
 
 static int ensure_sampled(pcore_ctx* c, int stride, hipStream_t s) {
     if (c->sampled_stride == stride) return PCORE_OK;
+    c->generation++;  // a captured graph would read a source sampled at another stride
     const int ws = (c->cam.width + stride - 1) / stride, hs = (c->cam.height + stride - 1) / stride;
     HIPC(c, dev_reserve(c->src_s, (size_t)ws * hs));
     HIPC(c, dev_reserve(c->lab_s, (size_t)ws * hs));
@@ -715,36 +744,51 @@ static int ensure_sampled(pcore_ctx* c, int stride, hipStream_t s) {
     return PCORE_OK;
 }
 
+// Every check pcore_evaluate makes before it launches anything.  pcore_evaluate_icp runs the same checks up
+// front, so an invalid call fails before it writes any output.
+static int validate_eval(pcore_ctx* c, const char* who, const float* d_poses, const int32_t* d_pose_model,
+                         const int32_t* d_pose_label, const float* d_pose_obs_total, int32_t num_poses,
+                         const pcore_eval_params* p, const float* d_out_rc, const float* d_out_oc,
+                         const float* d_out_diff) {
+    const std::string w(who);
+    if (!c->have_mesh || !c->have_cam || !c->have_obs)
+        return fail(c, PCORE_E_STATE, w + ": meshes, camera and observation must be set first");
+    if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_rc)))
+        return fail(c, PCORE_E_INVALID_ARG, w + ": null pose / output pointer");
+    if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF &&
+        p->cost_type != PCORE_COST_RGBD_3DOF)
+        return fail(c, PCORE_E_INVALID_ARG, w + ": unknown cost_type");
+    if (p->cost_type == PCORE_COST_RGBD_3DOF && (d_pose_label || !c->have_obs_colours))
+        return fail(c, PCORE_E_INVALID_ARG,
+                    w + ": cost_type 1 is 3-DoF (no pose labels) and needs pcore_set_observation_colors");
+    if (num_poses == 0) return PCORE_OK;
+    if (p->cost_type == PCORE_COST_DEPTH_6DOF && (!d_pose_label || !c->obs_has_mask))
+        return fail(c, PCORE_E_INVALID_ARG, w + ": cost_type 2 needs pose labels and a source mask");
+    if (p->calc_obs_cost && (!d_pose_obs_total || !d_out_oc || !d_out_diff))
+        return fail(c, PCORE_E_INVALID_ARG, w + ": calc_obs_cost needs pose_obs_total and oc/diff outputs");
+    const int W = c->cam.width, H = c->cam.height;
+    if (p->stride <= 0 || W % p->stride != 0)
+        return fail(c, PCORE_E_INVALID_ARG, w + ": width must be a multiple of stride");
+    const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
+    if (ws > 4095 || hs > 4095) return fail(c, PCORE_E_INVALID_ARG, w + ": sampled image too large");
+    // the overflow launch holds the whole sampled image in LDS (the GICP cloud launch needs less: no bitmap)
+    const size_t lds = fused_lds_bytes(ws * hs, c->bitmap_words, p->cost_type == PCORE_COST_RGBD_3DOF);
+    if (lds > (size_t)c->prop.sharedMemPerBlock)
+        return fail(c, PCORE_E_INVALID_ARG,
+                    w + ": sampled z-buffer does not fit in LDS (use a larger stride); need " + std::to_string(lds) +
+                        " B");
+    return PCORE_OK;
+}
+
 int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
                    const float* d_pose_obs_total, int32_t num_poses, const pcore_eval_params* p, float* d_out_rc,
                    float* d_out_oc, float* d_out_diff, int32_t* d_dbg_zs, pcore_stream stream) {
     if (!c || !p) return PCORE_E_INVALID_ARG;
-    if (!c->have_mesh || !c->have_cam || !c->have_obs)
-        return fail(c, PCORE_E_STATE, "evaluate: meshes, camera and observation must be set first");
-    if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_rc)))
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate: null pose / output pointer");
-    if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF &&
-        p->cost_type != PCORE_COST_RGBD_3DOF)
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate: unknown cost_type");
-    if (p->cost_type == PCORE_COST_RGBD_3DOF && (d_pose_label || !c->have_obs_colours))
-        return fail(c, PCORE_E_INVALID_ARG,
-                    "evaluate: cost_type 1 is 3-DoF (no pose labels) and needs pcore_set_observation_colors");
-    if (num_poses == 0) return PCORE_OK;
-    if (p->cost_type == PCORE_COST_DEPTH_6DOF && (!d_pose_label || !c->obs_has_mask))
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate: cost_type 2 needs pose labels and a source mask");
-    if (p->calc_obs_cost && (!d_pose_obs_total || !d_out_oc || !d_out_diff))
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate: calc_obs_cost needs pose_obs_total and oc/diff outputs");
+    const int vr = validate_eval(c, "evaluate", d_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p,
+                                 d_out_rc, d_out_oc, d_out_diff);
+    if (vr != PCORE_OK || num_poses == 0) return vr;
     const int W = c->cam.width, H = c->cam.height;
-    if (p->stride <= 0 || W % p->stride != 0)
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate: width must be a multiple of stride");
     const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
-    if (ws > 4095 || hs > 4095) return fail(c, PCORE_E_INVALID_ARG, "evaluate: sampled image too large");
-    const size_t lds = fused_lds_bytes(ws * hs, c->bitmap_words, p->cost_type == PCORE_COST_RGBD_3DOF);
-    if (lds > (size_t)c->prop.sharedMemPerBlock)
-        return fail(c, PCORE_E_INVALID_ARG,
-                    "evaluate: sampled z-buffer does not fit in LDS (use a larger stride); need " +
-                        std::to_string(lds) + " B");
-    if (num_poses == 0) return PCORE_OK;
     HIPC(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     int rc = ensure_sampled(c, p->stride, s);
@@ -792,7 +836,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
         a.tri_lab = c->tri_lab.p;
         a.obs_lab = c->obs_lab.p;
         a.colour_thr = p->color_distance_threshold;
-        HIPC(c, dev_reserve(c->colour_id, (size_t)num_poses * ws * hs));
+        HIPC(c, reserve_gen(c, c->colour_id, (size_t)num_poses * ws * hs));
         a.cid = c->colour_id.p;
     }
     if (const char* e = getenv("PCORE_DEBUG_SKIP")) a.dbg_skip = atoi(e);
@@ -843,23 +887,15 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     if (ip->k_correspondences <= 0 || ip->k_correspondences > 16 || ip->max_iterations < 0)
         return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: k_correspondences must be in [1, 16]");
     if (num_poses > 0 && !d_out_poses) return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: null d_out_poses");
-    // validate everything pcore_evaluate validates, without running it
-    if (!c->have_mesh || !c->have_cam || !c->have_obs)
-        return fail(c, PCORE_E_STATE, "evaluate_icp: meshes, camera and observation must be set first");
-    if (num_poses < 0 || (num_poses > 0 && (!d_poses || !d_pose_model || !d_out_rc)))
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: null pose / output pointer");
     if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF)
         return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: cost_type must be 0 or 2");
-    if (num_poses == 0) return PCORE_OK;
+    // everything the final pcore_evaluate (the re-score) checks, before any chunk writes an output
+    const int vr = validate_eval(c, "evaluate_icp", d_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses,
+                                 p, d_out_rc, d_out_oc, d_out_diff);
+    if (vr != PCORE_OK || num_poses == 0) return vr;
     const bool six = p->cost_type == PCORE_COST_DEPTH_6DOF;
-    if (six && (!d_pose_label || !c->obs_has_mask))
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: cost_type 2 needs pose labels and a source mask");
     const int W = c->cam.width;
-    if (p->stride <= 0 || W % p->stride != 0)
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: width must be a multiple of stride");
     const int ws = W / p->stride, hs = (c->cam.height + p->stride - 1) / p->stride;
-    if (fused_lds_bytes(ws, hs, c->bitmap_words) > (size_t)c->prop.sharedMemPerBlock)
-        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: sampled z-buffer does not fit in LDS");
     HIPC(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     int rc = ensure_sampled(c, p->stride, s);
@@ -952,7 +988,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
                                       c->icp_order_idx.p + chunk, c->icp_order_temp.p, order_temp, s));
             g.pose_order = c->icp_order_idx.p + chunk;
         }
-        HIPC(c, launch_gicp(g, n, s));
+        HIPC(c, launch_gicp(g, n, c->dinfo, s));
     }
     // re-render and re-score the adjusted poses (renderer.cu:1757-1907)
     return pcore_evaluate(c, d_out_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p, d_out_rc,

@@ -848,21 +848,14 @@ hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32
                                                         32, s);
 }
 
-hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s) {
+hipError_t gicp_occupancy_per_cu(int* per_cu) {
+    *per_cu = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel<kGicpWpp>, 64 * kGicpWpp, 0);
+}
+
+hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s) {
     if (num_poses <= 0) return hipSuccess;
-    static int resident_wgs = 0;  // workgroups the whole device holds at once (occupancy x CUs)
-    static int num_cus = 0;
-    if (resident_wgs == 0) {
-        int dev = 0, per_cu = 0;
-        hipDeviceProp_t prop;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipGetDeviceProperties(&prop, dev);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gicp_kernel<kGicpWpp>, 64 * kGicpWpp, 0);
-        if (e != hipSuccess) return e;
-        resident_wgs = std::max(1, per_cu) * prop.multiProcessorCount;
-        num_cus = prop.multiProcessorCount;
-    }
+    const int resident_wgs = std::max(1, d.gicp_resident_wgs), num_cus = std::max(1, d.num_cus);
     hipError_t e = hipMemsetAsync(g.work_counter, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     // a batch too small to give every SIMD a pose: spread each pose's searches over kGicpWideWpp waves

@@ -146,6 +146,22 @@ struct GicpArgs {
 // correspondences and target covariances); smaller ones the brute-force scans
 constexpr int kGridNNMin = 2048;
 
+// gfx950 allocates a workgroup's LDS in 1,280-byte granules (160 KiB = 128 of them), not the 512 bytes of
+// earlier CDNA parts: a census of resident fused_cost_kernel workgroups (tools/wg_timeline.py,
+// tools/lds_census.sh) found 27,136-byte tiles at 5 per CU and 32,768-byte ones at 4, but 26,880 and 32,000
+// bytes at 6 and 5.  PCORE_LDS_GRANULE overrides it (A/B only).
+constexpr size_t kLdsGranule = 1280;
+
+// Launch constants of one device, computed once per context (pcore_create) and passed to the launchers.
+struct DeviceInfo {
+    int num_cus = 0;
+    int gicp_resident_wgs = 0;  // gicp_kernel workgroups the whole device holds at once (occupancy x CUs)
+    size_t lds_per_cu = 0;
+    size_t lds_granule = kLdsGranule;
+};
+// resident gicp_kernel workgroups per CU (occupancy query of the persistent launch)
+hipError_t gicp_occupancy_per_cu(int* per_cu);
+
 // launchers (pcore_kernels.hip)
 hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s);
 // brute-force k-NN covariances, one workgroup per segment; segments above max_n points are skipped
@@ -156,7 +172,7 @@ hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const i
 hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_host, const int32_t* seg_cnt_host,
                                    int num_segs, int first_grid, const LabelGrid* grids, const int32_t* cell_start,
                                    const float4* grid_pts, int k, double* cov_out, hipStream_t s);
-hipError_t launch_gicp(const GicpArgs& g, int num_poses, hipStream_t s);
+hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s);
 // scratch of launch_gicp_order: 4 arrays of n 32-bit words + the radix sort's temporary storage
 size_t gicp_order_temp_bytes(int n);
 // g.pose_order for a chunk of n poses whose clouds are rendered (g.src_count): chunk-local indices sorted by
@@ -172,7 +188,7 @@ hipError_t launch_fused_cost(const FusedArgs& a, hipStream_t s);
 size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour = false);
 // tile capacity (samples) of tier t: the largest tile that leaves room for tier_wgs(t) workgroups per CU
 // (capped at the whole sampled image)
-int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, size_t lds_per_cu);
+int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, const DeviceInfo& d);
 constexpr int kOvfGrid = 1024;  // most workgroups of the overflow launch (grid-stride over the list)
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
                               const float* poses, const int32_t* pose_model, int num_poses, int width, int height,

@@ -949,19 +949,11 @@ hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// gfx950 allocates a workgroup's LDS in 1,280-byte granules (160 KiB = 128 of them), not the 512 bytes of
-// earlier CDNA parts: a census of resident fused_cost_kernel workgroups (tools/wg_timeline.py,
-// tools/lds_census.sh) found 27,136-byte tiles at 5 per CU and 32,768-byte ones at 4, but 26,880 and 32,000
-// bytes at 6 and 5.  PCORE_LDS_GRANULE overrides it (A/B only).
-constexpr size_t kLdsGranule = 1280;
-
-int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, size_t lds_per_cu) {
+// The LDS granule (kLdsGranule, pcore_internal.h) comes from the context's DeviceInfo.
+int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, const DeviceInfo& d) {
     const int nsamp = ws * hs;
-    static const size_t granule = [] {
-        const char* e = getenv("PCORE_LDS_GRANULE");
-        return (size_t)(e ? std::max(atoi(e), 4) : kLdsGranule);
-    }();
-    const size_t per_wg = (lds_per_cu / tier_wgs(t)) / granule * granule;
+    const size_t granule = d.lds_granule;
+    const size_t per_wg = (d.lds_per_cu / tier_wgs(t)) / granule * granule;
     const size_t fixed = fused_lds_bytes(0, bitmap_words, colour);
     if (per_wg <= fixed + 64) return 0;
     const int cap = (int)((per_wg - fixed) / 4) & ~3;

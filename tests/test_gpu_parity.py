@@ -267,6 +267,94 @@ def test_graph_replay_matches_oracle(one_object):
         assert _bits_equal(df.cpu().numpy(), odf)
 
 
+def test_graph_replay_refuses_stale_context():
+    """A captured evaluate graph bakes in the sampled source, the grids and the scratch pointers of its
+    capture: after set_observation, or after a larger batch reallocated the overflow list, replay() raises
+    instead of scoring against stale (or freed) state; a fresh capture scores the new state correctly."""
+    from perception_amd._native import PCORE_E_STATE, PcoreError
+
+    case = SceneCase(("003_cracker_box",), n_poses=40)
+    core, t = _setup(case)
+    sc = case.scene
+    n = 16
+    poses = t["poses"][:n].clone()
+    replay, (rc, oc, df) = core.capture_evaluate(poses, t["pm"][:n], t["pl"][:n], t["tot"][:n], cost_type=2,
+                                                 stride=case.stride)
+    g0 = core.generation()
+    replay()
+    torch.cuda.synchronize()
+    core.evaluate(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n], cost_type=2, stride=case.stride)
+    assert core.generation() == g0  # same-size eager calls leave the capture valid
+    replay()
+    # a new observation (here: the scene with its source depth shifted 5 cm back)
+    src2 = t["src"] + 5
+    core.set_observation(src2, t["mask"], t["obs_xyz"], t["obs_lab"], 0.01)
+    with pytest.raises(PcoreError) as ei:
+        replay()
+    assert ei.value.code == PCORE_E_STATE
+    replay2, (rc2, oc2, df2) = core.capture_evaluate(poses, t["pm"][:n], t["pl"][:n], t["tot"][:n], cost_type=2,
+                                                     stride=case.stride)
+    replay2()
+    torch.cuda.synchronize()
+    orc, ooc, odf = oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n],
+                                    case.pose_label[:n], sc.width, sc.height, sc.proj, sc.src_depth_cm + 5, sc.mask,
+                                    1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz,
+                                    case.label_start, case.label_end, case.pose_obs_total[:n], 2, True, 0.01)
+    assert _bits_equal(rc2.cpu().numpy(), orc) and _bits_equal(oc2.cpu().numpy(), ooc)
+    # a larger batch reallocates the overflow list the graph points into
+    big = t["poses"].repeat(64, 1)
+    core.evaluate(big, t["pm"].repeat(64), t["pl"].repeat(64), t["tot"].repeat(64), cost_type=2, stride=case.stride)
+    with pytest.raises(PcoreError):
+        replay2()
+    core.close()
+
+
+def test_evaluate_icp_invalid_call_writes_nothing(one_object):
+    """evaluate_icp validates everything the final re-score checks before its first chunk runs: a call with
+    calc_obs_cost and no observed-cost outputs fails with INVALID_ARG and leaves the adjusted poses
+    untouched; an image whose sampled z-buffer cannot fit in LDS is INVALID_ARG too, not a failed launch."""
+    import ctypes
+
+    from perception_amd import _native
+    from perception_amd._native import EvalParams, IcpParams, PcoreError
+
+    case, core, t = one_object
+    n = 8
+    dev = t["poses"].device
+    adj = torch.full((n, 16), -7.0, device=dev)
+    rc = torch.full((n,), -7.0, device=dev)
+    p = EvalParams(2, 1, case.stride, 100.0, 0.01, 1.0, 15.0)
+    ip = IcpParams(_native.ICP_K, _native.ICP_MAX_ITER, _native.ICP_ROT_EPS, _native.ICP_TRANS_EPS)
+    vp = ctypes.c_void_p
+    r = core.lib.pcore_evaluate_icp(core._h, vp(t["poses"].data_ptr()), vp(t["pm"].data_ptr()),
+                                    vp(t["pl"].data_ptr()), vp(t["tot"].data_ptr()), n, ctypes.byref(p),
+                                    ctypes.byref(ip), vp(adj.data_ptr()), None, vp(rc.data_ptr()), None, None,
+                                    vp(torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert r == _native.PCORE_E_INVALID_ARG
+    assert (adj == -7.0).all() and (rc == -7.0).all()
+    with pytest.raises(PcoreError) as ei:
+        core.evaluate_icp(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n], cost_type=2, stride=1)
+    assert ei.value.code == _native.PCORE_E_INVALID_ARG
+
+
+def test_evaluate_icp_multi_chunk_equals_single_chunk(monkeypatch):
+    """The GICP scratch budget splits a batch into equal chunks (pose_base offsets, per-chunk queue order):
+    4,000 C2 poses under a 1 GiB budget (3,495 poses per chunk at 640x480 / stride 8) run as two chunks and
+    give the single-chunk result bit for bit (adjusted poses, iterations, costs)."""
+    from perception_amd import workloads
+
+    w = workloads.build(poses_per_model=4000)
+    one = [x.cpu().numpy() for x in w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                          stride=w.stride)]
+    monkeypatch.setenv("PCORE_ICP_SCRATCH_GIB", "1")
+    two = [x.cpu().numpy() for x in w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                          stride=w.stride)]
+    for a, b in zip(one, two):
+        assert _bits_equal(a, b)
+    assert one[1].max() == 150 and (one[0] != w.poses.cpu().numpy()).any()
+
+
 def test_empty_batch_and_errors(one_object):
     case, core, t = one_object
     dev = t["poses"].device

@@ -5,8 +5,12 @@ are in KiB; FETCH_SIZE reports half the bytes of wide coalesced reads, so it is 
 for narrower accesses).  Writes profiles/pmc_traffic.json."""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from perception_amd.build import kernel_source_digest  # noqa: E402
 
 
 def load(path, counter):
@@ -32,6 +36,7 @@ def main(fetch_csv, write_csv, out, poses_per_launch=10000, threads=256):
         "hbm_bytes_per_launch": (2.0 * fetch_kib + write_kib) * 1024.0,
         "launches": [len(f), len(w)],
         "note": "FETCH_SIZE doubled per the gfx950 calibration; WRITE_SIZE as reported",
+        "kernel_source_digest": kernel_source_digest(),
     }
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
