@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpcore.so")
 SOURCES = ["pcore_kernels.hip", "pcore_gicp.hip", "pcore_metrics.hip", "pcore_api.hip"]
-HEADERS = ["pcore_internal.h", "pcore_gicp_math.h", "pcore_colour.h", os.path.join("..", "..", "include", "pcore.h")]
+HEADERS = ["pcore_internal.h", "pcore_gicp_math.h", "pcore_colour.h", "pcore_fdiv.h", os.path.join("..", "..", "include", "pcore.h")]
 ARCH = os.environ.get("PCORE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -36,7 +36,7 @@ def kernel_source_digest() -> str:
     import hashlib
 
     h = hashlib.sha256()
-    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h"):
+    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h", "pcore_fdiv.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
@@ -59,6 +59,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(LIB + ".tmp", LIB)
     return LIB
+
+
+def build_checkers(verbose: bool = False) -> list:
+    """Test-infrastructure binaries under tools/bin (not part of libpcore.so): fdiv_check compares
+    pcore_fdiv.h's division against the compiler's IEEE division on the GPU (tests/test_gpu_fdiv.py)."""
+    root = os.path.dirname(HERE)
+    out_dir = os.path.join(root, "tools", "bin")
+    os.makedirs(out_dir, exist_ok=True)
+    built = []
+    for name in ("fdiv_check",):
+        src = os.path.join(root, "tools", name + ".hip")
+        out = os.path.join(out_dir, name)
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", src,
+               "-o", out]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=root)
+        built.append(out)
+    return built
 
 
 if __name__ == "__main__":

@@ -40,7 +40,6 @@ struct pcore_ctx {
     DevBuf<int32_t> tri_lo, tri_hi;
     DevBuf<float4> mverts;
     DevBuf<uint32_t> mtris;
-    DevBuf<Meshlet> meshlets;
     DevBuf<int32_t> model_ml_lo, model_ml_hi;
     DevBuf<float4> model_box;  // FusedArgs::model_box
     bool have_mesh = false;
@@ -236,11 +235,20 @@ void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std:
         m.tbase = (int)out_t.size();
         m.nv = (int)mv.size();
         m.nt = (int)mt.size();
-        for (int v : mv) out_v.push_back(make_float4(vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], 0.0f));
+        // fixed 64-entry slots (pcore_internal.h, Meshlet); every vertex slot's w carries nv | nt << 8
+        uint32_t meta_u = (uint32_t)m.nv | ((uint32_t)m.nt << 8);
+        float meta;
+        std::memcpy(&meta, &meta_u, 4);
+        for (int v : mv) out_v.push_back(make_float4(vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], meta));
+        for (int k = m.nv; k < kMeshletSlots; k++) out_v.push_back(make_float4(0.0f, 0.0f, 0.0f, meta));
         for (int t : mt) {
             out_t.push_back((uint32_t)local[tri_verts[3 * t]] | ((uint32_t)local[tri_verts[3 * t + 1]] << 8) |
                             ((uint32_t)local[tri_verts[3 * t + 2]] << 16));
             out_orig.push_back((uint32_t)(tri_base + t));
+        }
+        for (int k = m.nt; k < kMeshletSlots; k++) {
+            out_t.push_back(0u);
+            out_orig.push_back(0u);
         }
         out_m.push_back(m);
         for (int v : mv) local[v] = -1;
@@ -353,7 +361,7 @@ void pcore_destroy(pcore_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)dev_free(c->tris); (void)dev_free(c->tri_lo); (void)dev_free(c->tri_hi);
-    (void)dev_free(c->mverts); (void)dev_free(c->mtris); (void)dev_free(c->meshlets);
+    (void)dev_free(c->mverts); (void)dev_free(c->mtris);
     (void)dev_free(c->model_ml_lo); (void)dev_free(c->model_ml_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
     (void)dev_free(c->ovf_list); (void)dev_free(c->ovf_ctr); (void)dev_free(c->win_hist);
     if (c->fb_host) (void)hipHostFree(c->fb_host);
@@ -442,7 +450,6 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     HIPC(c, dev_upload(c->mverts, mv));
     HIPC(c, dev_upload(c->mtris, mt));
     HIPC(c, dev_upload(c->mtri_orig, mo));
-    HIPC(c, dev_upload(c->meshlets, ml));
     std::vector<float4> tl((size_t)num_tris);
     for (int t = 0; t < num_tris; t++) {
         uint8_t col[3] = {128, 128, 128};
@@ -802,7 +809,6 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.num_poses = num_poses;
     a.mverts = c->mverts.p;
     a.mtris = c->mtris.p;
-    a.meshlets = c->meshlets.p;
     a.model_ml_lo = c->model_ml_lo.p;
     a.model_ml_hi = c->model_ml_hi.p;
     a.model_box = c->model_box.p;
@@ -851,7 +857,6 @@ static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& 
     a = FusedArgs{};
     a.mverts = c->mverts.p;
     a.mtris = c->mtris.p;
-    a.meshlets = c->meshlets.p;
     a.model_ml_lo = c->model_ml_lo.p;
     a.model_ml_hi = c->model_ml_hi.p;
     a.model_box = c->model_box.p;

@@ -1,0 +1,59 @@
+// pcore_fdiv.h -- IEEE-exact f32 division for the fused COST kernel without the range-scaling steps.
+//
+// hipcc expands every f32 `a / b` (no fast-math) into 11 instructions:
+//   v_div_scale(b), v_rcp, fma, fma        -> r1, a refined reciprocal of b
+//   v_div_scale(a), mul, fma, fma, fma     -> q1, e2
+//   v_div_fmas(e2, r1, q1)                 -> fma, times 2^+-64 when div_scale scaled an operand
+//   v_div_fixup(q, b, a)                   -> special cases (0, inf, NaN, over/underflow), sign
+// On gfx950 that sequence costs ~44 SIMD cycles (tools/valu_peak.hip: 0.25 instr/SIMD-cycle against 0.47
+// for plain FMAs; v_rcp alone is quarter rate), against ~2 per FMA.
+//
+// When the biased exponents of a and b lie in [87, 167] (|x| in [2^-40, 2^41)), v_div_scale returns both
+// operands unchanged with VCC = 0 (exponent difference < 96, no denormal operand / reciprocal / quotient,
+// numerator exponent > 23), v_div_fmas is then a plain fma, and v_div_fixup returns the fma result with
+// its own (correct) sign.  The steps below are therefore the compiler's sequence minus the no-op steps, and
+// the quotient is bit-identical to `a / b`, i.e. the correctly rounded IEEE quotient the CPU oracle
+// computes.  Lanes outside that range take `a / b` itself in an exec-masked branch (skipped by the wave
+// when no lane needs it), so every input -- zeros, denormals, infinities, NaNs -- keeps IEEE semantics.
+// Two quotients with one denominator (the vertex stage's px / z and py / z) share r1.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pcore {
+
+__device__ __forceinline__ float recip_refined(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+
+__device__ __forceinline__ float quot_refined(float a, float b, float r1) {
+    const float q0 = a * r1;
+    const float e1 = __builtin_fmaf(-b, q0, a);
+    const float q1 = __builtin_fmaf(e1, r1, q0);
+    const float e2 = __builtin_fmaf(-b, q1, a);
+    return __builtin_fmaf(e2, r1, q1);
+}
+
+// biased exponent of x (8 bits)
+__device__ __forceinline__ uint32_t fexp_bits(float x) { return (__float_as_uint(x) >> 23) & 0xffu; }
+
+// every biased exponent in [87, 167]: the unscaled steps equal the IEEE expansion
+__device__ __forceinline__ bool fdiv_range_ok(uint32_t emin, uint32_t emax) { return emin >= 87u && emax <= 167u; }
+
+// q0 = a0 / b, q1 = a1 / b, IEEE-exact
+__device__ __forceinline__ void fdiv2_exact(float a0, float a1, float b, float& q0, float& q1) {
+    const uint32_t e0 = fexp_bits(a0), e1 = fexp_bits(a1), eb = fexp_bits(b);
+    const uint32_t emin = min(min(e0, e1), eb), emax = max(max(e0, e1), eb);
+    const float r1 = recip_refined(b);
+    q0 = quot_refined(a0, b, r1);
+    q1 = quot_refined(a1, b, r1);
+    if (!fdiv_range_ok(emin, emax)) {  // rare: zeros, tiny / huge values, inf, NaN
+        asm volatile("");  // a side effect: keeps the compiler from speculating the division into every lane
+        q0 = a0 / b;
+        q1 = a1 / b;
+    }
+}
+
+}  // namespace pcore

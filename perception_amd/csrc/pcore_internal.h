@@ -6,18 +6,20 @@
 
 namespace pcore {
 
-// Meshlet: <= 64 unique vertices and <= 128 triangles of one model.  Vertices are stored per meshlet
-// (float4 x,y,z,0 in metres) so one lane loads one vertex with a single 16-byte load; triangles are
-// packed local indices i0 | i1 << 8 | i2 << 16.
+// Meshlet: <= 64 unique vertices and <= 64 triangles of one model, stored in fixed 64-entry slots so that
+// meshlet m's vertices are mverts[64 m + lane] and its triangles mtris[64 m + lane]: one lane loads one
+// vertex (float4, 16 B) and one triangle (packed local indices i0 | i1 << 8 | i2 << 16) per meshlet, with
+// addresses computed from m alone.  The loads are unconditional -- no header load in front of them, no
+// per-lane branch around them -- so the compiler can count them and keep the next meshlet's loads in
+// flight (s_waitcnt vmcnt(N)) while the current one is processed.  Every slot's vertex w holds the
+// meshlet's counts, nv | nt << 8, as integer bits; slots past nv / nt are padding.  (The 003_cracker_box
+// proxy: 197 meshlets; a builder limit of 128 triangles gave 191 meshlets in 264 mostly-empty batches.)
 constexpr int kMeshletMaxVerts = 64;
-constexpr int kMeshletMaxTris = 128;
-// The builder stops at 64 triangles: one vertex pass + one 64-lane triangle batch per meshlet.  With 128,
-// meshlets of 65..95 triangles cost a second, mostly empty batch (the 003_cracker_box proxy: 191 meshlets
-// and 264 batches vs 197 and 197).
+constexpr int kMeshletSlots = 64;
 constexpr int kMeshletBuildTris = 64;
-struct Meshlet {
-    int32_t vbase;  // first vertex in mverts
-    int32_t tbase;  // first triangle in mtris
+struct Meshlet {  // host-side bookkeeping of the builder
+    int32_t vbase;  // first vertex slot (64 m)
+    int32_t tbase;  // first triangle slot (64 m)
     int32_t nv;
     int32_t nt;
 };
@@ -52,9 +54,8 @@ struct FusedArgs {
     const float* pose_obs_total;
     int32_t num_poses;
     // mesh
-    const float4* mverts;
-    const uint32_t* mtris;
-    const Meshlet* meshlets;
+    const float4* mverts;   // 64 slots per meshlet (see Meshlet)
+    const uint32_t* mtris;  // 64 slots per meshlet
     const int32_t* model_ml_lo;
     const int32_t* model_ml_hi;
     const float4* model_box;  // 2 per model: (min x, y, z, 1 if every vertex is finite), (max x, y, z, 0)

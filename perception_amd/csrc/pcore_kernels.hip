@@ -17,6 +17,7 @@
 //   select_kernel          host selection of the reference (int cost, filter, per-model argmin key).
 #include "pcore_internal.h"
 #include "pcore_colour.h"
+#include "pcore_fdiv.h"
 
 #include <algorithm>
 #include <climits>
@@ -275,14 +276,56 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
 
-// Meshlet header through the scalar cache (the index is wave-uniform; a constant-address-space load is an
-// s_load, which the compiler cannot prove safe for a plain global pointer in a kernel that also stores)
-typedef int i4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(4))) const i4v ci4v;
-__device__ __forceinline__ Meshlet load_meshlet(const Meshlet* p, int m) {
-    const i4v v = ((const ci4v*)p)[m];
-    return Meshlet{v.x, v.y, v.z, v.w};
+// One meshlet's loads for one lane: vertex slot, triangle slot (and original triangle id for the colour id
+// pass), unconditionally (pcore_internal.h, Meshlet) -- the compiler then counts them in vmcnt, and the
+// prefetch of the next meshlet stays in flight while the current one is processed.
+struct MeshletLanes {
+    float4 v;
+    uint32_t pk, id;
+};
+template <bool IDPASS>
+__device__ __forceinline__ MeshletLanes load_meshlet_lanes(const FusedArgs& a, int m, int lane) {
+    const size_t k = (size_t)m * kMeshletSlots + lane;
+    MeshletLanes r;
+    r.v = a.mverts[k];
+    r.pk = a.mtris[k];
+    r.id = IDPASS ? a.mtri_orig[k] : 0u;
+    return r;
 }
+
+// Measurement build only (-DPCORE_FUSED_PROFILE, tools/fused_phase_prof.py): per-wave shader clocks of the
+// fused kernel's phases -- [0] setup, [1] vertex stage, [2] triangle windows + queueing, [3] fragment
+// batches, [4] wait at the end-of-raster barrier, [5] phase 2 (occlusion, unprojection, 1-NN, counts),
+// [6] phase 3 + barriers.  Each wave sums in registers and adds once at exit.
+#ifdef PCORE_FUSED_PROFILE
+__device__ unsigned long long g_fprof[8];
+extern "C" int pcore_debug_fused_profile(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(unsigned long long) * 8);
+    if (e == hipSuccess && reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_fprof), z, sizeof(z));
+    }
+    return e == hipSuccess ? 0 : 1;
+}
+struct FProf {
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long last = __builtin_amdgcn_s_memtime();
+    __device__ __forceinline__ void mark(int k) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        acc[k] += t - last;
+        last = t;
+    }
+    __device__ __forceinline__ void flush() {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < 8; k++) atomicAdd(&g_fprof[k], acc[k]);
+    }
+};
+#else
+struct FProf {
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush() {}
+};
+#endif
 
 #ifdef PCORE_FLUSH_STATS
 // measurement build only: small-triangle flush batches, records, fragment tests, loop trips
@@ -294,7 +337,7 @@ extern "C" int pcore_debug_flush_stats(unsigned long long* host) {
 
 template <int STRIDE, bool IDPASS = false>
 __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw,
-                                             int32_t* cid = nullptr) {
+                                             int32_t* cid, FProf& fp) {
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of meshlet headers
     const int lane = tid & 63;
@@ -329,6 +372,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     const int dbg = a.dbg_skip;
     auto ring_slot = [&](int i) { return i >= kRecCap ? i - kRecCap : i; };  // i < 2 kRecCap
     auto flush = [&](int head, int count) {
+        fp.mark(2);
         wave_sync();
         if (dbg & 1) return;
         for (int base = 0; base < count; base += kWave) {
@@ -365,51 +409,36 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             }
         }
         wave_sync();
+        fp.mark(3);
     };
 
     if (model < 0 || model >= a.num_models) return;
     const int ml_lo = a.model_ml_lo[model], ml_hi = a.model_ml_hi[model];
     int m = ml_lo + wave;
-    Meshlet ml = {0, 0, 0, 0};
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint32_t pk0 = 0, pk1 = 0, id0 = 0, id1 = 0;
-    if (m < ml_hi) {
-        ml = load_meshlet(a.meshlets, m);
-        if (lane < ml.nv) v = a.mverts[ml.vbase + lane];
-        if (lane < ml.nt) pk0 = a.mtris[ml.tbase + lane];
-        if (kWave + lane < ml.nt) pk1 = a.mtris[ml.tbase + kWave + lane];
-        if (IDPASS) {
-            if (lane < ml.nt) id0 = a.mtri_orig[ml.tbase + lane];
-            if (kWave + lane < ml.nt) id1 = a.mtri_orig[ml.tbase + kWave + lane];
-        }
-    }
+    MeshletLanes cur = {make_float4(0.f, 0.f, 0.f, 0.f), 0u, 0u};
+    if (m < ml_hi) cur = load_meshlet_lanes<IDPASS>(a, m, lane);
+    fp.mark(0);
     for (; m < ml_hi; m += kWaves) {
-        // prefetch the next meshlet of this wave while this one is processed
-        const int mn = m + kWaves;
-        Meshlet mln = {0, 0, 0, 0};
-        float4 vn = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t pn0 = 0, pn1 = 0, in0 = 0, in1 = 0;
-        if (mn < ml_hi) {
-            mln = load_meshlet(a.meshlets, mn);
-            if (lane < mln.nv) vn = a.mverts[mln.vbase + lane];
-            if (lane < mln.nt) pn0 = a.mtris[mln.tbase + lane];
-            if (kWave + lane < mln.nt) pn1 = a.mtris[mln.tbase + kWave + lane];
-            if (IDPASS) {
-                if (lane < mln.nt) in0 = a.mtri_orig[mln.tbase + lane];
-                if (kWave + lane < mln.nt) in1 = a.mtri_orig[mln.tbase + kWave + lane];
-            }
-        }
+        // prefetch the next meshlet of this wave while this one is processed (the last one re-loads itself:
+        // every load is unconditional, so the wait below covers only the current meshlet's loads)
+        const MeshletLanes nxt = load_meshlet_lanes<IDPASS>(a, min(m + kWaves, ml_hi - 1), lane);
+        const float4 v = cur.v;
+        const uint32_t meta = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(v.w));
+        const int ml_nv = (int)(meta & 0xffu), ml_nt = (int)((meta >> 8) & 0xffu);
         // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
         // (image_renderer.cuh:296-305, 82-84)
         bool bad_vertex = false;
-        if (lane < ml.nv && !(dbg & 8)) {
+        if (lane < ml_nv && !(dbg & 8)) {
             const float lx = row4(m00, m01, m02, m03, v.x, v.y, v.z);
             const float ly = row4(m10, m11, m12, m13, v.x, v.y, v.z);
             const float lz = row4(m20, m21, m22, m23, v.x, v.y, v.z);
             const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
             const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
-            const float sx = px / lz * Wf / 2.0f + Wf / 2.0f;
-            const float sy = py / lz * Hf / 2.0f + Hf / 2.0f;
+            // px / lz and py / lz, IEEE-exact, sharing one refined reciprocal of lz (pcore_fdiv.h)
+            float qx, qy;
+            fdiv2_exact(px, py, lz, qx, qy);
+            const float sx = qx * Wf / 2.0f + Wf / 2.0f;
+            const float sy = qy * Hf / 2.0f + Hf / 2.0f;
             vx[lane] = sx;
             vy[lane] = sy;
             vz[lane] = lz;
@@ -418,16 +447,14 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         }
         const uint64_t nanmask = __ballot(bad_vertex);
         wave_sync();
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const int t0 = half * kWave;
-            if (t0 >= ml.nt || (dbg & 2)) break;
-            const int t = t0 + lane;
-            const uint32_t pk = half == 0 ? pk0 : pk1;
-            const uint32_t oid = half == 0 ? id0 : id1;
+        fp.mark(1);
+        if (!(dbg & 2)) {
+            const int t = lane;
+            const uint32_t pk = cur.pk;
+            const uint32_t oid = cur.id;
             int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
             int i0 = 0, i1 = 0, i2 = 0;
-            if (t < ml.nt) {
+            if (t < ml_nt) {
                 i0 = pk & 0xff; i1 = (pk >> 8) & 0xff; i2 = (pk >> 16) & 0xff;
                 const bool nan_tri = nanmask != 0 && (((nanmask >> i0) | (nanmask >> i1) | (nanmask >> i2)) & 1ull);
                 if (!nan_tri) {
@@ -467,7 +494,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             uint64_t big = __ballot(nk > kSmallK);
 #ifdef PCORE_FLUSH_STATS
             {
-                const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(t < ml.nt);
+                const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(t < ml_nt);
                 if (lane == 0) {
                     atomicAdd(&pcore_flush_stats[4], (unsigned long long)__popcll(big));
                     atomicAdd(&pcore_flush_stats[5], (unsigned long long)__popcll(btouch));
@@ -521,12 +548,8 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             }
         }
         wave_sync();  // vertex slots are rewritten by the next meshlet
-        ml = mln;
-        v = vn;
-        pk0 = pn0;
-        pk1 = pn1;
-        id0 = in0;
-        id1 = in1;
+        fp.mark(2);
+        cur = nxt;
     }
     if (rec_count > 0) flush(rec_head, rec_count);
 }
@@ -603,15 +626,18 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
 
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
-    raster_phase<STRIDE>(a, sm, pose, sw);
+    FProf fp;
+    raster_phase<STRIDE>(a, sm, pose, sw, nullptr, fp);
+    fp.mark(2);
     __syncthreads();
+    fp.mark(4);
     int32_t* cid = nullptr;
     if constexpr (COLOUR) {
         // colour id pass (cost_type 1): which triangle left each sample's minimum depth (tile-local index)
         cid = a.cid + (size_t)pose * nsamp;
         for (int i = tid; i < tn; i += kThreads) cid[i] = INT_MAX;
         __syncthreads();
-        raster_phase<STRIDE, true>(a, sm, pose, sw, cid);
+        raster_phase<STRIDE, true>(a, sm, pose, sw, cid, fp);
         __syncthreads();
     }
 
@@ -739,6 +765,7 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
         }
     }
     if (qcount > 0) process_points(qcount);
+    fp.mark(5);
     // per-wave totals
     int wave_bad = my_bad;
     for (int off = 32; off > 0; off >>= 1) wave_bad += __shfl_xor(wave_bad, off);
@@ -774,6 +801,8 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
             if (a.out_diff) a.out_diff[pose] = 0.0f;
         }
     }
+    fp.mark(6);
+    fp.flush();
 }
 
 __device__ __forceinline__ void load_pose_rows(const float* poses, int pose, float (&m)[12]) {
@@ -897,7 +926,8 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
     if (tid == 0) carry_s = 0;
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
-    raster_phase<STRIDE>(a, sm, pose, sw);
+    FProf fp;
+    raster_phase<STRIDE>(a, sm, pose, sw, nullptr, fp);
     __syncthreads();
     float4* out = a.cloud_out + (size_t)pose * a.cloud_cap;
     // row-major over the window = the reference's row-major compaction order (no valid sample lies outside)

@@ -1,0 +1,65 @@
+// fdiv_check.hip -- checker (test infrastructure, not product code): pcore::fdiv2_exact (pcore_fdiv.h)
+// against the compiler's IEEE f32 division `a / b`, bit for bit, on the GPU.
+//
+// Inputs: 2^26 pairs per launch from a counter-based hash, with exponents drawn over the whole f32 range
+// (zeros, denormals, infinities and NaNs included) and a dense band around the [2^-40, 2^41) fast-path
+// bounds, plus structured pairs (exact quotients, quotients near rounding ties: a = b * (1 + k ulp)).
+// Prints one JSON line {"pairs": N, "mismatches": M, "fast_frac": F}; exit status 1 on any mismatch.
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/bin/fdiv_check tools/fdiv_check.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "../perception_amd/csrc/pcore_fdiv.h"
+
+#pragma clang fp contract(off)
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ float draw(uint32_t h, uint32_t h2) {
+    const uint32_t kind = h2 & 15u;
+    uint32_t e;
+    if (kind < 6) e = (h2 >> 4) & 0xffu;               // any exponent incl. 0 (denormal / zero) and 255
+    else if (kind < 12) e = 80u + ((h2 >> 4) % 96u);   // dense band around the fast-path bounds 87..167
+    else e = 120u + ((h2 >> 4) % 16u);                 // typical magnitudes (0.002 .. 500)
+    uint32_t m = h & 0x7fffffu;
+    if ((h2 >> 20) % 64u == 0) m = 0;                  // exact powers of two
+    const uint32_t s = (h2 >> 31) << 31;
+    return __uint_as_float(s | (e << 23) | m);
+}
+
+__global__ void check(uint32_t seed, unsigned long long* bad, unsigned long long* fast) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t h0 = mix(i * 4u + seed), h1 = mix(i * 4u + 1u + seed * 7u), h2 = mix(i * 4u + 2u + seed * 13u),
+                   h3 = mix(i * 4u + 3u + seed * 31u);
+    float a0 = draw(h0, h1), b = draw(h2, h3), a1 = draw(h1 ^ h3, h0 ^ h2);
+    if ((h3 >> 8) % 8u == 0) {  // quotients near rounding ties: a = b * (1 + k ulp) and exact multiples
+        const float q = draw(h1, h0 | 0xc00u);
+        a0 = b * q;
+        a1 = __uint_as_float(__float_as_uint(a0) + ((h3 >> 12) & 3u) - 1u);
+    }
+    float q0, q1;
+    pcore::fdiv2_exact(a0, a1, b, q0, q1);
+    const float r0 = a0 / b, r1 = a1 / b;
+    const bool ok0 = __float_as_uint(q0) == __float_as_uint(r0) || (q0 != q0 && r0 != r0);
+    const bool ok1 = __float_as_uint(q1) == __float_as_uint(r1) || (q1 != q1 && r1 != r1);
+    if (!ok0 || !ok1) atomicAdd(bad, 1ull);
+    const uint32_t e0 = pcore::fexp_bits(a0), e1 = pcore::fexp_bits(a1), eb = pcore::fexp_bits(b);
+    if (pcore::fdiv_range_ok(min(min(e0, e1), eb), max(max(e0, e1), eb))) atomicAdd(fast, 1ull);
+}
+
+int main() {
+    unsigned long long *d, h[2] = {0, 0};
+    if (hipMalloc(&d, 16) != hipSuccess) return 2;
+    if (hipMemset(d, 0, 16) != hipSuccess) return 2;
+    const int launches = 16, blocks = 1 << 18, threads = 256;
+    for (int l = 0; l < launches; l++) hipLaunchKernelGGL(check, dim3(blocks), dim3(threads), 0, 0, (uint32_t)l * 0x9e3779b9u, d, d + 1);
+    if (hipDeviceSynchronize() != hipSuccess) return 2;
+    if (hipMemcpy(h, d, 16, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    const double pairs = 2.0 * launches * (double)blocks * threads;
+    printf("{\"pairs\": %.0f, \"mismatches\": %llu, \"fast_frac\": %.4f}\n", pairs, h[0], 2.0 * h[1] / pairs);
+    return h[0] == 0 ? 0 : 1;
+}
