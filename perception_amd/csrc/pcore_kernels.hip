@@ -454,11 +454,18 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             const uint32_t oid = cur.id;
             int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
             int i0 = 0, i1 = 0, i2 = 0;
+            TriRec r;
             if (t < ml_nt) {
                 i0 = pk & 0xff; i1 = (pk >> 8) & 0xff; i2 = (pk >> 16) & 0xff;
+                // the record's vertex data is read with the windows, whether or not the triangle touches a
+                // sample: one LDS round trip instead of two (most waves have some touching lane anyway)
+                const uint2 w0 = vwin[i0], w1 = vwin[i1], w2 = vwin[i2];
+                r.a0 = vx[i0]; r.a1 = vy[i0];
+                r.b0 = vx[i1]; r.b1 = vy[i1];
+                r.c0 = vx[i2]; r.c1 = vy[i2];
+                r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
                 const bool nan_tri = nanmask != 0 && (((nanmask >> i0) | (nanmask >> i1) | (nanmask >> i2)) & 1ull);
                 if (!nan_tri) {
-                    const uint2 w0 = vwin[i0], w1 = vwin[i1], w2 = vwin[i2];
                     short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
                     short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
                     lo = __builtin_elementwise_max(lo, wzero);
@@ -469,7 +476,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     nk = (nx > 0 && ny > 0) ? nx * ny : 0;
                 } else {
                     // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
-                    const float p[3][2] = {{vx[i0], vy[i0]}, {vx[i1], vy[i1]}, {vx[i2], vy[i2]}};
+                    const float p[3][2] = {{r.a0, r.a1}, {r.b0, r.b1}, {r.c0, r.c1}};
                     float bmin[2], bmax[2];
                     bbox_ref(p, cmax0, cmax1, bmin, bmax);
                     nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
@@ -482,13 +489,6 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         nk = (nx > 0 && ny > 0) ? nx * ny : 0;
                     }
                 }
-            }
-            TriRec r;
-            if (nk > 0) {
-                r.a0 = vx[i0]; r.a1 = vy[i0];
-                r.b0 = vx[i1]; r.b1 = vy[i1];
-                r.c0 = vx[i2]; r.c1 = vy[i2];
-                r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
             }
             // large triangles: whole-wave cooperative
             uint64_t big = __ballot(nk > kSmallK);
