@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpcore.so")
 SOURCES = ["pcore_kernels.hip", "pcore_gicp.hip", "pcore_metrics.hip", "pcore_api.hip"]
-HEADERS = ["pcore_internal.h", "pcore_gicp_math.h", "pcore_colour.h", "pcore_fdiv.h", os.path.join("..", "..", "include", "pcore.h")]
+HEADERS = ["pcore_internal.h", "pcore_gicp_math.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h", os.path.join("..", "..", "include", "pcore.h")]
 ARCH = os.environ.get("PCORE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -36,7 +36,7 @@ def kernel_source_digest() -> str:
     import hashlib
 
     h = hashlib.sha256()
-    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h", "pcore_fdiv.h"):
+    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

@@ -1,9 +1,10 @@
 // pcore_api.hip -- C ABI (include/pcore.h) of the MI355X pose-search core: context, static inputs
-// (mesh dedupe + meshlets, camera), per-scene observation (label sort + neighbour grids) and dispatch of
+// (mesh dedupe + vertex-ring streams, camera), per-scene observation (label sort + neighbour grids) and dispatch of
 // the kernels in pcore_kernels.hip.  Host code; no hidden allocations on the per-batch path (evaluate /
 // select), scratch for the parity stages grows monotonically.
 #include "../../include/pcore.h"
 #include "pcore_internal.h"
+#include "pcore_streams.h"
 
 #include <algorithm>
 #include <climits>
@@ -38,9 +39,10 @@ struct pcore_ctx {
     int num_tris = 0;
     DevBuf<float> tris;          // original triangle soup (parity render)
     DevBuf<int32_t> tri_lo, tri_hi;
-    DevBuf<float4> mverts;
-    DevBuf<uint32_t> mtris;
-    DevBuf<int32_t> model_ml_lo, model_ml_hi;
+    DevBuf<float4> sverts;       // vertex-ring streams (pcore_internal.h, kVRing)
+    DevBuf<uint32_t> stris, ssteps;
+    DevBuf<int4> streams;
+    DevBuf<int32_t> model_st_lo, model_st_hi;
     DevBuf<float4> model_box;  // FusedArgs::model_box
     bool have_mesh = false;
     // camera
@@ -79,7 +81,7 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_order_idx;    // 2 x chunk indices (in, out = GicpArgs::pose_order)
     DevBuf<unsigned char> icp_order_temp;
     // colour gate (cost_type 1)
-    DevBuf<uint32_t> mtri_orig;   // original triangle of every meshlet triangle
+    DevBuf<uint32_t> stri_orig;   // original triangle of every stream triangle slot
     DevBuf<float4> tri_lab;       // Lab per original triangle
     DevBuf<float4> obs_lab;       // Lab per observed point, label-sorted
     DevBuf<int32_t> colour_id;    // N x nsamp scratch of the fused kernel's colour id pass
@@ -163,7 +165,6 @@ struct VKeyHash {
     }
 };
 
-// Greedy adjacency-growth meshlet builder for one model.  verts: unique vertex ids per triangle corner.
 // rgb2lab (compute_costs.cuh:57-88) in double with glibc pow / cbrt, stored as float.  The cost reads
 // its "red" from colour plane 2 and "blue" from plane 0 (compute_costs.cuh:214-220): rgb2lab(c2, c1, c0).
 float4 lab_of(const uint8_t c[3]) {
@@ -183,76 +184,6 @@ float4 lab_of(const uint8_t c[3]) {
     z = (z > 0.008856) ? std::cbrt(z) : (7.787 * z + 16.0 / 116.0);
     const float l = (float)((116.0 * y) - 16), a = (float)(500 * (x - y)), bb = (float)(200 * (y - z));
     return make_float4(l, a, bb, 0.0f);
-}
-
-void build_meshlets(const std::vector<int>& tri_verts, int num_verts, const std::vector<float>& vxyz, int tri_base,
-                    std::vector<float4>& out_v, std::vector<uint32_t>& out_t, std::vector<uint32_t>& out_orig,
-                    std::vector<Meshlet>& out_m) {
-    const int T = (int)tri_verts.size() / 3;
-    std::vector<std::vector<int>> adj(num_verts);
-    for (int t = 0; t < T; t++)
-        for (int k = 0; k < 3; k++) adj[tri_verts[3 * t + k]].push_back(t);
-    std::vector<char> assigned(T, 0);
-    std::vector<int> local(num_verts, -1);
-    int next_seed = 0;
-    std::vector<int> mv;  // meshlet vertex ids
-    std::vector<int> mt;  // meshlet triangles
-    while (true) {
-        while (next_seed < T && assigned[next_seed]) next_seed++;
-        if (next_seed >= T) break;
-        mv.clear();
-        mt.clear();
-        auto add_tri = [&](int t) {
-            assigned[t] = 1;
-            mt.push_back(t);
-            for (int k = 0; k < 3; k++) {
-                const int v = tri_verts[3 * t + k];
-                if (local[v] < 0) {
-                    local[v] = (int)mv.size();
-                    mv.push_back(v);
-                }
-            }
-        };
-        add_tri(next_seed);
-        while ((int)mt.size() < kMeshletBuildTris) {
-            int best = -1, best_score = -1;
-            for (size_t i = 0; i < mv.size(); i++)
-                for (int t : adj[mv[i]]) {
-                    if (assigned[t]) continue;
-                    int shared = 0;
-                    for (int k = 0; k < 3; k++) shared += local[tri_verts[3 * t + k]] >= 0 ? 1 : 0;
-                    if ((int)mv.size() + (3 - shared) > kMeshletMaxVerts) continue;
-                    if (shared > best_score || (shared == best_score && t < best)) {
-                        best_score = shared;
-                        best = t;
-                    }
-                }
-            if (best < 0) break;
-            add_tri(best);
-        }
-        Meshlet m;
-        m.vbase = (int)out_v.size();
-        m.tbase = (int)out_t.size();
-        m.nv = (int)mv.size();
-        m.nt = (int)mt.size();
-        // fixed 64-entry slots (pcore_internal.h, Meshlet); every vertex slot's w carries nv | nt << 8
-        uint32_t meta_u = (uint32_t)m.nv | ((uint32_t)m.nt << 8);
-        float meta;
-        std::memcpy(&meta, &meta_u, 4);
-        for (int v : mv) out_v.push_back(make_float4(vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], meta));
-        for (int k = m.nv; k < kMeshletSlots; k++) out_v.push_back(make_float4(0.0f, 0.0f, 0.0f, meta));
-        for (int t : mt) {
-            out_t.push_back((uint32_t)local[tri_verts[3 * t]] | ((uint32_t)local[tri_verts[3 * t + 1]] << 8) |
-                            ((uint32_t)local[tri_verts[3 * t + 2]] << 16));
-            out_orig.push_back((uint32_t)(tri_base + t));
-        }
-        for (int k = m.nt; k < kMeshletSlots; k++) {
-            out_t.push_back(0u);
-            out_orig.push_back(0u);
-        }
-        out_m.push_back(m);
-        for (int v : mv) local[v] = -1;
-    }
 }
 
 // Neighbour grid over one point set.  `pts` are (x,y,z, local index) in label-sorted order.
@@ -361,8 +292,8 @@ void pcore_destroy(pcore_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)dev_free(c->tris); (void)dev_free(c->tri_lo); (void)dev_free(c->tri_hi);
-    (void)dev_free(c->mverts); (void)dev_free(c->mtris);
-    (void)dev_free(c->model_ml_lo); (void)dev_free(c->model_ml_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
+    (void)dev_free(c->sverts); (void)dev_free(c->stris); (void)dev_free(c->ssteps); (void)dev_free(c->streams);
+    (void)dev_free(c->model_st_lo); (void)dev_free(c->model_st_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
     (void)dev_free(c->ovf_list); (void)dev_free(c->ovf_ctr); (void)dev_free(c->win_hist);
     if (c->fb_host) (void)hipHostFree(c->fb_host);
     (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
@@ -371,7 +302,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
     (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
-    (void)dev_free(c->mtri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
+    (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part);
     delete c;
 }
@@ -392,11 +323,9 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     HIPC(c, hipSetDevice(c->device));
     c->generation++;
 
-    std::vector<float4> mv;
-    std::vector<uint32_t> mt, mo;
-    std::vector<Meshlet> ml;
+    streams::Built sb;
     std::vector<float4> box;
-    std::vector<int32_t> mlo(num_models), mhi(num_models), tlo(num_models), thi(num_models);
+    std::vector<int32_t> slo(num_models), shi(num_models), tlo(num_models), thi(num_models);
     int t0 = 0;
     for (int m = 0; m < num_models; m++) {
         const int T = tris_model_count[m];
@@ -438,18 +367,25 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
         if (vxyz.empty()) bmin = bmax = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         box.push_back(bmin);
         box.push_back(bmax);
-        mlo[m] = (int)ml.size();
-        build_meshlets(tv, (int)(vxyz.size() / 3), vxyz, t0, mv, mt, mo, ml);
-        mhi[m] = (int)ml.size();
+        slo[m] = (int)sb.streams.size();
+        streams::build_model(tv, vxyz, t0, kFusedWaves, kVRing, kRefPasses, sb);
+        shi[m] = (int)sb.streams.size();
         t0 += T;
     }
     std::vector<float> soup(tri_xyz, tri_xyz + (size_t)9 * num_tris);
     HIPC(c, dev_upload(c->tris, soup));
     HIPC(c, dev_upload(c->tri_lo, tlo));
     HIPC(c, dev_upload(c->tri_hi, thi));
-    HIPC(c, dev_upload(c->mverts, mv));
-    HIPC(c, dev_upload(c->mtris, mt));
-    HIPC(c, dev_upload(c->mtri_orig, mo));
+    static_assert(sizeof(streams::F4) == sizeof(float4) && sizeof(streams::I4) == sizeof(int4), "stream layouts");
+    std::vector<float4> sv(sb.sverts.size());
+    if (!sv.empty()) std::memcpy(sv.data(), sb.sverts.data(), sv.size() * sizeof(float4));
+    std::vector<int4> sd(sb.streams.size());
+    if (!sd.empty()) std::memcpy(sd.data(), sb.streams.data(), sd.size() * sizeof(int4));
+    HIPC(c, dev_upload(c->sverts, sv));
+    HIPC(c, dev_upload(c->stris, sb.stris));
+    HIPC(c, dev_upload(c->ssteps, sb.ssteps));
+    HIPC(c, dev_upload(c->streams, sd));
+    HIPC(c, dev_upload(c->stri_orig, sb.sorig));
     std::vector<float4> tl((size_t)num_tris);
     for (int t = 0; t < num_tris; t++) {
         uint8_t col[3] = {128, 128, 128};
@@ -457,8 +393,8 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
         tl[t] = lab_of(col);
     }
     HIPC(c, dev_upload(c->tri_lab, tl));
-    HIPC(c, dev_upload(c->model_ml_lo, mlo));
-    HIPC(c, dev_upload(c->model_ml_hi, mhi));
+    HIPC(c, dev_upload(c->model_st_lo, slo));
+    HIPC(c, dev_upload(c->model_st_hi, shi));
     HIPC(c, dev_upload(c->model_box, box));
     c->num_models = num_models;
     c->num_tris = num_tris;
@@ -807,10 +743,12 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.pose_label = (p->cost_type == PCORE_COST_DEPTH_6DOF) ? d_pose_label : nullptr;
     a.pose_obs_total = d_pose_obs_total;
     a.num_poses = num_poses;
-    a.mverts = c->mverts.p;
-    a.mtris = c->mtris.p;
-    a.model_ml_lo = c->model_ml_lo.p;
-    a.model_ml_hi = c->model_ml_hi.p;
+    a.sverts = c->sverts.p;
+    a.stris = c->stris.p;
+    a.ssteps = c->ssteps.p;
+    a.streams = c->streams.p;
+    a.model_st_lo = c->model_st_lo.p;
+    a.model_st_hi = c->model_st_hi.p;
     a.model_box = c->model_box.p;
     a.num_models = c->num_models;
     const float* pj = c->cam.proj;
@@ -838,7 +776,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.out_diff = d_out_diff;
     a.dbg_zs = d_dbg_zs;
     if (p->cost_type == PCORE_COST_RGBD_3DOF) {
-        a.mtri_orig = c->mtri_orig.p;
+        a.stri_orig = c->stri_orig.p;
         a.tri_lab = c->tri_lab.p;
         a.obs_lab = c->obs_lab.p;
         a.colour_thr = p->color_distance_threshold;
@@ -855,10 +793,12 @@ static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& 
     const int W = c->cam.width, H = c->cam.height;
     const int ws = W / p->stride, hs = (H + p->stride - 1) / p->stride;
     a = FusedArgs{};
-    a.mverts = c->mverts.p;
-    a.mtris = c->mtris.p;
-    a.model_ml_lo = c->model_ml_lo.p;
-    a.model_ml_hi = c->model_ml_hi.p;
+    a.sverts = c->sverts.p;
+    a.stris = c->stris.p;
+    a.ssteps = c->ssteps.p;
+    a.streams = c->streams.p;
+    a.model_st_lo = c->model_st_lo.p;
+    a.model_st_hi = c->model_st_hi.p;
     a.model_box = c->model_box.p;
     a.num_models = c->num_models;
     const float* pj = c->cam.proj;

@@ -6,23 +6,32 @@
 
 namespace pcore {
 
-// Meshlet: <= 64 unique vertices and <= 64 triangles of one model, stored in fixed 64-entry slots so that
-// meshlet m's vertices are mverts[64 m + lane] and its triangles mtris[64 m + lane]: one lane loads one
-// vertex (float4, 16 B) and one triangle (packed local indices i0 | i1 << 8 | i2 << 16) per meshlet, with
-// addresses computed from m alone.  The loads are unconditional -- no header load in front of them, no
-// per-lane branch around them -- so the compiler can count them and keep the next meshlet's loads in
-// flight (s_waitcnt vmcnt(N)) while the current one is processed.  Every slot's vertex w holds the
-// meshlet's counts, nv | nt << 8, as integer bits; slots past nv / nt are padding.  (The 003_cracker_box
-// proxy: 197 meshlets; a builder limit of 128 triangles gave 191 meshlets in 264 mostly-empty batches.)
-constexpr int kMeshletMaxVerts = 64;
-constexpr int kMeshletSlots = 64;
-constexpr int kMeshletBuildTris = 64;
-struct Meshlet {  // host-side bookkeeping of the builder
-    int32_t vbase;  // first vertex slot (64 m)
-    int32_t tbase;  // first triangle slot (64 m)
-    int32_t nv;
-    int32_t nt;
-};
+// Vertex-ring streams ("Vertex-ring streams").  A model's triangles are cut into streams, one
+// per wave of the fused workgroup.  A stream is a sequence of steps; a step is an optional vertex pass (<= 64
+// new vertices, transformed by one lane each into the wave's LDS vertex ring) followed by one batch of <= 64
+// triangles (one lane each).  The ring holds the last kVRing passes: pass p of a stream lives in ring buffer
+// p mod kVRing, and a triangle names its three vertices by ring slot (buffer * 64 + lane), 9 bits each.  The
+// builder guarantees that a batch issued after pass h references only passes h - 1 and h (kRefPasses = 2),
+// so a vertex is transformed once for every ~2 triangles (the 64-vertex meshlets of round 1 transformed one
+// per ~1.1), and a queued triangle record needs only its three slot numbers: before pass P overwrites the
+// buffer of pass P - kVRing, the kernel flushes the records that may still reference it.
+//   sverts: 64 float4 slots per vertex pass (x, y, z, 0), stream-major
+//   stris:  64 uint32 slots per step, i0 | i1 << 9 | i2 << 18 (ring slots; padding 0)
+//   ssteps: one uint32 header per step, nt | nv << 8 (nv = 0: no vertex pass)
+//   streams: int4 (first step, end step, first vertex pass, end vertex pass) per stream
+// All loads of a step are unconditional (the next step's triangle slots and the next unconsumed vertex pass
+// are prefetched while the current step runs), so the compiler counts them in vmcnt.
+constexpr int kStepSlots = 64;
+#ifndef PCORE_VRING
+#define PCORE_VRING 5
+#endif
+constexpr int kVRing = PCORE_VRING;    // vertex passes resident per wave
+constexpr int kRefPasses = 2;          // a batch references the last kRefPasses passes
+constexpr int kRingSlotBits = 9;       // kVRing * 64 <= 512
+#ifndef PCORE_FUSED_WAVES
+#define PCORE_FUSED_WAVES 4
+#endif
+constexpr int kFusedWaves = PCORE_FUSED_WAVES;  // waves per fused / cloud workgroup = streams per model
 
 // Fixed-radius neighbour grid over the observed points of one label (6-DoF) or of the whole cloud
 // (3-DoF).  Cells are >= 2 * sensor_resolution wide, so every point within the radius of a query lies
@@ -53,11 +62,13 @@ struct FusedArgs {
     const int32_t* pose_label;  // nullptr: 3-DoF
     const float* pose_obs_total;
     int32_t num_poses;
-    // mesh
-    const float4* mverts;   // 64 slots per meshlet (see Meshlet)
-    const uint32_t* mtris;  // 64 slots per meshlet
-    const int32_t* model_ml_lo;
-    const int32_t* model_ml_hi;
+    // mesh: vertex-ring streams (see kVRing above)
+    const float4* sverts;
+    const uint32_t* stris;
+    const uint32_t* ssteps;
+    const int4* streams;
+    const int32_t* model_st_lo;
+    const int32_t* model_st_hi;
     const float4* model_box;  // 2 per model: (min x, y, z, 1 if every vertex is finite), (max x, y, z, 0)
     int32_t num_models;
     // camera
@@ -85,7 +96,7 @@ struct FusedArgs {
     int32_t* cloud_count;
     int32_t cloud_cap;
     // colour gate of cost_type 1 (compute_costs.cuh:201-240); null / 0 otherwise
-    const uint32_t* mtri_orig;  // original triangle index of every meshlet triangle
+    const uint32_t* stri_orig;  // original triangle index of every stream triangle slot
     const float4* tri_lab;      // Lab of every original triangle's colour (reference channel order)
     const float4* obs_lab;      // Lab of every observed point, label-sorted order
     int32_t* cid;               // N x nsamp scratch: original triangle of each sample's nearest fragment

@@ -7,7 +7,7 @@
 //
 // Kernels
 //   fused_cost_kernel      stage COST: one workgroup per candidate pose; z-buffer of the stride-sampled
-//                          pixels kept in LDS, meshlet vertex transform, per-wave compaction of the
+//                          pixels kept in LDS, vertex-ring stream transform, per-wave compaction of the
 //                          (triangle, sample) work, source occlusion, unprojection, fixed-radius 1-NN and
 //                          the three per-pose costs.  No per-pose HBM traffic except 64 B of pose in and
 //                          12 B of costs out.
@@ -29,12 +29,12 @@
 namespace pcore {
 
 constexpr int kWave = 64;
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
-#ifndef PCORE_REC_CAP
-#define PCORE_REC_CAP 96
-#endif
-constexpr int kRecCap = PCORE_REC_CAP;  // per-wave circular ring of queued triangle records (flushed 64 at a time)
+constexpr int kWaves = kFusedWaves;  // waves per fused / cloud workgroup (one pose)
+constexpr int kThreads = kWaves * kWave;
+// per-wave circular ring of queued triangle records, flushed 64 at a time: after every full flush fewer than
+// 64 remain and a batch appends at most 64, so 128 never overflows; phase 2 reuses it as a point queue of
+// up to 127 (tile index, kx | ky << 16) pairs
+constexpr int kRecCap = 128;
 constexpr int64_t PCORE_KEY_NONE_DEV = 0x7fffffffffffffffLL;
 constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queued; larger ones are
                               // processed cooperatively by the whole wave
@@ -145,10 +145,11 @@ __device__ __forceinline__ int mbcnt64(uint64_t mask) {
 // Stage COST: fused sampled render + unproject + 1-NN + cost
 // ------------------------------------------------------------------------------------------------
 
-struct TriRec {  // 40 bytes: screen-space vertices, camera z, sample window
+struct TriRec {  // a triangle in registers: screen-space vertices, camera z
     float a0, a1, b0, b1, c0, c1, z0, z1, z2;
-    uint32_t meta;  // kx0 | ky0 << 12 | (nx-1) << 24 | (ny-1) << 28   (nx, ny <= kSmallK... or 16)
 };
+// A queued triangle in the LDS record ring (8 bytes): x = its three vertex-ring slots i0 | i1 << 9 | i2 << 18,
+// y = its sample window kx0 | ky0 << 12 | (nx-1) << 24 | (ny-1) << 28 (nx * ny <= kSmallK).
 
 template <int STRIDE>
 __device__ __forceinline__ int sdiv(int v, int s) {
@@ -177,16 +178,18 @@ __device__ __forceinline__ int sample_window(const float (&bmin)[2], const float
 }
 
 struct FusedSmem {
-    int32_t* zbuf;  // hs * ws
-    float* vx;      // kWaves * 64: screen x of the wave's meshlet vertices
-    float* vy;
-    float* vz;      // camera z (cm)
-    uint2* vwin;    // kWaves * 64: packed int16 sample-window bounds per vertex (see vertex_window)
-    TriRec* ring;   // kWaves * kRecCap (phase 1); reused as int32 point queues in phase 2
+    int32_t* zbuf;  // tile samples
+    float2* vxy;    // kWaves * kVRing * 64: screen (x, y) of the wave's vertex ring
+    float* vz;      // kWaves * kVRing * 64: camera z (cm)
+    uint2* ring;    // kWaves * kRecCap queued triangle records (phase 1); int32 point queues in phase 2
     uint32_t* ring_id;  // kWaves * kRecCap original triangle ids (colour id pass only)
     uint32_t* bitmap;
     int32_t* counters;  // [0] bad, [1] explained, [2] points
 };
+constexpr int kRingSlots = kVRing * kWave;
+static_assert(kRingSlots <= (1 << kRingSlotBits), "vertex ring slots must fit the 9-bit triangle indices");
+static_assert(kVRing > kRefPasses, "the ring must hold the referenced passes and the one being written");
+static_assert(kRecCap >= 128 && (kRecCap & (kRecCap - 1)) == 0, "record ring: >= 128 records, a power of two");
 
 // IDPASS = false: depth pass (atomicMin of the fragment depth).  IDPASS = true: colour id pass over the
 // final depths: the fragments whose depth equals the sample's minimum leave the lowest original triangle
@@ -216,9 +219,9 @@ __device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, i
 size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
     size_t b = al((size_t)tile_samples * 4);
-    b += al((size_t)kWaves * kWave * 4) * 3;
-    b += al((size_t)kWaves * kWave * 8);
-    b += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+    b += al((size_t)kWaves * kRingSlots * 8);
+    b += al((size_t)kWaves * kRingSlots * 4);
+    b += al((size_t)kWaves * kRecCap * 8);
     if (colour) b += al((size_t)kWaves * kRecCap * 4);
     b += al((size_t)bitmap_words * 4);
     b += 16;
@@ -231,11 +234,9 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
     FusedSmem sm;
     unsigned char* p = smem_raw;
     sm.zbuf = (int32_t*)p; p += al((size_t)nsamp * 4);
-    sm.vx = (float*)p; p += al((size_t)kWaves * kWave * 4);
-    sm.vy = (float*)p; p += al((size_t)kWaves * kWave * 4);
-    sm.vz = (float*)p; p += al((size_t)kWaves * kWave * 4);
-    sm.vwin = (uint2*)p; p += al((size_t)kWaves * kWave * 8);
-    sm.ring = (TriRec*)p; p += al((size_t)kWaves * kRecCap * sizeof(TriRec));
+    sm.vxy = (float2*)p; p += al((size_t)kWaves * kRingSlots * 8);
+    sm.vz = (float*)p; p += al((size_t)kWaves * kRingSlots * 4);
+    sm.ring = (uint2*)p; p += al((size_t)kWaves * kRecCap * 8);
     sm.ring_id = nullptr;
     if (colour) { sm.ring_id = (uint32_t*)p; p += al((size_t)kWaves * kRecCap * 4); }
     sm.bitmap = (uint32_t*)p; p += al((size_t)bitmap_words * 4);
@@ -252,45 +253,32 @@ __device__ __forceinline__ int floor_div(int v, int s) {
     }
 }
 
-// Per-vertex contribution to the sample window of every triangle that uses the vertex.  For finite
-// screen coordinates the window of sample_window() (reference bbox + loop bounds) decomposes over the
-// three vertices because every step is monotone: trunc(max(0, min p) + 0.5) = max(0, min trunc(p + 0.5)),
-// floor(min(W-1, max p)) = min(W-1, max floor p), and ceil/floor division by s are monotone.  Clamping
-// p to +-65536 first changes no window of a <= 16384-pixel image and keeps every bound in int16.
-//   lo = (ceil(trunc(sx+0.5)/s), ceil((H-1-floor(sy))/s)),  hi = (floor(floor(sx)/s), floor((H-1-trunc(sy+0.5))/s))
-// A triangle's window is kx in [max(0, min lo.x), min(ws-1, max hi.x)] (same for y).
+// Sample window of a triangle whose screen coordinates are not NaN (finite or infinite), straight from the
+// reference's bounding box and loop bounds (image_renderer.cuh:86-111): bmin = max(0, min p), first pixel
+// trunc(bmin + 0.5); bmax = min(W-1, max p), last pixel floor(bmax) -- for non-NaN inputs the ternary chains
+// of bbox_ref() are exactly these min / max.  Clamping to [0, 65536] / [-65536, W-1] first changes no window
+// of a <= 16384-pixel image and keeps the conversions in range.  Sample kx covers raster column kx * s,
+// sample row ky raster row H-1-ky*s.  The window is clipped to the pose window; returns its sample count.
 template <int STRIDE>
-__device__ __forceinline__ uint2 vertex_window(float sx, float sy, int s, int H) {
-    const float cx = fminf(fmaxf(sx, -65536.0f), 65536.0f);
-    const float cy = fminf(fmaxf(sy, -65536.0f), 65536.0f);
-    const int tx = (int)(cx + 0.5f), fx = (int)floorf(cx);
-    const int ty = (int)(cy + 0.5f), fy = (int)floorf(cy);
-    const int lox = -floor_div<STRIDE>(-tx, s);
-    const int loy = -floor_div<STRIDE>(fy - (H - 1), s);
-    const int hix = floor_div<STRIDE>(fx, s);
-    const int hiy = floor_div<STRIDE>(H - 1 - ty, s);
-    return make_uint2(((uint32_t)lox & 0xffffu) | ((uint32_t)loy << 16), ((uint32_t)hix & 0xffffu) | ((uint32_t)hiy << 16));
-}
-
-typedef short short2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
-
-// One meshlet's loads for one lane: vertex slot, triangle slot (and original triangle id for the colour id
-// pass), unconditionally (pcore_internal.h, Meshlet) -- the compiler then counts them in vmcnt, and the
-// prefetch of the next meshlet stays in flight while the current one is processed.
-struct MeshletLanes {
-    float4 v;
-    uint32_t pk, id;
-};
-template <bool IDPASS>
-__device__ __forceinline__ MeshletLanes load_meshlet_lanes(const FusedArgs& a, int m, int lane) {
-    const size_t k = (size_t)m * kMeshletSlots + lane;
-    MeshletLanes r;
-    r.v = a.mverts[k];
-    r.pk = a.mtris[k];
-    r.id = IDPASS ? a.mtri_orig[k] : 0u;
-    return r;
+__device__ __forceinline__ int triangle_window(float x0, float x1, float x2, float y0, float y1, float y2, int s,
+                                               float cmax0, float cmax1, int H, const SampleWin& sw, int& kx0,
+                                               int& ky0, int& nx, int& ny) {
+    const float mnx = fminf(x0, fminf(x1, x2)), mxx = fmaxf(x0, fmaxf(x1, x2));
+    const float mny = fminf(y0, fminf(y1, y2)), mxy = fmaxf(y0, fmaxf(y1, y2));
+    const int lo0 = (int)(fminf(fmaxf(mnx, 0.0f), 65536.0f) + 0.5f);
+    const int lo1 = (int)(fminf(fmaxf(mny, 0.0f), 65536.0f) + 0.5f);
+    const int hi0 = (int)floorf(fmaxf(fminf(mxx, cmax0), -65536.0f));
+    const int hi1 = (int)floorf(fmaxf(fminf(mxy, cmax1), -65536.0f));
+    const int ss = STRIDE > 0 ? STRIDE : s;
+    const int a0 = max(floor_div<STRIDE>(lo0 + ss - 1, s), sw.x0);          // lo0 >= 0: ceil
+    const int a1 = min(floor_div<STRIDE>(hi0, s), sw.x0 + sw.nx - 1);
+    const int b0 = max(floor_div<STRIDE>(H - 1 - hi1 + ss - 1, s), sw.y0);  // H-1-hi1 >= 0: ceil
+    const int b1 = min(floor_div<STRIDE>(H - 1 - lo1, s), sw.y0 + sw.ny - 1);
+    kx0 = a0;
+    ky0 = b0;
+    nx = a1 - a0 + 1;
+    ny = b1 - b0 + 1;
+    return (nx > 0 && ny > 0) ? nx * ny : 0;
 }
 
 // Measurement build only (-DPCORE_FUSED_PROFILE, tools/fused_phase_prof.py): per-wave shader clocks of the
@@ -329,9 +317,9 @@ struct FProf {
 
 #ifdef PCORE_FLUSH_STATS
 // measurement build only: small-triangle flush batches, records, fragment tests, loop trips
-__device__ unsigned long long pcore_flush_stats[8];
+__device__ unsigned long long pcore_flush_stats[9];
 extern "C" int pcore_debug_flush_stats(unsigned long long* host) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcore_flush_stats), sizeof(unsigned long long) * 8);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcore_flush_stats), sizeof(unsigned long long) * 9);
 }
 #endif
 
@@ -339,7 +327,7 @@ template <int STRIDE, bool IDPASS = false>
 __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw,
                                              int32_t* cid, FProf& fp) {
     const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of meshlet headers
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of stream headers
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int W = a.width, H = a.height;
@@ -354,204 +342,216 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     // ---------------- phase 1: raster of the sampled pixels ----------------
     const float Wf = (float)W, Hf = (float)H;
     const float cmax0 = (float)(W - 1), cmax1 = (float)(H - 1);
-    float* vx = sm.vx + wave * kWave;
-    float* vy = sm.vy + wave * kWave;
-    float* vz = sm.vz + wave * kWave;
-    uint2* vwin = sm.vwin + wave * kWave;
-    TriRec* ring = sm.ring + wave * kRecCap;
+    float2* vxy = sm.vxy + wave * kRingSlots;
+    float* vz = sm.vz + wave * kRingSlots;
+    uint2* ring = sm.ring + wave * kRecCap;
     uint32_t* ring_id = IDPASS ? sm.ring_id + wave * kRecCap : nullptr;
-    // every triangle window is clipped to the pose window (a no-op when the window is conservative, and the
-    // bound that keeps the tile indexing in range whatever the input)
-    const short2v wzero = {(short)sw.x0, (short)sw.y0};
-    const short2v wlim = {(short)(sw.x0 + sw.nx - 1), (short)(sw.y0 + sw.ny - 1)};
-    // circular ring of queued small triangles: records [rec_head, rec_head + rec_count) modulo kRecCap;
-    // flushed 64 at a time, so that every fragment-test batch fills the wave (a partial batch only when an
-    // append would overflow the ring, and at the end)
-    int rec_head = 0, rec_count = 0;  // wave-uniform
+    // record ring: wave-uniform monotone counters of appended and flushed records; record i lives in slot
+    // i mod kRecCap.  Full 64-record batches are flushed as soon as they exist; a partial batch only when a
+    // vertex pass would overwrite vertices a pending record may reference, at a stream switch and at the end.
+    int rec_total = 0, rec_done = 0;
 
     const int dbg = a.dbg_skip;
-    auto ring_slot = [&](int i) { return i >= kRecCap ? i - kRecCap : i; };  // i < 2 kRecCap
-    auto flush = [&](int head, int count) {
+    auto flush = [&](int count) {  // the `count` oldest pending records
         fp.mark(2);
         wave_sync();
-        if (dbg & 1) return;
-        for (int base = 0; base < count; base += kWave) {
-            const int j = ring_slot(head + min(base + lane, count - 1));
+        if (!(dbg & 1)) {
+            for (int base = 0; base < count; base += kWave) {
 #ifdef PCORE_FLUSH_STATS
-            {
-                const bool in = base + lane < count;
-                const TriRec rs = ring[j];
-                const int nxs = ((rs.meta >> 24) & 0xf) + 1, nys = ((rs.meta >> 28) & 0xf) + 1;
-                const int nks = in ? nxs * nys : 0;
-                int mx_ny = in ? nys : 0, mx_nx = in ? nxs : 0;
-                int sum = nks;
-                for (int o = 32; o > 0; o >>= 1) {
-                    mx_ny = max(mx_ny, __shfl_xor(mx_ny, o));
-                    mx_nx = max(mx_nx, __shfl_xor(mx_nx, o));
-                    sum += __shfl_xor(sum, o);
-                }
                 if (lane == 0) {
-                    atomicAdd(&pcore_flush_stats[0], 1ull);                             // 64-lane batches
-                    atomicAdd(&pcore_flush_stats[1], (unsigned long long)min(count - base, kWave));  // records
-                    atomicAdd(&pcore_flush_stats[2], (unsigned long long)sum);          // fragment tests
-                    atomicAdd(&pcore_flush_stats[3], (unsigned long long)(mx_ny * mx_nx));  // loop trips (upper)
+                    atomicAdd(&pcore_flush_stats[0], 1ull);
+                    atomicAdd(&pcore_flush_stats[1], (unsigned long long)min(count - base, kWave));
                 }
-            }
 #endif
-            if (base + lane < count) {
-                const TriRec r = ring[j];
-                const uint32_t id = IDPASS ? ring_id[j] : 0u;
-                const int kx0 = r.meta & 0xfff, ky0 = (r.meta >> 12) & 0xfff;
-                const int nx = ((r.meta >> 24) & 0xf) + 1, ny = ((r.meta >> 28) & 0xf) + 1;
-                for (int iy = 0; iy < ny; iy++)
-                    for (int ix = 0; ix < nx; ix++)
-                        raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
+                if (base + lane < count) {
+                    const int j = (rec_done + base + lane) & (kRecCap - 1);
+                    const uint2 rec = ring[j];
+                    const uint32_t id = IDPASS ? ring_id[j] : 0u;
+                    const int i0 = rec.x & 511, i1 = (rec.x >> 9) & 511, i2 = (rec.x >> 18) & 511;
+                    const float2 q0 = vxy[i0], q1 = vxy[i1], q2 = vxy[i2];
+                    TriRec r;
+                    r.a0 = q0.x; r.a1 = q0.y;
+                    r.b0 = q1.x; r.b1 = q1.y;
+                    r.c0 = q2.x; r.c1 = q2.y;
+                    r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
+                    const int kx0 = rec.y & 0xfff, ky0 = (rec.y >> 12) & 0xfff;
+                    const int nx = ((rec.y >> 24) & 0xf) + 1, ny = ((rec.y >> 28) & 0xf) + 1;
+#ifdef PCORE_FLUSH_STATS
+                    atomicAdd(&pcore_flush_stats[2], (unsigned long long)(nx * ny));
+#endif
+                    for (int iy = 0; iy < ny; iy++)
+                        for (int ix = 0; ix < nx; ix++)
+                            raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
+                }
             }
         }
+        rec_done += count;
         wave_sync();
         fp.mark(3);
     };
 
     if (model < 0 || model >= a.num_models) return;
-    const int ml_lo = a.model_ml_lo[model], ml_hi = a.model_ml_hi[model];
-    int m = ml_lo + wave;
-    MeshletLanes cur = {make_float4(0.f, 0.f, 0.f, 0.f), 0u, 0u};
-    if (m < ml_hi) cur = load_meshlet_lanes<IDPASS>(a, m, lane);
+    const int st_lo = a.model_st_lo[model], st_hi = a.model_st_hi[model];
     fp.mark(0);
-    for (; m < ml_hi; m += kWaves) {
-        // prefetch the next meshlet of this wave while this one is processed (the last one re-loads itself:
-        // every load is unconditional, so the wait below covers only the current meshlet's loads)
-        const MeshletLanes nxt = load_meshlet_lanes<IDPASS>(a, min(m + kWaves, ml_hi - 1), lane);
-        const float4 v = cur.v;
-        const uint32_t meta = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(v.w));
-        const int ml_nv = (int)(meta & 0xffu), ml_nt = (int)((meta >> 8) & 0xffu);
-        // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
-        // (image_renderer.cuh:296-305, 82-84)
-        bool bad_vertex = false;
-        if (lane < ml_nv && !(dbg & 8)) {
-            const float lx = row4(m00, m01, m02, m03, v.x, v.y, v.z);
-            const float ly = row4(m10, m11, m12, m13, v.x, v.y, v.z);
-            const float lz = row4(m20, m21, m22, m23, v.x, v.y, v.z);
-            const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
-            const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
-            // px / lz and py / lz, IEEE-exact, sharing one refined reciprocal of lz (pcore_fdiv.h)
-            float qx, qy;
-            fdiv2_exact(px, py, lz, qx, qy);
-            const float sx = qx * Wf / 2.0f + Wf / 2.0f;
-            const float sy = qy * Hf / 2.0f + Hf / 2.0f;
-            vx[lane] = sx;
-            vy[lane] = sy;
-            vz[lane] = lz;
-            vwin[lane] = vertex_window<STRIDE>(sx, sy, s, H);
-            bad_vertex = !(sx == sx) || !(sy == sy);
+    for (int st = st_lo + wave; st < st_hi; st += kWaves) {
+        const int4 sd = a.streams[st];  // first step, end step, first vertex pass, end vertex pass
+        if (rec_total > rec_done) {      // a new stream numbers its ring slots from buffer 0
+#ifdef PCORE_FLUSH_STATS
+            if (lane == 0) atomicAdd(&pcore_flush_stats[3], 1ull);
+#endif
+            flush(rec_total - rec_done);
         }
-        const uint64_t nanmask = __ballot(bad_vertex);
-        wave_sync();
-        fp.mark(1);
-        if (!(dbg & 2)) {
-            const int t = lane;
-            const uint32_t pk = cur.pk;
-            const uint32_t oid = cur.id;
-            int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
-            int i0 = 0, i1 = 0, i2 = 0;
-            TriRec r;
-            if (t < ml_nt) {
-                i0 = pk & 0xff; i1 = (pk >> 8) & 0xff; i2 = (pk >> 16) & 0xff;
-                // the record's vertex data is read with the windows, whether or not the triangle touches a
-                // sample: one LDS round trip instead of two (most waves have some touching lane anyway)
-                const uint2 w0 = vwin[i0], w1 = vwin[i1], w2 = vwin[i2];
-                r.a0 = vx[i0]; r.a1 = vy[i0];
-                r.b0 = vx[i1]; r.b1 = vy[i1];
-                r.c0 = vx[i2]; r.c1 = vy[i2];
-                r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
-                const bool nan_tri = nanmask != 0 && (((nanmask >> i0) | (nanmask >> i1) | (nanmask >> i2)) & 1ull);
-                if (!nan_tri) {
-                    short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
-                    short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
-                    lo = __builtin_elementwise_max(lo, wzero);
-                    hi = __builtin_elementwise_min(hi, wlim);
-                    kx0 = lo.x; ky0 = lo.y;
-                    nx = (int)hi.x - (int)lo.x + 1;
-                    ny = (int)hi.y - (int)lo.y + 1;
-                    nk = (nx > 0 && ny > 0) ? nx * ny : 0;
-                } else {
-                    // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
-                    const float p[3][2] = {{r.a0, r.a1}, {r.b0, r.b1}, {r.c0, r.c1}};
-                    float bmin[2], bmax[2];
-                    bbox_ref(p, cmax0, cmax1, bmin, bmax);
-                    nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
-                    if (nk > 0) {  // clip to the pose window
-                        const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
-                        kx0 = max(kx0, sw.x0);
-                        ky0 = max(ky0, sw.y0);
-                        nx = kx1 - kx0;
-                        ny = ky1 - ky0;
-                        nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+        // hist[k]: rec_total when pass P-1-k was written (P = the next pass).  A batch issued after pass h
+        // references passes >= h - kRefPasses + 1, so before pass P overwrites the buffer of pass P - kVRing every
+        // record appended before pass P - (kVRing - kRefPasses) was written must be flushed.
+        int hist[kVRing - kRefPasses];
+#pragma unroll
+        for (int k = 0; k < kVRing - kRefPasses; k++) hist[k] = rec_total;
+        int buf = 0;                 // ring buffer of the next vertex pass
+        int vp = sd.z;               // next vertex pass to consume
+        const int vp_last = max(sd.w - 1, sd.z);
+        float4 cv = a.sverts[(size_t)min(vp, vp_last) * kStepSlots + lane];
+        uint32_t ct = a.stris[(size_t)sd.x * kStepSlots + lane];
+        uint32_t cidt = IDPASS ? a.stri_orig[(size_t)sd.x * kStepSlots + lane] : 0u;
+        uint32_t hdr = a.ssteps[sd.x];
+        for (int step = sd.x; step < sd.y; step++) {
+            // prefetch the next step's triangles and the next unconsumed vertex pass (unconditional loads; the
+            // last step re-loads itself)
+            const int ns = min(step + 1, sd.y - 1);
+            const uint32_t nct = a.stris[(size_t)ns * kStepSlots + lane];
+            const uint32_t ncid = IDPASS ? a.stri_orig[(size_t)ns * kStepSlots + lane] : 0u;
+            const uint32_t nhdr = a.ssteps[ns];
+            const int nv = (int)((hdr >> 8) & 0xffu), ntri = (int)(hdr & 0xffu);
+            const int vp_next = vp + (nv > 0 ? 1 : 0);
+            const float4 ncv = a.sverts[(size_t)min(vp_next, vp_last) * kStepSlots + lane];
+            if (nv > 0) {
+                if (rec_done < hist[kVRing - kRefPasses - 1]) {
+#ifdef PCORE_FLUSH_STATS
+                    if (lane == 0) atomicAdd(&pcore_flush_stats[3], 1ull);
+#endif
+                    flush(rec_total - rec_done);
+                }
+                // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
+                // (image_renderer.cuh:296-305, 82-84)
+                if (lane < nv && !(dbg & 8)) {
+                    const float lx = row4(m00, m01, m02, m03, cv.x, cv.y, cv.z);
+                    const float ly = row4(m10, m11, m12, m13, cv.x, cv.y, cv.z);
+                    const float lz = row4(m20, m21, m22, m23, cv.x, cv.y, cv.z);
+                    const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
+                    const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
+                    // px / lz and py / lz, IEEE-exact, sharing one refined reciprocal of lz (pcore_fdiv.h)
+                    float qx, qy;
+                    fdiv2_exact(px, py, lz, qx, qy);
+                    const float sx = qx * Wf / 2.0f + Wf / 2.0f;
+                    const float sy = qy * Hf / 2.0f + Hf / 2.0f;
+                    vxy[buf * kWave + lane] = make_float2(sx, sy);
+                    vz[buf * kWave + lane] = lz;
+                }
+#pragma unroll
+                for (int k = kVRing - kRefPasses - 1; k > 0; k--) hist[k] = hist[k - 1];
+                hist[0] = rec_total;
+                buf = buf + 1 == kVRing ? 0 : buf + 1;
+#ifdef PCORE_FLUSH_STATS
+                if (lane == 0) atomicAdd(&pcore_flush_stats[8], 1ull);
+#endif
+                wave_sync();
+            }
+            fp.mark(1);
+            if (!(dbg & 2)) {
+                int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
+                const uint32_t tri = ct & 0x7ffffffu;
+                const int i0 = (int)(ct & 511u), i1 = (int)((ct >> 9) & 511u), i2 = (int)((ct >> 18) & 511u);
+                float2 q0 = make_float2(0.f, 0.f), q1 = q0, q2 = q0;
+                if (lane < ntri) {
+                    q0 = vxy[i0];
+                    q1 = vxy[i1];
+                    q2 = vxy[i2];
+                    const bool nan_tri = (q0.x != q0.x) || (q0.y != q0.y) || (q1.x != q1.x) || (q1.y != q1.y) ||
+                                         (q2.x != q2.x) || (q2.y != q2.y);
+                    if (!nan_tri) {
+                        nk = triangle_window<STRIDE>(q0.x, q1.x, q2.x, q0.y, q1.y, q2.y, s, cmax0, cmax1, H, sw, kx0,
+                                                     ky0, nx, ny);
+                    } else {
+                        // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
+                        const float p[3][2] = {{q0.x, q0.y}, {q1.x, q1.y}, {q2.x, q2.y}};
+                        float bmin[2], bmax[2];
+                        bbox_ref(p, cmax0, cmax1, bmin, bmax);
+                        nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
+                        if (nk > 0) {  // clip to the pose window
+                            const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
+                            kx0 = max(kx0, sw.x0);
+                            ky0 = max(ky0, sw.y0);
+                            nx = kx1 - kx0;
+                            ny = ky1 - ky0;
+                            nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+                        }
                     }
                 }
-            }
-            // large triangles: whole-wave cooperative
-            uint64_t big = __ballot(nk > kSmallK);
+                // large triangles: whole-wave cooperative
+                uint64_t big = __ballot(nk > kSmallK);
 #ifdef PCORE_FLUSH_STATS
-            {
-                const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(t < ml_nt);
-                if (lane == 0) {
-                    atomicAdd(&pcore_flush_stats[4], (unsigned long long)__popcll(big));
-                    atomicAdd(&pcore_flush_stats[5], (unsigned long long)__popcll(btouch));
-                    atomicAdd(&pcore_flush_stats[6], (unsigned long long)__popcll(blanes));
-                    atomicAdd(&pcore_flush_stats[7], 1ull);
+                {
+                    const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(lane < ntri);
+                    if (lane == 0) {
+                        atomicAdd(&pcore_flush_stats[4], (unsigned long long)__popcll(big));
+                        atomicAdd(&pcore_flush_stats[5], (unsigned long long)__popcll(btouch));
+                        atomicAdd(&pcore_flush_stats[6], (unsigned long long)__popcll(blanes));
+                        atomicAdd(&pcore_flush_stats[7], 1ull);
+                    }
                 }
-            }
 #endif
-            while (big) {
-                const int j = __ffsll((unsigned long long)big) - 1;
-                big &= big - 1;
-                // j is wave-uniform: v_readlane into SGPRs (no LDS round trip)
-                auto rl = [&](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j)); };
-                TriRec rb;
-                rb.a0 = rl(r.a0); rb.a1 = rl(r.a1);
-                rb.b0 = rl(r.b0); rb.b1 = rl(r.b1);
-                rb.c0 = rl(r.c0); rb.c1 = rl(r.c1);
-                rb.z0 = rl(r.z0); rb.z1 = rl(r.z1); rb.z2 = rl(r.z2);
-                const int bkx0 = __builtin_amdgcn_readlane(kx0, j), bky0 = __builtin_amdgcn_readlane(ky0, j);
-                const int bnx = __builtin_amdgcn_readlane(nx, j), bnk = __builtin_amdgcn_readlane(nk, j);
-                const uint32_t bid = IDPASS ? (uint32_t)__builtin_amdgcn_readlane((int)oid, j) : 0u;
-                // q / bnx without an integer division: the float quotient is within 1e-3 of q / bnx (q / bnx
-                // is at most the sample rows), so one correction step gives the exact row
-                const float inv_nx = 1.0f / (float)bnx;
-                for (int q = lane; q < bnk; q += kWave) {
-                    int iy = (int)(((float)q + 0.5f) * inv_nx), ix = q - iy * bnx;
-                    if (ix < 0) { iy--; ix += bnx; } else if (ix >= bnx) { iy++; ix -= bnx; }
-                    raster_sample<IDPASS>(rb, bkx0 + ix, bky0 + iy, s, H, sw, sm.zbuf, cid, bid);
+                if (big) {
+                    float z0 = 0.0f, z1 = 0.0f, z2 = 0.0f;
+                    if (nk > kSmallK) {
+                        z0 = vz[i0];
+                        z1 = vz[i1];
+                        z2 = vz[i2];
+                    }
+                    do {
+                        const int j = __ffsll((unsigned long long)big) - 1;
+                        big &= big - 1;
+                        // j is wave-uniform: v_readlane into SGPRs (no LDS round trip)
+                        auto rl = [&](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j)); };
+                        TriRec rb;
+                        rb.a0 = rl(q0.x); rb.a1 = rl(q0.y);
+                        rb.b0 = rl(q1.x); rb.b1 = rl(q1.y);
+                        rb.c0 = rl(q2.x); rb.c1 = rl(q2.y);
+                        rb.z0 = rl(z0); rb.z1 = rl(z1); rb.z2 = rl(z2);
+                        const int bkx0 = __builtin_amdgcn_readlane(kx0, j), bky0 = __builtin_amdgcn_readlane(ky0, j);
+                        const int bnx = __builtin_amdgcn_readlane(nx, j), bnk = __builtin_amdgcn_readlane(nk, j);
+                        const uint32_t bid = IDPASS ? (uint32_t)__builtin_amdgcn_readlane((int)cidt, j) : 0u;
+                        // q / bnx without an integer division: the float quotient is within 1e-3 of q / bnx (q / bnx
+                        // is at most the sample rows), so one correction step gives the exact row
+                        const float inv_nx = 1.0f / (float)bnx;
+                        for (int q = lane; q < bnk; q += kWave) {
+                            int iy = (int)(((float)q + 0.5f) * inv_nx), ix = q - iy * bnx;
+                            if (ix < 0) { iy--; ix += bnx; } else if (ix >= bnx) { iy++; ix -= bnx; }
+                            raster_sample<IDPASS>(rb, bkx0 + ix, bky0 + iy, s, H, sw, sm.zbuf, cid, bid);
+                        }
+                    } while (big);
                 }
+                // small triangles: queue into the wave's record ring
+                const bool qd = nk > 0 && nk <= kSmallK;
+                const uint64_t bq = __ballot(qd);
+                if (qd) {
+                    const uint32_t meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) |
+                                          ((uint32_t)(ny - 1) << 28);
+                    const int slot = (rec_total + mbcnt64(bq)) & (kRecCap - 1);
+                    ring[slot] = make_uint2(tri, meta);
+                    if (IDPASS) ring_id[slot] = cidt;
+                }
+                rec_total += __popcll(bq);
+                while (rec_total - rec_done >= kWave) flush(kWave);  // full batches only
             }
-            // small triangles: queue into the wave's ring
-            const bool qd = nk > 0 && nk <= kSmallK;
-            const uint64_t bq = __ballot(qd);
-            const int nq = __popcll(bq);
-            if (rec_count + nq > kRecCap) {  // rare: more queued than the ring holds -> partial batch first
-                flush(rec_head, rec_count);
-                rec_head = 0;
-                rec_count = 0;
-            }
-            if (qd) {
-                r.meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) | ((uint32_t)(ny - 1) << 28);
-                const int slot = ring_slot(rec_head + rec_count + mbcnt64(bq));
-                ring[slot] = r;
-                if (IDPASS) ring_id[slot] = oid;
-            }
-            rec_count += nq;
-            while (rec_count >= kWave) {  // full batches only
-                flush(rec_head, kWave);
-                rec_head = ring_slot(rec_head + kWave);
-                rec_count -= kWave;
-            }
+            fp.mark(2);
+            cv = ncv;
+            vp = vp_next;
+            ct = nct;
+            cidt = ncid;
+            hdr = nhdr;
         }
-        wave_sync();  // vertex slots are rewritten by the next meshlet
-        fp.mark(2);
-        cur = nxt;
     }
-    if (rec_count > 0) flush(rec_head, rec_count);
+    if (rec_total > rec_done) flush(rec_total - rec_done);
 }
 
 // Conservative sample window of a pose ("Pose windows").  Lanes 0-7 of every wave project the
@@ -643,7 +643,7 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
 
     // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
     // per-wave point queue in the (now free) triangle ring: (tile index, kx | ky << 16) pairs
-    int32_t* queue = reinterpret_cast<int32_t*>(sm.ring) + wave * (kRecCap * (int)sizeof(TriRec) / 4);
+    int32_t* queue = reinterpret_cast<int32_t*>(sm.ring + wave * kRecCap);  // <= 127 pairs (kRecCap >= 128)
     int qcount = 0;
     const int grid_id = use_seg ? pl : a.num_grids;
     const bool grid_ok = use_seg ? (pl >= 0 && pl < a.num_grids) : true;

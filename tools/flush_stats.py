@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Small-triangle flush statistics of the fused kernel (C2 workload) from a -DPCORE_FLUSH_STATS build
-(PCORE_LIB=build_ab/fst.so), one launch: 64-lane flush batches, queued records, fragment tests, the loop
-trips the batches execute (max nx x max ny over the batch's lanes), big (cooperative) triangles,
-triangles touching a sample, triangle lanes and triangle half-passes."""
+(PCORE_LIB=build_ab/fst.so), one launch, per pose: flush batches (64 lanes), queued records, fragment tests,
+partial flushes forced by the vertex ring or a stream switch, big (cooperative) triangles, triangles touching
+a sample, triangle lanes, triangle batches (steps) and vertex passes."""
 import ctypes
 import json
 import os
@@ -21,14 +21,15 @@ w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.
 torch.cuda.synchronize()
 L = _native.load()
 L.pcore_debug_flush_stats.argtypes = [ctypes.c_void_p]
-base = np.zeros(8, dtype=np.uint64)
+base = np.zeros(9, dtype=np.uint64)
 assert L.pcore_debug_flush_stats(base.ctypes.data) == 0
 w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
 torch.cuda.synchronize()
-after = np.zeros(8, dtype=np.uint64)
+after = np.zeros(9, dtype=np.uint64)
 assert L.pcore_debug_flush_stats(after.ctypes.data) == 0
 d = (after - base).astype(np.int64) / 10000.0
-names = ["batches", "records", "frag_tests", "loop_trips", "big_tris", "tris_touching", "tri_lanes", "tri_passes"]
+names = ["batches", "records", "frag_tests", "forced_flushes", "big_tris", "tris_touching", "tri_lanes", "tri_steps",
+         "vertex_passes"]
 res = {k: float(v) for k, v in zip(names, d)}
-res["lane_util_flush"] = res["frag_tests"] / max(res["loop_trips"] * 64, 1)
+res["lane_util_flush"] = res["records"] / max(res["batches"] * 64, 1)
 print(json.dumps({"per_pose": res}))

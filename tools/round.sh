@@ -1,9 +1,11 @@
 #!/bin/bash
-# Full GPU session: parity tests, smoke, bench, rocprofv3 kernel-trace summary of the bench command,
-# and the two PMC passes (FETCH_SIZE, WRITE_SIZE) of the same command.  Every GPU step has its own
-# time limit; the chain stops at the first failure.
+# Full GPU session: parity tests, smoke, the counter passes that the bench line's roofline reads (two PMC
+# passes FETCH_SIZE / WRITE_SIZE -> profiles/pmc_traffic.json, three SQ passes -> profiles/sq_counters.json,
+# both tagged with the kernel-source digest), the bench itself, and the rocprofv3 kernel-trace summary of the
+# same bench command.  The folded json files are copied to $OUT (gpurun_out/ comes back; profiles/ on the box
+# does not).  Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
-OUT=${OUT:-gpurun_out}; TAG=${TAG:-r01}
+OUT=${OUT:-gpurun_out}; TAG=${TAG:-r02}
 mkdir -p $OUT; export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
   echo "== pytest"
@@ -13,16 +15,22 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -30 $OUT/smoke_$TAG.log; exit 1; }
   cat $OUT/smoke_$TAG.log
 fi
+if [ -z "$SKIP_PMC" ]; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "== pmc $C"
+    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${TAG}_$C -o run -- python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmc_${TAG}_$C.json 2> $OUT/pmc_${TAG}_$C.err || { tail -20 $OUT/pmc_${TAG}_$C.err; exit 1; }
+  done
+  python tools/pmc_traffic.py $OUT/pmc_${TAG}_FETCH_SIZE/run_counter_collection.csv $OUT/pmc_${TAG}_WRITE_SIZE/run_counter_collection.csv profiles/pmc_traffic.json || exit 1
+  cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
+  echo "== sq counters"
+  OUT=$OUT TAG=sq_$TAG bash tools/sq_counters.sh || exit 1
+  python tools/sq_json.py $OUT sq_$TAG 10000 || exit 1
+  cp profiles/sq_counters.json $OUT/sq_counters.json
+fi
 echo "== bench"
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -20 $OUT/bench_$TAG.err; exit 1; }
 cat $OUT/bench_$TAG.json
 echo "== rocprof stats"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python bench.py --no-cpu ${BENCH_ARGS} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
 cat $OUT/prof_bench_$TAG.json
-if [ -z "$SKIP_PMC" ]; then
-  for C in FETCH_SIZE WRITE_SIZE; do
-    echo "== pmc $C"
-    timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${TAG}_$C -o run -- python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmc_${TAG}_$C.json 2> $OUT/pmc_${TAG}_$C.err || { tail -20 $OUT/pmc_${TAG}_$C.err; exit 1; }
-  done
-fi
 find $OUT -path "*_$TAG*" -name "*.csv" | head -20
