@@ -40,7 +40,7 @@ struct pcore_ctx {
     DevBuf<float> tris;          // original triangle soup (parity render)
     DevBuf<int32_t> tri_lo, tri_hi;
     DevBuf<float4> sverts;       // vertex-ring streams (pcore_internal.h, kVRing)
-    DevBuf<uint32_t> stris, ssteps;
+    DevBuf<uint32_t> stris;
     DevBuf<int4> streams;
     DevBuf<int32_t> model_st_lo, model_st_hi;
     DevBuf<float4> model_box;  // FusedArgs::model_box
@@ -292,7 +292,7 @@ void pcore_destroy(pcore_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)dev_free(c->tris); (void)dev_free(c->tri_lo); (void)dev_free(c->tri_hi);
-    (void)dev_free(c->sverts); (void)dev_free(c->stris); (void)dev_free(c->ssteps); (void)dev_free(c->streams);
+    (void)dev_free(c->sverts); (void)dev_free(c->stris); (void)dev_free(c->streams);
     (void)dev_free(c->model_st_lo); (void)dev_free(c->model_st_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
     (void)dev_free(c->ovf_list); (void)dev_free(c->ovf_ctr); (void)dev_free(c->win_hist);
     if (c->fb_host) (void)hipHostFree(c->fb_host);
@@ -383,7 +383,6 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     if (!sd.empty()) std::memcpy(sd.data(), sb.streams.data(), sd.size() * sizeof(int4));
     HIPC(c, dev_upload(c->sverts, sv));
     HIPC(c, dev_upload(c->stris, sb.stris));
-    HIPC(c, dev_upload(c->ssteps, sb.ssteps));
     HIPC(c, dev_upload(c->streams, sd));
     HIPC(c, dev_upload(c->stri_orig, sb.sorig));
     std::vector<float4> tl((size_t)num_tris);
@@ -745,7 +744,6 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     a.num_poses = num_poses;
     a.sverts = c->sverts.p;
     a.stris = c->stris.p;
-    a.ssteps = c->ssteps.p;
     a.streams = c->streams.p;
     a.model_st_lo = c->model_st_lo.p;
     a.model_st_hi = c->model_st_hi.p;
@@ -795,7 +793,6 @@ static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& 
     a = FusedArgs{};
     a.sverts = c->sverts.p;
     a.stris = c->stris.p;
-    a.ssteps = c->ssteps.p;
     a.streams = c->streams.p;
     a.model_st_lo = c->model_st_lo.p;
     a.model_st_hi = c->model_st_hi.p;

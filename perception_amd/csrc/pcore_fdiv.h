@@ -42,6 +42,17 @@ __device__ __forceinline__ uint32_t fexp_bits(float x) { return (__float_as_uint
 // every biased exponent in [87, 167]: the unscaled steps equal the IEEE expansion
 __device__ __forceinline__ bool fdiv_range_ok(uint32_t emin, uint32_t emax) { return emin >= 87u && emax <= 167u; }
 
+// a / b, IEEE-exact
+__device__ __forceinline__ float fdiv_exact(float a, float b) {
+    const uint32_t ea = fexp_bits(a), eb = fexp_bits(b);
+    float q = quot_refined(a, b, recip_refined(b));
+    if (!fdiv_range_ok(min(ea, eb), max(ea, eb))) {
+        asm volatile("");
+        q = a / b;
+    }
+    return q;
+}
+
 // q0 = a0 / b, q1 = a1 / b, IEEE-exact
 __device__ __forceinline__ void fdiv2_exact(float a0, float a1, float b, float& q0, float& q1) {
     const uint32_t e0 = fexp_bits(a0), e1 = fexp_bits(a1), eb = fexp_bits(b);

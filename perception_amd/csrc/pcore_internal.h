@@ -15,9 +15,9 @@ namespace pcore {
 // so a vertex is transformed once for every ~2 triangles (the 64-vertex meshlets of round 1 transformed one
 // per ~1.1), and a queued triangle record needs only its three slot numbers: before pass P overwrites the
 // buffer of pass P - kVRing, the kernel flushes the records that may still reference it.
-//   sverts: 64 float4 slots per vertex pass (x, y, z, 0), stream-major
-//   stris:  64 uint32 slots per step, i0 | i1 << 9 | i2 << 18 (ring slots; padding 0)
-//   ssteps: one uint32 header per step, nt | nv << 8 (nv = 0: no vertex pass)
+//   sverts: 64 float4 slots per vertex pass (x, y, z, w), stream-major; w = 1 for a vertex, 0 for padding
+//   stris:  64 uint32 slots per step, i0 | i1 << 9 | i2 << 18 (ring slots) | vpass << 30 (the step begins with a
+//           vertex pass; the same in all 64 slots, read with readfirstlane); padding slots have bit 31 set
 //   streams: int4 (first step, end step, first vertex pass, end vertex pass) per stream
 // All loads of a step are unconditional (the next step's triangle slots and the next unconsumed vertex pass
 // are prefetched while the current step runs), so the compiler counts them in vmcnt.
@@ -65,7 +65,6 @@ struct FusedArgs {
     // mesh: vertex-ring streams (see kVRing above)
     const float4* sverts;
     const uint32_t* stris;
-    const uint32_t* ssteps;
     const int4* streams;
     const int32_t* model_st_lo;
     const int32_t* model_st_hi;

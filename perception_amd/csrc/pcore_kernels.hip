@@ -26,6 +26,13 @@
 
 #pragma clang fp contract(off)
 
+#ifndef PCORE_FRAG_FDIV
+#define PCORE_FRAG_FDIV 0
+#endif
+#ifndef PCORE_FLUSH_FLAT
+#define PCORE_FLUSH_FLAT 0
+#endif
+
 namespace pcore {
 
 constexpr int kWave = 64;
@@ -118,13 +125,23 @@ __device__ __forceinline__ bool loop_bounds(float bmin, float bmax, int& lo, int
 __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1, float C0, float C1, float z0,
                                          float z1, float z2, float P0, float P1, int32_t& depth) {
     const float area = 0.5f * ((C0 - A0) * (B1 - A1) - (B0 - A0) * (C1 - A1));
+#if PCORE_FRAG_FDIV
+    // IEEE-exact quotients without the range-scaling steps (pcore_fdiv.h)
+    const float base_inv = fdiv_exact(1.0f, area);
+#else
     const float base_inv = 1.0f / area;
+#endif
     const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
     const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
     const float alpha = 1.0f - beta - gamma;
     if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
+#if PCORE_FRAG_FDIV
+    const float ox = fdiv_exact(alpha, z0), oy = fdiv_exact(beta, z1), oz = fdiv_exact(gamma, z2);
+    const float frag = fdiv_exact(alpha + beta + gamma, ox + oy + oz);
+#else
     const float ox = alpha / z0, oy = beta / z1, oz = gamma / z2;
     const float frag = (alpha + beta + gamma) / (ox + oy + oz);
+#endif
     depth = cvt_i32_gpu(frag + 0.5f);
     return true;
 }
@@ -379,9 +396,19 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
 #ifdef PCORE_FLUSH_STATS
                     atomicAdd(&pcore_flush_stats[2], (unsigned long long)(nx * ny));
 #endif
+#if PCORE_FLUSH_FLAT
+                    // nx * ny <= kSmallK = 4: the first sample always exists; the others (a loop the wave skips when
+                    // every record touches one sample) at q = iy * nx + ix
+                    raster_sample<IDPASS>(r, kx0, ky0, s, H, sw, sm.zbuf, cid, id);
+                    for (int q = 1; q < nx * ny; q++) {
+                        const int iy = nx == 1 ? q : (nx == 2 ? q >> 1 : 0), ix = q - iy * nx;
+                        raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
+                    }
+#else
                     for (int iy = 0; iy < ny; iy++)
                         for (int ix = 0; ix < nx; ix++)
                             raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
+#endif
                 }
             }
         }
@@ -413,18 +440,17 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         float4 cv = a.sverts[(size_t)min(vp, vp_last) * kStepSlots + lane];
         uint32_t ct = a.stris[(size_t)sd.x * kStepSlots + lane];
         uint32_t cidt = IDPASS ? a.stri_orig[(size_t)sd.x * kStepSlots + lane] : 0u;
-        uint32_t hdr = a.ssteps[sd.x];
         for (int step = sd.x; step < sd.y; step++) {
             // prefetch the next step's triangles and the next unconsumed vertex pass (unconditional loads; the
             // last step re-loads itself)
             const int ns = min(step + 1, sd.y - 1);
             const uint32_t nct = a.stris[(size_t)ns * kStepSlots + lane];
             const uint32_t ncid = IDPASS ? a.stri_orig[(size_t)ns * kStepSlots + lane] : 0u;
-            const uint32_t nhdr = a.ssteps[ns];
-            const int nv = (int)((hdr >> 8) & 0xffu), ntri = (int)(hdr & 0xffu);
-            const int vp_next = vp + (nv > 0 ? 1 : 0);
+            // the step's "vertex pass first" flag is in every triangle slot (pcore_internal.h)
+            const bool vpass = (__builtin_amdgcn_readfirstlane((int)ct) >> 30) & 1;
+            const int vp_next = vp + (vpass ? 1 : 0);
             const float4 ncv = a.sverts[(size_t)min(vp_next, vp_last) * kStepSlots + lane];
-            if (nv > 0) {
+            if (vpass) {
                 if (rec_done < hist[kVRing - kRefPasses - 1]) {
 #ifdef PCORE_FLUSH_STATS
                     if (lane == 0) atomicAdd(&pcore_flush_stats[3], 1ull);
@@ -433,7 +459,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 }
                 // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
                 // (image_renderer.cuh:296-305, 82-84)
-                if (lane < nv && !(dbg & 8)) {
+                if (cv.w != 0.0f && !(dbg & 8)) {
                     const float lx = row4(m00, m01, m02, m03, cv.x, cv.y, cv.z);
                     const float ly = row4(m10, m11, m12, m13, cv.x, cv.y, cv.z);
                     const float lz = row4(m20, m21, m22, m23, cv.x, cv.y, cv.z);
@@ -462,7 +488,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 const uint32_t tri = ct & 0x7ffffffu;
                 const int i0 = (int)(ct & 511u), i1 = (int)((ct >> 9) & 511u), i2 = (int)((ct >> 18) & 511u);
                 float2 q0 = make_float2(0.f, 0.f), q1 = q0, q2 = q0;
-                if (lane < ntri) {
+                if (!(ct >> 31)) {  // not a padding slot
                     q0 = vxy[i0];
                     q1 = vxy[i1];
                     q2 = vxy[i2];
@@ -491,7 +517,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 uint64_t big = __ballot(nk > kSmallK);
 #ifdef PCORE_FLUSH_STATS
                 {
-                    const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(lane < ntri);
+                    const uint64_t btouch = __ballot(nk > 0), blanes = __ballot(!(ct >> 31));
                     if (lane == 0) {
                         atomicAdd(&pcore_flush_stats[4], (unsigned long long)__popcll(big));
                         atomicAdd(&pcore_flush_stats[5], (unsigned long long)__popcll(btouch));
@@ -548,7 +574,6 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             vp = vp_next;
             ct = nct;
             cidt = ncid;
-            hdr = nhdr;
         }
     }
     if (rec_total > rec_done) flush(rec_total - rec_done);

@@ -9,6 +9,9 @@
 //     in order of first use, up to 64;
 //   - the following batches take triangles in order while all three vertices were loaded by the last two
 //     passes (kRefPasses), 64 per step.
+// Layout (no per-step header, so the kernel never waits on a separate uniform load): every triangle slot of a
+// step carries the step's "vertex pass first" flag in bit 30, padding slots have bit 31 set, and a vertex
+// slot's w is 1 for a vertex, 0 for padding.
 // A triangle names each vertex by the ring slot of its latest load: (pass mod kVRing) * 64 + lane.
 #pragma once
 #include <algorithm>
@@ -28,11 +31,10 @@ struct I4 {
 
 struct Built {
     std::vector<F4> sverts;         // 64 per vertex pass
-    std::vector<uint32_t> stris;    // 64 per step
+    std::vector<uint32_t> stris;    // 64 per step: i0 | i1 << 9 | i2 << 18 | vpass << 30, padding bit 31
     std::vector<uint32_t> sorig;    // 64 per step: original triangle index
-    std::vector<uint32_t> ssteps;   // one header per step: nt | nv << 8
     std::vector<I4> streams;        // (first step, end step, first pass, end pass)
-    long long passes = 0, steps = 0, tri_slots = 0, vert_slots = 0;
+    long long passes = 0, steps = 0, filled = 0;
 };
 
 // Greedy adjacency-growth order: grow a patch from the lowest unassigned triangle, always adding the
@@ -84,7 +86,9 @@ inline std::vector<int> locality_order(const std::vector<int>& tv, int num_verts
     return order;
 }
 
-constexpr int kNever = -(1 << 20);  // "latest pass" of a vertex no pass of the stream has loaded
+constexpr int kNever = -(1 << 20);
+constexpr uint32_t kStepVertexPass = 1u << 30;  // every triangle slot of a step that begins with a vertex pass
+constexpr uint32_t kSlotPadding = 1u << 31;     // a triangle slot past the batch  // "latest pass" of a vertex no pass of the stream has loaded
 
 // Append the streams of one model.  tri_base: index of the model's first triangle in the upload.
 inline void build_model(const std::vector<int>& tv, const std::vector<float>& vxyz, int tri_base, int num_streams,
@@ -100,7 +104,7 @@ inline void build_model(const std::vector<int>& tv, const std::vector<float>& vx
     for (int sidx = 0; sidx < S; sidx++) {
         const int b0 = (int)((long long)T * sidx / S), b1 = (int)((long long)T * (sidx + 1) / S);
         I4 sd;
-        sd.x = (int)out.ssteps.size();
+        sd.x = (int)(out.stris.size() / 64);
         sd.z = (int)(out.sverts.size() / 64);
         // fresh ring per stream
         for (int i = b0; i < b1; i++)
@@ -130,27 +134,25 @@ inline void build_model(const std::vector<int>& tv, const std::vector<float>& vx
                 in_new[v] = 0;
                 latest[v] = P;
                 slot[v] = (P % vring) * 64 + k;
-                out.sverts.push_back(F4{vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], 0.0f});
+                out.sverts.push_back(F4{vxyz[3 * v], vxyz[3 * v + 1], vxyz[3 * v + 2], 1.0f});
             }
-            for (int k = (int)newv.size(); k < 64; k++) out.sverts.push_back(F4{0.0f, 0.0f, 0.0f, 0.0f});
+            for (int k = (int)newv.size(); k < 64; k++) out.sverts.push_back(F4{0.0f, 0.0f, 0.0f, 0.0f});  // w 0: padding
             out.passes++;
-            out.vert_slots += 64;
             // batches: triangles whose vertices were all loaded by the last ref_passes passes
             bool first = true;
             auto emit = [&]() {
-                const uint32_t nv = first ? (uint32_t)newv.size() : 0u;
-                out.ssteps.push_back((uint32_t)batch.size() | (nv << 8));
+                const uint32_t vflag = first ? kStepVertexPass : 0u;
                 for (int t : batch) {
                     const int v0 = tv[3 * t], v1 = tv[3 * t + 1], v2 = tv[3 * t + 2];
-                    out.stris.push_back((uint32_t)slot[v0] | ((uint32_t)slot[v1] << 9) | ((uint32_t)slot[v2] << 18));
+                    out.stris.push_back((uint32_t)slot[v0] | ((uint32_t)slot[v1] << 9) | ((uint32_t)slot[v2] << 18) | vflag);
                     out.sorig.push_back((uint32_t)(tri_base + t));
                 }
                 for (int k = (int)batch.size(); k < 64; k++) {
-                    out.stris.push_back(0u);
+                    out.stris.push_back(kSlotPadding | vflag);
                     out.sorig.push_back(0u);
                 }
+                out.filled += (long long)batch.size();
                 out.steps++;
-                out.tri_slots += 64;
                 first = false;
                 batch.clear();
             };
@@ -165,7 +167,7 @@ inline void build_model(const std::vector<int>& tv, const std::vector<float>& vx
             }
             if (!batch.empty() || first) emit();
         }
-        sd.y = (int)out.ssteps.size();
+        sd.y = (int)(out.stris.size() / 64);
         sd.w = (int)(out.sverts.size() / 64);
         out.streams.push_back(sd);
     }

@@ -25,11 +25,9 @@ extern "C" int stream_stats(const float* tri_xyz, int T, int num_streams, int vr
     pcore::streams::Built b;
     pcore::streams::build_model(tv, vxyz, 0, num_streams, vring, ref_passes, b);
     out[0] = b.passes; out[1] = b.steps; out[2] = (long long)vxyz.size() / 3; out[3] = T;
-    long long filled = 0;
-    for (uint32_t h : b.ssteps) filled += h & 0xff;
-    out[4] = filled;
+    out[4] = b.filled;
     long long vfill = 0;
-    for (uint32_t h : b.ssteps) vfill += (h >> 8) & 0xff;
+    for (const auto& v : b.sverts) vfill += v.w != 0.0f ? 1 : 0;
     out[5] = vfill;
     return 0;
 }
