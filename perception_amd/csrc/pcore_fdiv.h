@@ -1,4 +1,5 @@
-// pcore_fdiv.h -- IEEE-exact f32 division for the fused COST kernel without the range-scaling steps.
+// pcore_fdiv.h -- IEEE-exact f32 division for the fused COST kernel without the range-scaling steps, and the
+// reference GPU's float -> int32 conversion as one instruction.
 //
 // hipcc expands every f32 `a / b` (no fast-math) into 11 instructions:
 //   v_div_scale(b), v_rcp, fma, fma        -> r1, a refined reciprocal of b
@@ -51,6 +52,16 @@ __device__ __forceinline__ float fdiv_exact(float a, float b) {
         q = a / b;
     }
     return q;
+}
+
+// int32_t(f) with NVIDIA cvt.rzi.s32.f32 semantics (image_renderer.cuh:129 on the reference's GPU): round toward
+// zero, saturate to INT_MIN / INT_MAX, NaN -> 0.  v_cvt_i32_f32 implements exactly that (checked against the
+// branchy restatement over special values and random bit patterns by tools/fdiv_check.hip), so the fragment
+// test needs none of the compiler's range branches around a C++ conversion (undefined out of range).
+__device__ __forceinline__ int32_t cvt_i32_rz_sat(float f) {
+    int32_t r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
 }
 
 // q0 = a0 / b, q1 = a1 / b, IEEE-exact

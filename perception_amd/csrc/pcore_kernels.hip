@@ -32,6 +32,9 @@
 #ifndef PCORE_FLUSH_FLAT
 #define PCORE_FLUSH_FLAT 0
 #endif
+#ifndef PCORE_STEP_UNROLL
+#define PCORE_STEP_UNROLL 1
+#endif
 
 namespace pcore {
 
@@ -49,14 +52,6 @@ constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queue
 // ------------------------------------------------------------------------------------------------
 // Exact-semantics helpers (shared by every kernel)
 // ------------------------------------------------------------------------------------------------
-
-// NVIDIA cvt.rzi.s32.f32 semantics of `int32_t(float)` (image_renderer.cuh:129): NaN -> 0, saturate.
-__device__ __forceinline__ int32_t cvt_i32_gpu(float f) {
-    if (!(f == f)) return 0;
-    if (f >= 2147483648.0f) return INT_MAX;
-    if (f <= -2147483648.0f) return INT_MIN;
-    return (int32_t)f;
-}
 
 // x86 cvttss2si semantics of the host `(int) float` casts (search_env.cpp:2022-2048).
 __device__ __forceinline__ int32_t cvt_i32_x86(float f) {
@@ -142,7 +137,7 @@ __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1,
     const float ox = alpha / z0, oy = beta / z1, oz = gamma / z2;
     const float frag = (alpha + beta + gamma) / (ox + oy + oz);
 #endif
-    depth = cvt_i32_gpu(frag + 0.5f);
+    depth = cvt_i32_rz_sat(frag + 0.5f);
     return true;
 }
 
@@ -224,7 +219,7 @@ __device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, i
     const float P1 = (float)(H - 1 - ky * s);
     int32_t d;
     if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d)) {
-        const int k = (ky - w.y0) * w.nx + (kx - w.x0);
+        const int k = (int)__umul24((uint32_t)(ky - w.y0), (uint32_t)w.nx) + (kx - w.x0);
         if constexpr (IDPASS) {
             if (d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
         } else {
@@ -295,7 +290,7 @@ __device__ __forceinline__ int triangle_window(float x0, float x1, float x2, flo
     ky0 = b0;
     nx = a1 - a0 + 1;
     ny = b1 - b0 + 1;
-    return (nx > 0 && ny > 0) ? nx * ny : 0;
+    return (nx > 0 && ny > 0) ? (int)__umul24((uint32_t)nx, (uint32_t)ny) : 0;
 }
 
 // Measurement build only (-DPCORE_FUSED_PROFILE, tools/fused_phase_prof.py): per-wave shader clocks of the
@@ -437,19 +432,19 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
         int buf = 0;                 // ring buffer of the next vertex pass
         int vp = sd.z;               // next vertex pass to consume
         const int vp_last = max(sd.w - 1, sd.z);
-        float4 cv = a.sverts[(size_t)min(vp, vp_last) * kStepSlots + lane];
-        uint32_t ct = a.stris[(size_t)sd.x * kStepSlots + lane];
-        uint32_t cidt = IDPASS ? a.stri_orig[(size_t)sd.x * kStepSlots + lane] : 0u;
-        for (int step = sd.x; step < sd.y; step++) {
-            // prefetch the next step's triangles and the next unconsumed vertex pass (unconditional loads; the
-            // last step re-loads itself)
+        // one step: the current step's triangle slots / vertex pass in (cv, ct, cidt); prefetches the next step's
+        // triangle slots and the next unconsumed vertex pass into (ncv, nct, ncid) -- unconditional loads, the last
+        // step re-loads itself.  The loop below alternates two register sets, so no copy of a prefetched register
+        // makes the wave wait for the load at the end of its step.
+        auto run_step = [&](int step, const float4& cv, const uint32_t ct, const uint32_t cidt, float4& ncv,
+                            uint32_t& nct, uint32_t& ncid) {
             const int ns = min(step + 1, sd.y - 1);
-            const uint32_t nct = a.stris[(size_t)ns * kStepSlots + lane];
-            const uint32_t ncid = IDPASS ? a.stri_orig[(size_t)ns * kStepSlots + lane] : 0u;
+            nct = a.stris[(size_t)ns * kStepSlots + lane];
+            ncid = IDPASS ? a.stri_orig[(size_t)ns * kStepSlots + lane] : 0u;
             // the step's "vertex pass first" flag is in every triangle slot (pcore_internal.h)
             const bool vpass = (__builtin_amdgcn_readfirstlane((int)ct) >> 30) & 1;
             const int vp_next = vp + (vpass ? 1 : 0);
-            const float4 ncv = a.sverts[(size_t)min(vp_next, vp_last) * kStepSlots + lane];
+            ncv = a.sverts[(size_t)min(vp_next, vp_last) * kStepSlots + lane];
             if (vpass) {
                 if (rec_done < hist[kVRing - kRefPasses - 1]) {
 #ifdef PCORE_FLUSH_STATS
@@ -492,8 +487,8 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     q0 = vxy[i0];
                     q1 = vxy[i1];
                     q2 = vxy[i2];
-                    const bool nan_tri = (q0.x != q0.x) || (q0.y != q0.y) || (q1.x != q1.x) || (q1.y != q1.y) ||
-                                         (q2.x != q2.x) || (q2.y != q2.y);
+                    const bool nan_tri = __builtin_isunordered(q0.x, q0.y) || __builtin_isunordered(q1.x, q1.y) ||
+                                         __builtin_isunordered(q2.x, q2.y);
                     if (!nan_tri) {
                         nk = triangle_window<STRIDE>(q0.x, q1.x, q2.x, q0.y, q1.y, q2.y, s, cmax0, cmax1, H, sw, kx0,
                                                      ky0, nx, ny);
@@ -570,11 +565,22 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 while (rec_total - rec_done >= kWave) flush(kWave);  // full batches only
             }
             fp.mark(2);
-            cv = ncv;
             vp = vp_next;
-            ct = nct;
-            cidt = ncid;
+        };
+        float4 cvA = a.sverts[(size_t)min(vp, vp_last) * kStepSlots + lane], cvB;
+        uint32_t ctA = a.stris[(size_t)sd.x * kStepSlots + lane], ctB, cidA, cidB;
+        cidA = IDPASS ? a.stri_orig[(size_t)sd.x * kStepSlots + lane] : 0u;
+#if PCORE_STEP_UNROLL
+        for (int step = sd.x; step < sd.y; step += 2) {
+            run_step(step, cvA, ctA, cidA, cvB, ctB, cidB);
+            if (step + 1 < sd.y) run_step(step + 1, cvB, ctB, cidB, cvA, ctA, cidA);
         }
+#else
+        for (int step = sd.x; step < sd.y; step++) {
+            run_step(step, cvA, ctA, cidA, cvB, ctB, cidB);
+            cvA = cvB; ctA = ctB; cidA = cidB;
+        }
+#endif
     }
     if (rec_total > rec_done) flush(rec_total - rec_done);
 }

@@ -4,7 +4,10 @@
 // Inputs: 2^26 pairs per launch from a counter-based hash, with exponents drawn over the whole f32 range
 // (zeros, denormals, infinities and NaNs included) and a dense band around the [2^-40, 2^41) fast-path
 // bounds, plus structured pairs (exact quotients, quotients near rounding ties: a = b * (1 + k ulp)).
-// Prints one JSON line {"pairs": N, "mismatches": M, "fast_frac": F}; exit status 1 on any mismatch.
+// Also pcore::cvt_i32_rz_sat (one v_cvt_i32_f32) against the branchy NVIDIA-semantics conversion on special
+// values and random bit patterns.
+// Prints one JSON line {"pairs": N, "mismatches": M, "fast_frac": F, "cvt_values": C, "cvt_mismatches": K};
+// exit status 1 on any mismatch.
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/bin/fdiv_check tools/fdiv_check.hip
 #include <hip/hip_runtime.h>
 
@@ -51,15 +54,39 @@ __global__ void check(uint32_t seed, unsigned long long* bad, unsigned long long
     if (pcore::fdiv_range_ok(min(min(e0, e1), eb), max(max(e0, e1), eb))) atomicAdd(fast, 1ull);
 }
 
+// reference semantics of cvt_i32_rz_sat (NVIDIA cvt.rzi.s32.f32), written out with branches
+__device__ __forceinline__ int32_t cvt_ref(float f) {
+    if (!(f == f)) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (int32_t)0x80000000u;
+    return (int32_t)f;
+}
+
+__global__ void check_cvt(uint32_t seed, unsigned long long* bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t h0 = mix(i * 2u + seed), h1 = mix(i * 2u + 1u + seed * 5u);
+    float f = draw(h0, h1);
+    if ((h1 >> 24) % 4u == 0) f = (float)(int32_t)h0 + (float)((h1 >> 8) & 3u) * 0.25f;  // near integers
+    if (i < 8) {
+        const float sp[8] = {__int_as_float(0x7fc00000), __int_as_float(0xffc00001), __int_as_float(0x7f800000),
+                             __int_as_float(0xff800000), 2147483648.0f, -2147483648.0f, 2147483520.0f, -0.0f};
+        f = sp[i];
+    }
+    if (pcore::cvt_i32_rz_sat(f) != cvt_ref(f)) atomicAdd(bad, 1ull);
+}
+
 int main() {
-    unsigned long long *d, h[2] = {0, 0};
-    if (hipMalloc(&d, 16) != hipSuccess) return 2;
-    if (hipMemset(d, 0, 16) != hipSuccess) return 2;
+    unsigned long long *d, h[3] = {0, 0, 0};
+    if (hipMalloc(&d, 24) != hipSuccess) return 2;
+    if (hipMemset(d, 0, 24) != hipSuccess) return 2;
     const int launches = 16, blocks = 1 << 18, threads = 256;
     for (int l = 0; l < launches; l++) hipLaunchKernelGGL(check, dim3(blocks), dim3(threads), 0, 0, (uint32_t)l * 0x9e3779b9u, d, d + 1);
+    for (int l = 0; l < 4; l++) hipLaunchKernelGGL(check_cvt, dim3(blocks), dim3(threads), 0, 0, (uint32_t)l * 0x85ebca6bu, d + 2);
     if (hipDeviceSynchronize() != hipSuccess) return 2;
-    if (hipMemcpy(h, d, 16, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    if (hipMemcpy(h, d, 24, hipMemcpyDeviceToHost) != hipSuccess) return 2;
     const double pairs = 2.0 * launches * (double)blocks * threads;
-    printf("{\"pairs\": %.0f, \"mismatches\": %llu, \"fast_frac\": %.4f}\n", pairs, h[0], 2.0 * h[1] / pairs);
-    return h[0] == 0 ? 0 : 1;
+    const double cvts = 4.0 * (double)blocks * threads;
+    printf("{\"pairs\": %.0f, \"mismatches\": %llu, \"fast_frac\": %.4f, \"cvt_values\": %.0f, \"cvt_mismatches\": %llu}\n",
+           pairs, h[0], 2.0 * h[1] / pairs, cvts, h[2]);
+    return h[0] == 0 && h[2] == 0 ? 0 : 1;
 }
