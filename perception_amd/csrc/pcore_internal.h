@@ -28,6 +28,7 @@ constexpr int kStepSlots = 64;
 constexpr int kVRing = PCORE_VRING;    // vertex passes resident per wave
 constexpr int kRefPasses = 2;          // a batch references the last kRefPasses passes
 constexpr int kRingSlotBits = 9;       // kVRing * 64 <= 512
+constexpr int kStreamChunks = 1;       // chunks per stream (pcore_streams.h, build_model)
 #ifndef PCORE_FUSED_WAVES
 #define PCORE_FUSED_WAVES 4
 #endif

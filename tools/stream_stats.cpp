@@ -5,7 +5,8 @@
 
 #include "../perception_amd/csrc/pcore_streams.h"
 
-extern "C" int stream_stats(const float* tri_xyz, int T, int num_streams, int vring, int ref_passes, long long* out) {
+extern "C" int stream_stats(const float* tri_xyz, int T, int num_streams, int vring, int ref_passes, int chunks,
+                            long long* out) {
     struct K { uint32_t x, y, z; bool operator==(const K& o) const { return x == o.x && y == o.y && z == o.z; } };
     struct H { size_t operator()(const K& k) const { return (size_t)k.x * 73856093u ^ (size_t)k.y * 19349663u ^ (size_t)k.z * 83492791u; } };
     std::unordered_map<K, int, H> idx;
@@ -23,7 +24,7 @@ extern "C" int stream_stats(const float* tri_xyz, int T, int num_streams, int vr
             tv[3 * (size_t)t + k] = id;
         }
     pcore::streams::Built b;
-    pcore::streams::build_model(tv, vxyz, 0, num_streams, vring, ref_passes, b);
+    pcore::streams::build_model(tv, vxyz, 0, num_streams, vring, ref_passes, b, chunks);
     out[0] = b.passes; out[1] = b.steps; out[2] = (long long)vxyz.size() / 3; out[3] = T;
     out[4] = b.filled;
     long long vfill = 0;
