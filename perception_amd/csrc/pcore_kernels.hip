@@ -193,6 +193,7 @@ struct FusedSmem {
     int32_t* zbuf;  // tile samples
     float2* vxy;    // kWaves * kVRing * 64: screen (x, y) of the wave's vertex ring
     float* vz;      // kWaves * kVRing * 64: camera z (cm)
+    uint2* vbd;     // kWaves * 2 * 64 (kVBounds): packed int16 sample-window bounds of the last two passes
     uint2* ring;    // kWaves * kRecCap queued triangle records (phase 1); int32 point queues in phase 2
     uint32_t* ring_id;  // kWaves * kRecCap original triangle ids (colour id pass only)
     uint32_t* bitmap;
@@ -233,6 +234,7 @@ size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour) {
     size_t b = al((size_t)tile_samples * 4);
     b += al((size_t)kWaves * kRingSlots * 8);
     b += al((size_t)kWaves * kRingSlots * 4);
+    if (kVBounds) b += al((size_t)kWaves * 2 * kWave * 8);
     b += al((size_t)kWaves * kRecCap * 8);
     if (colour) b += al((size_t)kWaves * kRecCap * 4);
     b += al((size_t)bitmap_words * 4);
@@ -248,6 +250,8 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
     sm.zbuf = (int32_t*)p; p += al((size_t)nsamp * 4);
     sm.vxy = (float2*)p; p += al((size_t)kWaves * kRingSlots * 8);
     sm.vz = (float*)p; p += al((size_t)kWaves * kRingSlots * 4);
+    sm.vbd = nullptr;
+    if (kVBounds) { sm.vbd = (uint2*)p; p += al((size_t)kWaves * 2 * kWave * 8); }
     sm.ring = (uint2*)p; p += al((size_t)kWaves * kRecCap * 8);
     sm.ring_id = nullptr;
     if (colour) { sm.ring_id = (uint32_t*)p; p += al((size_t)kWaves * kRecCap * 4); }
@@ -291,6 +295,38 @@ __device__ __forceinline__ int triangle_window(float x0, float x1, float x2, flo
     nx = a1 - a0 + 1;
     ny = b1 - b0 + 1;
     return (nx > 0 && ny > 0) ? (int)__umul24((uint32_t)nx, (uint32_t)ny) : 0;
+}
+
+// triangle_window, decomposed over the vertices.  Each of its four bounds is a monotone function of the
+// triangle's min or max screen coordinate -- a0 = A0(min x), a1 = A1(max x), b0 = B0(max y), b1 = B1(min y) --
+// so it equals the min or max of that function over the three vertices: a0 = min A0(x_i), a1 = max A1(x_i),
+// b0 = min B0(y_i), b1 = max B1(y_i) (clipping to the pose window commutes as well).  The vertex pass
+// stores (A0, B0) and (A1, B1) as int16 pairs; the triangle stage takes two packed minima and two packed
+// maxima.  At stride 8 every bound fits int16 (|bound| <= (16384 + 65536) / 8); the generic stride clamps
+// them to +-32767, which leaves a window of a <= 16384-sample image empty exactly when it was.  A NaN screen
+// coordinate marks the vertex with -32768 lower bounds (a real lower bound is >= 0), and its triangles take
+// the reference's NaN-propagating bbox instead.
+typedef short short2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
+constexpr uint32_t kNanBounds = 0x80008000u;
+
+template <int STRIDE>
+__device__ __forceinline__ uint2 vertex_bounds(float sx, float sy, int s, float cmax0, float cmax1, int H) {
+    if (__builtin_isunordered(sx, sy)) return make_uint2(kNanBounds, 0u);
+    const int ss = STRIDE > 0 ? STRIDE : s;
+    const int lo0 = (int)(fminf(fmaxf(sx, 0.0f), 65536.0f) + 0.5f);
+    const int lo1 = (int)(fminf(fmaxf(sy, 0.0f), 65536.0f) + 0.5f);
+    const int hi0 = (int)floorf(fmaxf(fminf(sx, cmax0), -65536.0f));
+    const int hi1 = (int)floorf(fmaxf(fminf(sy, cmax1), -65536.0f));
+    int A0 = floor_div<STRIDE>(lo0 + ss - 1, s), A1 = floor_div<STRIDE>(hi0, s);
+    int B0 = floor_div<STRIDE>(H - 1 - hi1 + ss - 1, s), B1 = floor_div<STRIDE>(H - 1 - lo1, s);
+    if constexpr (STRIDE == 0) {
+        A0 = min(A0, 32767);
+        B0 = min(B0, 32767);
+        A1 = max(A1, -32767);
+        B1 = max(B1, -32767);
+    }
+    return make_uint2(((uint32_t)A0 & 0xffffu) | ((uint32_t)B0 << 16), ((uint32_t)A1 & 0xffffu) | ((uint32_t)B1 << 16));
 }
 
 // Measurement build only (-DPCORE_FUSED_PROFILE, tools/fused_phase_prof.py): per-wave shader clocks of the
@@ -356,6 +392,10 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     const float cmax0 = (float)(W - 1), cmax1 = (float)(H - 1);
     float2* vxy = sm.vxy + wave * kRingSlots;
     float* vz = sm.vz + wave * kRingSlots;
+    uint2* vbd = kVBounds ? sm.vbd + wave * 2 * kWave : nullptr;
+    // the pose window as int16 pairs (first sample, last sample); an empty window has last < first
+    const short2v wfirst = {(short)sw.x0, (short)sw.y0};
+    const short2v wlast = {(short)(sw.x0 + sw.nx - 1), (short)(sw.y0 + sw.ny - 1)};
     uint2* ring = sm.ring + wave * kRecCap;
     uint32_t* ring_id = IDPASS ? sm.ring_id + wave * kRecCap : nullptr;
     // record ring: wave-uniform monotone counters of appended and flushed records; record i lives in slot
@@ -467,6 +507,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     const float sy = qy * Hf / 2.0f + Hf / 2.0f;
                     vxy[buf * kWave + lane] = make_float2(sx, sy);
                     vz[buf * kWave + lane] = lz;
+                    if constexpr (kVBounds) vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H);
                 }
 #pragma unroll
                 for (int k = kVRing - kRefPasses - 1; k > 0; k--) hist[k] = hist[k - 1];
@@ -482,11 +523,39 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
                 const uint32_t tri = ct & 0x7ffffffu;
                 const int i0 = (int)(ct & 511u), i1 = (int)((ct >> 9) & 511u), i2 = (int)((ct >> 18) & 511u);
-                float2 q0 = make_float2(0.f, 0.f), q1 = q0, q2 = q0;
+#if PCORE_VBOUNDS
+                // a padding slot names slot 0 three times: its bounds are read (harmless) and nk forced to 0
+                const bool pad = ct >> 31;
+                const uint2 w0 = vbd[i0 & (2 * kWave - 1)], w1 = vbd[i1 & (2 * kWave - 1)], w2 = vbd[i2 & (2 * kWave - 1)];
+                short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
+                short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
+                const bool nan_tri = lo.x < 0 && !pad;
+                lo = __builtin_elementwise_max(lo, wfirst);
+                hi = __builtin_elementwise_min(hi, wlast);
+                kx0 = lo.x;
+                ky0 = lo.y;
+                nx = (int)hi.x - (int)lo.x + 1;
+                ny = (int)hi.y - (int)lo.y + 1;
+                nk = (nx > 0 && ny > 0 && !pad) ? (int)__umul24((uint32_t)nx, (uint32_t)ny) : 0;
+                if (nan_tri) {
+                    // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
+                    const float2 q0 = vxy[i0], q1 = vxy[i1], q2 = vxy[i2];
+                    const float p[3][2] = {{q0.x, q0.y}, {q1.x, q1.y}, {q2.x, q2.y}};
+                    float bmin[2], bmax[2];
+                    bbox_ref(p, cmax0, cmax1, bmin, bmax);
+                    nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
+                    if (nk > 0) {  // clip to the pose window
+                        const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
+                        kx0 = max(kx0, sw.x0);
+                        ky0 = max(ky0, sw.y0);
+                        nx = kx1 - kx0;
+                        ny = ky1 - ky0;
+                        nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+                    }
+                }
+#else
                 if (!(ct >> 31)) {  // not a padding slot
-                    q0 = vxy[i0];
-                    q1 = vxy[i1];
-                    q2 = vxy[i2];
+                    const float2 q0 = vxy[i0], q1 = vxy[i1], q2 = vxy[i2];
                     const bool nan_tri = __builtin_isunordered(q0.x, q0.y) || __builtin_isunordered(q1.x, q1.y) ||
                                          __builtin_isunordered(q2.x, q2.y);
                     if (!nan_tri) {
@@ -508,6 +577,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         }
                     }
                 }
+#endif
                 // large triangles: whole-wave cooperative
                 uint64_t big = __ballot(nk > kSmallK);
 #ifdef PCORE_FLUSH_STATS
@@ -522,8 +592,13 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 }
 #endif
                 if (big) {
+                    // the big triangles' screen vertices, read again (rare: not kept in registers through the step)
+                    float2 q0 = make_float2(0.f, 0.f), q1 = q0, q2 = q0;
                     float z0 = 0.0f, z1 = 0.0f, z2 = 0.0f;
                     if (nk > kSmallK) {
+                        q0 = vxy[i0];
+                        q1 = vxy[i1];
+                        q2 = vxy[i2];
                         z0 = vz[i0];
                         z1 = vz[i1];
                         z2 = vz[i2];
