@@ -64,6 +64,18 @@ __device__ __forceinline__ int32_t cvt_i32_rz_sat(float f) {
     return r;
 }
 
+// |x| as bits, with 0 mapped to 1.0f: a zero numerator is exact in the unscaled steps except for the sign of a
+// zero quotient (-0 / b can come out +0), which only matters where noted
+__device__ __forceinline__ uint32_t absbits_zero_as_one(float x) {
+    const uint32_t u = __float_as_uint(x) & 0x7fffffffu;
+    return u == 0u ? 0x3f800000u : u;
+}
+// every |x| (as bits, non-negative floats order like their bit patterns) in [2^-40, 2^41): the exponent range
+// of fdiv_range_ok
+__device__ __forceinline__ bool absbits_range_ok(uint32_t umin, uint32_t umax) {
+    return umin >= (87u << 23) && umax < (168u << 23);
+}
+
 // q0 = a0 / b, q1 = a1 / b, IEEE-exact
 __device__ __forceinline__ void fdiv2_exact(float a0, float a1, float b, float& q0, float& q1) {
     const uint32_t e0 = fexp_bits(a0), e1 = fexp_bits(a1), eb = fexp_bits(b);

@@ -120,7 +120,45 @@ __device__ __forceinline__ bool loop_bounds(float bmin, float bmax, int& lo, int
 __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1, float C0, float C1, float z0,
                                          float z1, float z2, float P0, float P1, int32_t& depth) {
     const float area = 0.5f * ((C0 - A0) * (B1 - A1) - (B0 - A0) * (C1 - A1));
-#if PCORE_FRAG_FDIV
+#if PCORE_FRAG_FDIV == 2
+    // The five quotients through the unscaled steps of pcore_fdiv.h, each IEEE-exact when its operands' exponents
+    // are in range; an exec-masked IEEE branch takes the lanes where one is not.  alpha / beta / gamma may also be
+    // zero: a zero quotient may then come out with the other sign, but the three quotients are only summed and
+    // never all zero (alpha = 1 - beta - gamma), so the sum -- and the depth -- is the IEEE one bit for bit.
+    float base_inv = quot_refined(1.0f, area, recip_refined(area));
+    {
+        const uint32_t ua = __float_as_uint(area) & 0x7fffffffu;
+        if (!absbits_range_ok(ua, ua)) {
+            asm volatile("");
+            base_inv = 1.0f / area;
+        }
+    }
+    const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
+    const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
+    const float alpha = 1.0f - beta - gamma;
+    if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
+    const float num = alpha + beta + gamma;
+    const float ox = quot_refined(alpha, z0, recip_refined(z0));
+    const float oy = quot_refined(beta, z1, recip_refined(z1));
+    const float oz = quot_refined(gamma, z2, recip_refined(z2));
+    const float den = ox + oy + oz;
+    float frag = quot_refined(num, den, recip_refined(den));
+    {
+        const uint32_t m = 0x7fffffffu;
+        const uint32_t uz0 = __float_as_uint(z0) & m, uz1 = __float_as_uint(z1) & m, uz2 = __float_as_uint(z2) & m;
+        const uint32_t ub0 = absbits_zero_as_one(alpha), ub1 = absbits_zero_as_one(beta), ub2 = absbits_zero_as_one(gamma);
+        const uint32_t un = __float_as_uint(num) & m, ud = __float_as_uint(den) & m;
+        const uint32_t umin = min(min(min(uz0, uz1), min(uz2, ub0)), min(min(ub1, ub2), min(un, ud)));
+        const uint32_t umax = max(max(max(uz0, uz1), max(uz2, ub0)), max(max(ub1, ub2), max(un, ud)));
+        if (!absbits_range_ok(umin, umax)) {
+            asm volatile("");
+            frag = (alpha + beta + gamma) / (alpha / z0 + beta / z1 + gamma / z2);
+        }
+    }
+    depth = cvt_i32_rz_sat(frag + 0.5f);
+    return true;
+#else
+#if PCORE_FRAG_FDIV == 1
     // IEEE-exact quotients without the range-scaling steps (pcore_fdiv.h)
     const float base_inv = fdiv_exact(1.0f, area);
 #else
@@ -130,7 +168,7 @@ __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1,
     const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
     const float alpha = 1.0f - beta - gamma;
     if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
-#if PCORE_FRAG_FDIV
+#if PCORE_FRAG_FDIV == 1
     const float ox = fdiv_exact(alpha, z0), oy = fdiv_exact(beta, z1), oz = fdiv_exact(gamma, z2);
     const float frag = fdiv_exact(alpha + beta + gamma, ox + oy + oz);
 #else
@@ -139,6 +177,7 @@ __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1,
 #endif
     depth = cvt_i32_rz_sat(frag + 0.5f);
     return true;
+#endif
 }
 
 __device__ __forceinline__ void wave_sync() {

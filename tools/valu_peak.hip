@@ -58,6 +58,28 @@ __global__ void __launch_bounds__(256) chains(float* out, float a, float b) {
                 x[i] = __int_as_float(v);
             } else if constexpr (KIND == 4) {  // IEEE division (the compiler's 10-11 instruction sequence)
                 x[i] = x[i] / a + b;
+            } else if constexpr (KIND == 5) {  // v_pk_mul_f32
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                f2 v = {y[i].x, y[i].y};
+                const f2 va = {a, b};
+                v = v * va;
+                y[i] = make_float2(v.x, v.y);
+            } else if constexpr (KIND == 6) {  // v_lshl_add_u64 (64-bit address arithmetic)
+                unsigned long long v = ((unsigned long long)__float_as_uint(y[i].x) << 32) | __float_as_uint(y[i].y);
+                v = (v << 2) + (unsigned long long)(threadIdx.x + it);
+                y[i] = make_float2(__uint_as_float((unsigned)(v >> 32)), __uint_as_float((unsigned)v));
+            } else if constexpr (KIND == 7) {  // v_cvt_i32_f32 + v_cvt_f32_i32
+                int v;
+                asm volatile("v_cvt_i32_f32 %0, %1" : "=v"(v) : "v"(x[i]));
+                x[i] = (float)v + a;
+            } else if constexpr (KIND == 8) {  // v_pk_min_i16
+                typedef short s2 __attribute__((ext_vector_type(2)));
+                s2 v = __builtin_bit_cast(s2, __float_as_uint(x[i]));
+                const s2 w = {(short)it, (short)(it + 1)};
+                v = __builtin_elementwise_min(v, w);
+                x[i] = __uint_as_float(__builtin_bit_cast(unsigned, v));
+            } else if constexpr (KIND == 9) {  // v_cmp + v_cndmask
+                x[i] = x[i] > a ? x[i] * b : x[i] + b;
             }
         }
     }
@@ -110,6 +132,11 @@ int main() {
     if (run<2>("v_rcp_f32", 1, out, cus)) return 1;
     if (run<3>("v_lshrrev_b32 + v_add_u32", 2, out, cus)) return 1;
     if (run<4>("fdiv_ieee_plus_add (11.5 instr)", 11.5, out, cus)) return 1;
+    if (run<5>("v_pk_mul_f32", 1, out, cus)) return 1;
+    if (run<6>("v_lshl_add_u64 (+ v_add_co 2)", 3, out, cus)) return 1;
+    if (run<7>("v_cvt_i32_f32 + v_cvt_f32_i32 + v_add", 3, out, cus)) return 1;
+    if (run<8>("v_pk_min_i16", 1, out, cus)) return 1;
+    if (run<9>("v_cmp + v_mul + v_add + v_cndmask", 4, out, cus)) return 1;
     CHECK(hipFree(out));
     return 0;
 }
