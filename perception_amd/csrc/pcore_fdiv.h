@@ -76,6 +76,40 @@ __device__ __forceinline__ bool absbits_range_ok(uint32_t umin, uint32_t umax) {
     return umin >= (87u << 23) && umax < (168u << 23);
 }
 
+// The fragment depth of the reference (image_renderer.cuh:123-129) from its barycentrics and vertex depths, with IEEE
+// divisions in the reference's order: int32_t((alpha + beta + gamma) / (alpha/z0 + beta/z1 + gamma/z2) + 0.5f).
+__device__ __forceinline__ int32_t frag_depth_ieee(float alpha, float beta, float gamma, float z0, float z1, float z2) {
+    const float ox = alpha / z0, oy = beta / z1, oz = gamma / z2;
+    return cvt_i32_rz_sat((alpha + beta + gamma) / (ox + oy + oz) + 0.5f);
+}
+
+// frag_depth_ieee, bit for bit, mostly without divisions.  Precondition (what passes the reference's inside
+// test): each of alpha, beta, gamma is in [-0, 1] or NaN.  The depth d(Q) = int(Q + 0.5) is monotone in the
+// quotient Q of the IEEE chain.  With every z_i in [2^-100, 2^100] and no NaN, every term of the denominator is
+// non-negative, so the chain through v_rcp_f32 (<= 1 ulp) and products has a relative error below 2^-20 against
+// Q: 2^-22 per term (reciprocal, product and the IEEE quotient's own rounding), no cancellation in the two sums,
+// then 2^-21 + 2^-23 + 2 * 2^-24 for the last quotient.  Q therefore lies in [f - e, f + e] with e = 2^-19 |f| (a
+// factor-2 margin that also covers the rounding of f -/+ e), and where d(f - e) == d(f + e) that value is d(Q).
+// Anywhere else -- a half-integer within e, depths out of range, a NaN -- the lane takes the IEEE divisions in an
+// exec-masked branch.
+__device__ __forceinline__ int32_t frag_depth_certified(float alpha, float beta, float gamma, float z0, float z1,
+                                                        float z2) {
+    const float num = alpha + beta + gamma;
+    const float oxa = alpha * __builtin_amdgcn_rcpf(z0), oya = beta * __builtin_amdgcn_rcpf(z1),
+                oza = gamma * __builtin_amdgcn_rcpf(z2);
+    const float f = num * __builtin_amdgcn_rcpf(oxa + oya + oza);
+    const float e = fabsf(f) * 0x1p-19f;
+    int32_t d = cvt_i32_rz_sat((f - e) + 0.5f);
+    const int32_t dh = cvt_i32_rz_sat((f + e) + 0.5f);
+    // fminf / fmaxf skip a NaN operand; a NaN depth makes zs NaN, a NaN barycentric makes num NaN
+    const float zmin = fminf(fminf(z0, z1), z2), zmax = fmaxf(fmaxf(z0, z1), z2), zs = z0 + z1 + z2;
+    if (!(zmin >= 0x1p-100f) || !(zmax <= 0x1p100f) || zs != zs || num != num || d != dh) {
+        asm volatile("");
+        d = frag_depth_ieee(alpha, beta, gamma, z0, z1, z2);
+    }
+    return d;
+}
+
 // q0 = a0 / b, q1 = a1 / b, IEEE-exact
 __device__ __forceinline__ void fdiv2_exact(float a0, float a1, float b, float& q0, float& q1) {
     const uint32_t e0 = fexp_bits(a0), e1 = fexp_bits(a1), eb = fexp_bits(b);

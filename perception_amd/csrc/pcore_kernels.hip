@@ -26,8 +26,10 @@
 
 #pragma clang fp contract(off)
 
+// fragment depth quotients: 0 IEEE divisions, 1 / 2 unscaled exact divisions (measured slower), 3 reciprocal
+// estimates with an error certificate and IEEE fallback (pcore_fdiv.h, frag_depth_certified)
 #ifndef PCORE_FRAG_FDIV
-#define PCORE_FRAG_FDIV 0
+#define PCORE_FRAG_FDIV 3
 #endif
 #ifndef PCORE_FLUSH_FLAT
 #define PCORE_FLUSH_FLAT 0
@@ -156,6 +158,16 @@ __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1,
         }
     }
     depth = cvt_i32_rz_sat(frag + 0.5f);
+    return true;
+#elif PCORE_FRAG_FDIV == 3
+    // IEEE barycentrics and inside test; the depth quotient chain through frag_depth_certified (pcore_fdiv.h):
+    // reciprocal estimates with an error certificate, the IEEE divisions only where the certificate fails
+    const float base_inv = 1.0f / area;
+    const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
+    const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
+    const float alpha = 1.0f - beta - gamma;
+    if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
+    depth = frag_depth_certified(alpha, beta, gamma, z0, z1, z2);
     return true;
 #else
 #if PCORE_FRAG_FDIV == 1
@@ -967,12 +979,14 @@ extern "C" int pcore_debug_wg_clock(unsigned long long* host, int n) {
 }
 #endif
 
-// register budget of the fused kernel: 7 waves per SIMD (72 VGPRs, 94 SGPRs) when a 7-workgroup tier exists
+// register budget of the fused kernel: as many waves per SIMD as the most-occupied tile tier has workgroups per CU
+// (6: <= 80 VGPRs; without the bound the certified fragment depth takes 82 and the kernel drops to 5 waves).  The
+// colour-cost kernel (two raster passes, CIEDE2000) is left unbounded: under 80 VGPRs it spills.
 #ifndef PCORE_FUSED_WAVES_PER_EU
-#define PCORE_FUSED_WAVES_PER_EU (PCORE_TIER_MAX > 6 ? PCORE_TIER_MAX : 1)
+#define PCORE_FUSED_WAVES_PER_EU PCORE_TIER_MAX
 #endif
 template <int STRIDE, bool COLOUR = false>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PCORE_FUSED_WAVES_PER_EU)))
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(COLOUR ? 1 : PCORE_FUSED_WAVES_PER_EU)))
 fused_cost_kernel(FusedArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int pose = blockIdx.x;
