@@ -22,21 +22,16 @@ namespace pcore {
 // All loads of a step are unconditional (the next step's triangle slots and the next unconsumed vertex pass
 // are prefetched while the current step runs), so the compiler counts them in vmcnt.
 constexpr int kStepSlots = 64;
-// Per-vertex sample-window bounds (packed int16, computed once per vertex in the vertex pass) instead of a
-// float window per triangle from its three screen vertices.  A batch reads the bounds of the last kRefPasses
-// passes only, so they live in kRefPasses ring buffers of their own (pass p in buffer p mod 2, which equals
-// (p mod kVRing) mod 2 when kVRing is even).  PCORE_VBOUNDS=0 restores the per-triangle float window (A/B).
-#ifndef PCORE_VBOUNDS
-#define PCORE_VBOUNDS 1
-#endif
+// Per-vertex sample-window bounds (packed int16, computed once per vertex in the vertex pass; pcore_kernels.hip,
+// vertex_bounds).  A batch reads the bounds of the last kRefPasses passes only, so they live in two ring buffers of
+// their own: pass p in buffer p mod 2, which equals (p mod kVRing) mod 2 because kVRing is even.
 #ifndef PCORE_VRING
-#define PCORE_VRING (PCORE_VBOUNDS ? 4 : 5)
+#define PCORE_VRING 4
 #endif
 constexpr int kVRing = PCORE_VRING;    // vertex passes resident per wave
 constexpr int kRefPasses = 2;          // a batch references the last kRefPasses passes
 constexpr int kRingSlotBits = 9;       // kVRing * 64 <= 512
-constexpr bool kVBounds = PCORE_VBOUNDS != 0;
-static_assert(!kVBounds || (PCORE_VRING % 2 == 0), "per-vertex bounds index their two buffers by ring slot parity");
+static_assert(PCORE_VRING % 2 == 0, "per-vertex bounds index their two buffers by ring slot parity");
 constexpr int kStreamChunks = 1;       // chunks per stream (pcore_streams.h, build_model)
 #ifndef PCORE_FUSED_WAVES
 #define PCORE_FUSED_WAVES 4

@@ -31,9 +31,6 @@
 #ifndef PCORE_FRAG_FDIV
 #define PCORE_FRAG_FDIV 3
 #endif
-#ifndef PCORE_FLUSH_FLAT
-#define PCORE_FLUSH_FLAT 0
-#endif
 #ifndef PCORE_STEP_UNROLL
 #define PCORE_STEP_UNROLL 1
 #endif
@@ -244,7 +241,7 @@ struct FusedSmem {
     int32_t* zbuf;  // tile samples
     float2* vxy;    // kWaves * kVRing * 64: screen (x, y) of the wave's vertex ring
     float* vz;      // kWaves * kVRing * 64: camera z (cm)
-    uint2* vbd;     // kWaves * 2 * 64 (kVBounds): packed int16 sample-window bounds of the last two passes
+    uint2* vbd;     // kWaves * 2 * 64: packed int16 sample-window bounds of the last two passes
     uint2* ring;    // kWaves * kRecCap queued triangle records (phase 1); int32 point queues in phase 2
     uint32_t* ring_id;  // kWaves * kRecCap original triangle ids (colour id pass only)
     uint32_t* bitmap;
@@ -285,7 +282,7 @@ size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour) {
     size_t b = al((size_t)tile_samples * 4);
     b += al((size_t)kWaves * kRingSlots * 8);
     b += al((size_t)kWaves * kRingSlots * 4);
-    if (kVBounds) b += al((size_t)kWaves * 2 * kWave * 8);
+    b += al((size_t)kWaves * 2 * kWave * 8);
     b += al((size_t)kWaves * kRecCap * 8);
     if (colour) b += al((size_t)kWaves * kRecCap * 4);
     b += al((size_t)bitmap_words * 4);
@@ -301,8 +298,7 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
     sm.zbuf = (int32_t*)p; p += al((size_t)nsamp * 4);
     sm.vxy = (float2*)p; p += al((size_t)kWaves * kRingSlots * 8);
     sm.vz = (float*)p; p += al((size_t)kWaves * kRingSlots * 4);
-    sm.vbd = nullptr;
-    if (kVBounds) { sm.vbd = (uint2*)p; p += al((size_t)kWaves * 2 * kWave * 8); }
+    sm.vbd = (uint2*)p; p += al((size_t)kWaves * 2 * kWave * 8);
     sm.ring = (uint2*)p; p += al((size_t)kWaves * kRecCap * 8);
     sm.ring_id = nullptr;
     if (colour) { sm.ring_id = (uint32_t*)p; p += al((size_t)kWaves * kRecCap * 4); }
@@ -320,43 +316,20 @@ __device__ __forceinline__ int floor_div(int v, int s) {
     }
 }
 
-// Sample window of a triangle whose screen coordinates are not NaN (finite or infinite), straight from the
-// reference's bounding box and loop bounds (image_renderer.cuh:86-111): bmin = max(0, min p), first pixel
-// trunc(bmin + 0.5); bmax = min(W-1, max p), last pixel floor(bmax) -- for non-NaN inputs the ternary chains
-// of bbox_ref() are exactly these min / max.  Clamping to [0, 65536] / [-65536, W-1] first changes no window
-// of a <= 16384-pixel image and keeps the conversions in range.  Sample kx covers raster column kx * s,
-// sample row ky raster row H-1-ky*s.  The window is clipped to the pose window; returns its sample count.
-template <int STRIDE>
-__device__ __forceinline__ int triangle_window(float x0, float x1, float x2, float y0, float y1, float y2, int s,
-                                               float cmax0, float cmax1, int H, const SampleWin& sw, int& kx0,
-                                               int& ky0, int& nx, int& ny) {
-    const float mnx = fminf(x0, fminf(x1, x2)), mxx = fmaxf(x0, fmaxf(x1, x2));
-    const float mny = fminf(y0, fminf(y1, y2)), mxy = fmaxf(y0, fmaxf(y1, y2));
-    const int lo0 = (int)(fminf(fmaxf(mnx, 0.0f), 65536.0f) + 0.5f);
-    const int lo1 = (int)(fminf(fmaxf(mny, 0.0f), 65536.0f) + 0.5f);
-    const int hi0 = (int)floorf(fmaxf(fminf(mxx, cmax0), -65536.0f));
-    const int hi1 = (int)floorf(fmaxf(fminf(mxy, cmax1), -65536.0f));
-    const int ss = STRIDE > 0 ? STRIDE : s;
-    const int a0 = max(floor_div<STRIDE>(lo0 + ss - 1, s), sw.x0);          // lo0 >= 0: ceil
-    const int a1 = min(floor_div<STRIDE>(hi0, s), sw.x0 + sw.nx - 1);
-    const int b0 = max(floor_div<STRIDE>(H - 1 - hi1 + ss - 1, s), sw.y0);  // H-1-hi1 >= 0: ceil
-    const int b1 = min(floor_div<STRIDE>(H - 1 - lo1, s), sw.y0 + sw.ny - 1);
-    kx0 = a0;
-    ky0 = b0;
-    nx = a1 - a0 + 1;
-    ny = b1 - b0 + 1;
-    return (nx > 0 && ny > 0) ? (int)__umul24((uint32_t)nx, (uint32_t)ny) : 0;
-}
-
-// triangle_window, decomposed over the vertices.  Each of its four bounds is a monotone function of the
-// triangle's min or max screen coordinate -- a0 = A0(min x), a1 = A1(max x), b0 = B0(max y), b1 = B1(min y) --
-// so it equals the min or max of that function over the three vertices: a0 = min A0(x_i), a1 = max A1(x_i),
-// b0 = min B0(y_i), b1 = max B1(y_i) (clipping to the pose window commutes as well).  The vertex pass
-// stores (A0, B0) and (A1, B1) as int16 pairs; the triangle stage takes two packed minima and two packed
-// maxima.  At stride 8 every bound fits int16 (|bound| <= (16384 + 65536) / 8); the generic stride clamps
-// them to +-32767, which leaves a window of a <= 16384-sample image empty exactly when it was.  A NaN screen
-// coordinate marks the vertex with -32768 lower bounds (a real lower bound is >= 0), and its triangles take
-// the reference's NaN-propagating bbox instead.
+// Sample window of a triangle whose screen coordinates are not NaN (finite or infinite), from the reference's
+// bounding box and loop bounds (image_renderer.cuh:86-111): bmin = max(0, min p), first pixel trunc(bmin + 0.5);
+// bmax = min(W-1, max p), last pixel floor(bmax) -- for non-NaN inputs the ternary chains of bbox_ref() are exactly
+// these min / max.  Clamping to [0, 65536] / [-65536, W-1] first changes no window of a <= 16384-pixel image and
+// keeps the conversions in range.  Sample kx covers raster column kx * s, sample row ky raster row H-1-ky*s:
+//   a0 = ceil(trunc(max(0, min x) + 0.5) / s)      a1 = floor(floor(min(W-1, max x)) / s)
+//   b0 = ceil((H-1 - floor(min(H-1, max y))) / s)  b1 = floor((H-1 - trunc(max(0, min y) + 0.5)) / s)
+// Each bound is a monotone function of the triangle's min or max coordinate, so it equals the min or max of that
+// function over the three vertices: a0 = min A0(x_i), a1 = max A1(x_i), b0 = min B0(y_i), b1 = max B1(y_i), and
+// clipping to the pose window commutes as well.  The vertex pass stores (A0, B0) and (A1, B1) as int16 pairs;
+// the triangle stage takes two packed minima and two packed maxima.  At stride 8 every bound fits int16
+// (|bound| <= (16384 + 65536) / 8); the generic stride clamps them to +-32767, which leaves a window of a
+// <= 16384-sample image empty exactly when it was.  A NaN screen coordinate marks the vertex with -32768 lower
+// bounds (a real lower bound is >= 0), and its triangles take the reference's NaN-propagating bbox instead.
 typedef short short2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
 constexpr uint32_t kNanBounds = 0x80008000u;
@@ -443,7 +416,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     const float cmax0 = (float)(W - 1), cmax1 = (float)(H - 1);
     float2* vxy = sm.vxy + wave * kRingSlots;
     float* vz = sm.vz + wave * kRingSlots;
-    uint2* vbd = kVBounds ? sm.vbd + wave * 2 * kWave : nullptr;
+    uint2* vbd = sm.vbd + wave * 2 * kWave;
     // the pose window as int16 pairs (first sample, last sample); an empty window has last < first
     const short2v wfirst = {(short)sw.x0, (short)sw.y0};
     const short2v wlast = {(short)(sw.x0 + sw.nx - 1), (short)(sw.y0 + sw.ny - 1)};
@@ -477,24 +450,11 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     r.b0 = q1.x; r.b1 = q1.y;
                     r.c0 = q2.x; r.c1 = q2.y;
                     r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
-                    const int kx0 = rec.y & 0xfff, ky0 = (rec.y >> 12) & 0xfff;
-                    const int nx = ((rec.y >> 24) & 0xf) + 1, ny = ((rec.y >> 28) & 0xf) + 1;
+                    // one record per (triangle, sample): the sample is rec.y = kx | ky << 16
 #ifdef PCORE_FLUSH_STATS
-                    atomicAdd(&pcore_flush_stats[2], (unsigned long long)(nx * ny));
+                    atomicAdd(&pcore_flush_stats[2], 1ull);
 #endif
-#if PCORE_FLUSH_FLAT
-                    // nx * ny <= kSmallK = 4: the first sample always exists; the others (a loop the wave skips when
-                    // every record touches one sample) at q = iy * nx + ix
-                    raster_sample<IDPASS>(r, kx0, ky0, s, H, sw, sm.zbuf, cid, id);
-                    for (int q = 1; q < nx * ny; q++) {
-                        const int iy = nx == 1 ? q : (nx == 2 ? q >> 1 : 0), ix = q - iy * nx;
-                        raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
-                    }
-#else
-                    for (int iy = 0; iy < ny; iy++)
-                        for (int ix = 0; ix < nx; ix++)
-                            raster_sample<IDPASS>(r, kx0 + ix, ky0 + iy, s, H, sw, sm.zbuf, cid, id);
-#endif
+                    raster_sample<IDPASS>(r, (int)(rec.y & 0xffffu), (int)(rec.y >> 16), s, H, sw, sm.zbuf, cid, id);
                 }
             }
         }
@@ -558,7 +518,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     const float sy = qy * Hf / 2.0f + Hf / 2.0f;
                     vxy[buf * kWave + lane] = make_float2(sx, sy);
                     vz[buf * kWave + lane] = lz;
-                    if constexpr (kVBounds) vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H);
+                    vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H);
                 }
 #pragma unroll
                 for (int k = kVRing - kRefPasses - 1; k > 0; k--) hist[k] = hist[k - 1];
@@ -574,7 +534,6 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
                 const uint32_t tri = ct & 0x7ffffffu;
                 const int i0 = (int)(ct & 511u), i1 = (int)((ct >> 9) & 511u), i2 = (int)((ct >> 18) & 511u);
-#if PCORE_VBOUNDS
                 // a padding slot names slot 0 three times: its bounds are read (harmless) and nk forced to 0
                 const bool pad = ct >> 31;
                 const uint2 w0 = vbd[i0 & (2 * kWave - 1)], w1 = vbd[i1 & (2 * kWave - 1)], w2 = vbd[i2 & (2 * kWave - 1)];
@@ -604,31 +563,6 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         nk = (nx > 0 && ny > 0) ? nx * ny : 0;
                     }
                 }
-#else
-                if (!(ct >> 31)) {  // not a padding slot
-                    const float2 q0 = vxy[i0], q1 = vxy[i1], q2 = vxy[i2];
-                    const bool nan_tri = __builtin_isunordered(q0.x, q0.y) || __builtin_isunordered(q1.x, q1.y) ||
-                                         __builtin_isunordered(q2.x, q2.y);
-                    if (!nan_tri) {
-                        nk = triangle_window<STRIDE>(q0.x, q1.x, q2.x, q0.y, q1.y, q2.y, s, cmax0, cmax1, H, sw, kx0,
-                                                     ky0, nx, ny);
-                    } else {
-                        // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
-                        const float p[3][2] = {{q0.x, q0.y}, {q1.x, q1.y}, {q2.x, q2.y}};
-                        float bmin[2], bmax[2];
-                        bbox_ref(p, cmax0, cmax1, bmin, bmax);
-                        nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
-                        if (nk > 0) {  // clip to the pose window
-                            const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
-                            kx0 = max(kx0, sw.x0);
-                            ky0 = max(ky0, sw.y0);
-                            nx = kx1 - kx0;
-                            ny = ky1 - ky0;
-                            nk = (nx > 0 && ny > 0) ? nx * ny : 0;
-                        }
-                    }
-                }
-#endif
                 // large triangles: whole-wave cooperative
                 uint64_t big = __ballot(nk > kSmallK);
 #ifdef PCORE_FLUSH_STATS
@@ -677,18 +611,33 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         }
                     } while (big);
                 }
-                // small triangles: queue into the wave's record ring
+                // small triangles: one record per (triangle, sample) into the wave's record ring -- the first
+                // sample of every queued triangle, then (rare) the second to fourth of those touching more, one
+                // ballot round each; full 64-record batches are flushed after every round (<= 127 pending)
                 const bool qd = nk > 0 && nk <= kSmallK;
                 const uint64_t bq = __ballot(qd);
                 if (qd) {
-                    const uint32_t meta = (uint32_t)kx0 | ((uint32_t)ky0 << 12) | ((uint32_t)(nx - 1) << 24) |
-                                          ((uint32_t)(ny - 1) << 28);
                     const int slot = (rec_total + mbcnt64(bq)) & (kRecCap - 1);
-                    ring[slot] = make_uint2(tri, meta);
+                    ring[slot] = make_uint2(tri, (uint32_t)kx0 | ((uint32_t)ky0 << 16));
                     if (IDPASS) ring_id[slot] = cidt;
                 }
                 rec_total += __popcll(bq);
                 while (rec_total - rec_done >= kWave) flush(kWave);  // full batches only
+                if (__ballot(qd && nk > 1)) {
+                    for (int q = 1; q < kSmallK; q++) {
+                        const bool qr = qd && nk > q;
+                        const uint64_t br = __ballot(qr);
+                        if (!br) break;
+                        if (qr) {  // sample q of the window, row-major (nx * ny <= 4)
+                            const int iy = nx == 1 ? q : (nx == 2 ? q >> 1 : 0), ix = q - iy * nx;
+                            const int slot = (rec_total + mbcnt64(br)) & (kRecCap - 1);
+                            ring[slot] = make_uint2(tri, (uint32_t)(kx0 + ix) | ((uint32_t)(ky0 + iy) << 16));
+                            if (IDPASS) ring_id[slot] = cidt;
+                        }
+                        rec_total += __popcll(br);
+                        while (rec_total - rec_done >= kWave) flush(kWave);
+                    }
+                }
             }
             fp.mark(2);
             vp = vp_next;
