@@ -269,6 +269,62 @@ class PoseCore:
         return keys
 
 
+class PoseLanes:
+    """Batches in flight on one device: `lanes` independent contexts, each with its own HIP stream.
+
+    A stage-COST launch ends with a drain (its last workgroups leave CUs idle) and starts with a fill in which
+    every workgroup runs the same phase at once; on one stream the next batch waits for the drain.  Consecutive
+    batches submitted to consecutive lanes overlap one batch's drain with the next one's fill (C2, 10k poses
+    per batch: 0.40 -> 0.36 ms per batch with two lanes; tools/pipeline_probe.py).  Every lane holds the same
+    meshes, camera and observation (setup calls go to all of them) and its own scratch, so lanes never share
+    per-batch state, and each lane's results equal a single context's bit for bit.
+
+    Work on lane i runs on streams[i]: run the whole step (evaluate, select, anything reading its outputs) under
+    `with torch.cuda.stream(lanes.streams[i])`, or pass stream=.  Inputs written on another stream must be
+    ordered before the lane's stream (lanes.streams[i].wait_stream(...)); lane i's output buffers are reused
+    only by lane i, so stream order protects them."""
+
+    def __init__(self, device: int = 0, lanes: int = 2):
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        self.cores = [PoseCore(device) for _ in range(lanes)]
+        dev = torch.device("cuda", int(device))
+        self.streams = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
+
+    def __len__(self):
+        return len(self.cores)
+
+    def __getitem__(self, i: int) -> Tuple[PoseCore, torch.cuda.Stream]:
+        return self.cores[i], self.streams[i]
+
+    def upload_meshes(self, *a, **kw):
+        for c in self.cores:
+            c.upload_meshes(*a, **kw)
+
+    def set_camera(self, *a, **kw):
+        for c in self.cores:
+            c.set_camera(*a, **kw)
+
+    def set_observation(self, *a, **kw):
+        for c in self.cores:
+            c.set_observation(*a, **kw)
+
+    def set_observation_colors(self, *a, **kw):
+        for c in self.cores:
+            c.set_observation_colors(*a, **kw)
+
+    @classmethod
+    def replicate(cls, core: "PoseCore", scene_setup, lanes: int = 2) -> "PoseLanes":
+        """Lanes whose lane 0 is an existing, set-up context; scene_setup(c) repeats its setup on a new one."""
+        self = cls.__new__(cls)
+        self.cores = [core] + [PoseCore(core.device) for _ in range(lanes - 1)]
+        dev = torch.device("cuda", core.device)
+        self.streams = [torch.cuda.Stream(device=dev) for _ in range(lanes)]
+        for c in self.cores[1:]:
+            scene_setup(c)
+        return self
+
+
 def decode_keys(keys) -> Tuple[np.ndarray, np.ndarray]:
     """Per-model key -> (best cost, best global index); (INT_MAX, -1) where no pose qualified."""
     k = np.asarray(keys.cpu() if isinstance(keys, torch.Tensor) else keys, dtype=np.int64)

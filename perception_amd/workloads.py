@@ -97,6 +97,26 @@ def build(names: Sequence[str] = ("003_cracker_box",), poses_per_model: int = 10
                     stride, rank * n, K, gt_index)
 
 
+def lanes(w: Workload, count: int = 2):
+    """core.PoseLanes over the workload's context plus count - 1 more with the same meshes, camera and
+    observation (the bench keeps two batches in flight)."""
+    from .core import PoseLanes
+
+    sc = w.scene
+    dev = w.poses.device
+    src = torch.from_numpy(sc.src_depth_cm).to(dev)
+    mask = torch.from_numpy(sc.mask).to(dev)
+
+    def setup(c):
+        c.upload_meshes(sc.bank.tris, sc.bank.tris_model_count, sc.bank.colors)
+        c.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+        c.set_observation(src, mask, w.obs_xyz, w.obs_label, 0.01)
+
+    ln = PoseLanes.replicate(w.core, setup, count)
+    torch.cuda.synchronize(dev)
+    return ln
+
+
 def step(w: Workload, out, keys):
     """One pass of the hot path over the batch: render + score every pose, fold the argmin keys."""
     rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, cost_type=COST_DEPTH_6DOF,

@@ -551,3 +551,35 @@ def test_evaluate_icp_3dof_whole_scene_targets_matches_oracle(kernel, monkeypatc
     assert _bits_equal(adj.cpu().numpy(), oadj)
     assert _bits_equal(rc.cpu().numpy(), orc)
     assert _bits_equal(oc.cpu().numpy(), ooc)
+
+
+def test_pose_lanes_overlapped_batches_match_oracle(three_objects):
+    """core.PoseLanes (the bench's two batches in flight): batches submitted round-robin to two contexts on two
+    streams, with no synchronisation between them, each give the oracle's costs bit for bit."""
+    from perception_amd.core import PoseLanes
+
+    case, core, t = three_objects
+    sc = case.scene
+
+    def setup(c):
+        c.upload_meshes(sc.bank.tris, sc.bank.tris_model_count)
+        c.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+        c.set_observation(t["src"], t["mask"], t["obs_xyz"], t["obs_lab"], 0.01)
+
+    lanes = PoseLanes(0, 2)
+    for c in lanes.cores:
+        setup(c)
+    torch.cuda.synchronize()
+    n = len(case.poses)
+    outs = []
+    for i in range(6):  # six batches, three per lane, back to back
+        c, st = lanes[i % 2]
+        with torch.cuda.stream(st):
+            outs.append(c.evaluate(t["poses"], t["pm"], t["pl"], t["tot"], cost_type=2, stride=case.stride,
+                                   stream=st))
+    torch.cuda.synchronize()
+    orc, ooc, odf = case.oracle_costs(cost_type=2)
+    for rc, oc, df in outs:
+        assert rc.shape[0] == n
+        assert np.array_equal(rc.cpu().numpy(), orc) and np.array_equal(oc.cpu().numpy(), ooc)
+        assert np.array_equal(df.cpu().numpy(), odf)
