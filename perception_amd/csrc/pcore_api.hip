@@ -754,6 +754,7 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
     const float* pj = c->cam.proj;
     a.p00 = pj[0]; a.p01 = pj[1]; a.p02 = pj[2]; a.p03 = pj[3];
     a.p10 = pj[4]; a.p11 = pj[5]; a.p12 = pj[6]; a.p13 = pj[7];
+    a.proj_sparse = (pj[1] == 0.0f && pj[3] == 0.0f && pj[4] == 0.0f && pj[7] == 0.0f) ? 1 : 0;
     a.width = W;
     a.height = H;
     a.stride = p->stride;
@@ -803,6 +804,7 @@ static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& 
     const float* pj = c->cam.proj;
     a.p00 = pj[0]; a.p01 = pj[1]; a.p02 = pj[2]; a.p03 = pj[3];
     a.p10 = pj[4]; a.p11 = pj[5]; a.p12 = pj[6]; a.p13 = pj[7];
+    a.proj_sparse = (pj[1] == 0.0f && pj[3] == 0.0f && pj[4] == 0.0f && pj[7] == 0.0f) ? 1 : 0;
     a.width = W;
     a.height = H;
     a.stride = p->stride;

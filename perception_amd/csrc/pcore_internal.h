@@ -77,6 +77,7 @@ struct FusedArgs {
     int32_t num_models;
     // camera
     float p00, p01, p02, p03, p10, p11, p12, p13;  // rows 0 and 1 of proj
+    int32_t proj_sparse;  // p01, p03, p10, p13 are zeros (compute_proj's layout, renderer.cu:1386-1410)
     int32_t width, height, stride, ws, hs;
     float cx, cy, fx, fy, depth_factor;
     // observation (sampled source depth / mask at the stride grid)

@@ -409,6 +409,20 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     const float m10 = P[4], m11 = P[5], m12 = P[6], m13 = P[7];
     const float m20 = P[8], m21 = P[9], m22 = P[10], m23 = P[11];
     const int model = a.pose_model[pose];
+    // Projection with compute_proj's zeros skipped: the reference's ((p00 x + p01 y) + p02 z) + p03 with
+    // p01 = p03 = 0 differs from p00 x + p02 z only in the sign of a zero result -- which x / z * W/2 + W/2
+    // does not see (both give W/2 exactly) -- as long as the skipped products 0 * y are zeros, i.e. the camera
+    // point is finite.  It is when every model vertex is finite (model_box flag) and the bound of |row . v|
+    // over the model's box (B below, as in pose_window) stays far from FLT_MAX; NaN entries fail the test.
+    bool proj_sparse = false;
+    if (a.proj_sparse && model >= 0 && model < a.num_models) {
+        const float4 lo = a.model_box[2 * model], hi = a.model_box[2 * model + 1];
+        const float ax = fmaxf(fabsf(lo.x), fabsf(hi.x)), ay = fmaxf(fabsf(lo.y), fabsf(hi.y));
+        const float az = fmaxf(fabsf(lo.z), fabsf(hi.z));
+        const float Bx = fabsf(m00) * ax + fabsf(m01) * ay + fabsf(m02) * az + fabsf(m03);
+        const float By = fabsf(m10) * ax + fabsf(m11) * ay + fabsf(m12) * az + fabsf(m13);
+        proj_sparse = lo.w != 0.0f && Bx < 1.0e30f && By < 1.0e30f;
+    }
     __syncthreads();
 
     // ---------------- phase 1: raster of the sampled pixels ----------------
@@ -509,8 +523,14 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     const float lx = row4(m00, m01, m02, m03, cv.x, cv.y, cv.z);
                     const float ly = row4(m10, m11, m12, m13, cv.x, cv.y, cv.z);
                     const float lz = row4(m20, m21, m22, m23, cv.x, cv.y, cv.z);
-                    const float px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
-                    const float py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
+                    float px, py;
+                    if (proj_sparse) {
+                        px = a.p00 * lx + a.p02 * lz;
+                        py = a.p11 * ly + a.p12 * lz;
+                    } else {
+                        px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
+                        py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
+                    }
                     // px / lz and py / lz, IEEE-exact, sharing one refined reciprocal of lz (pcore_fdiv.h)
                     float qx, qy;
                     fdiv2_exact(px, py, lz, qx, qy);

@@ -583,3 +583,25 @@ def test_pose_lanes_overlapped_batches_match_oracle(three_objects):
         assert rc.shape[0] == n
         assert np.array_equal(rc.cpu().numpy(), orc) and np.array_equal(oc.cpu().numpy(), ooc)
         assert np.array_equal(df.cpu().numpy(), odf)
+
+
+def test_general_projection_matrix(one_object):
+    """A projection without compute_proj's zeros (skew and offsets in rows 0 / 1) takes the full four-term
+    rows in the fused kernel's vertex pass: its sampled z-buffers equal the oracle's full render, and the
+    sparse-row path of the default camera is not taken."""
+    case, _, t = one_object
+    sc = case.scene
+    proj = sc.proj.copy()
+    proj[1], proj[3], proj[4], proj[7] = np.float32(0.0123), np.float32(0.0625), np.float32(-0.0071), np.float32(-0.03)
+    core = PoseCore(0)
+    core.upload_meshes(sc.bank.tris, sc.bank.tris_model_count)
+    core.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, proj)
+    core.set_observation(t["src"], t["mask"], t["obs_xyz"], t["obs_lab"], 0.01)
+    n, s = 32, case.stride
+    hs, ws = (sc.height + s - 1) // s, sc.width // s
+    dbg = torch.empty((n, hs, ws), dtype=torch.int32, device=t["poses"].device)
+    core.evaluate(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n], cost_type=2, stride=s, dbg_zs=dbg)
+    ref = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n],
+                              case.pose_label[:n], sc.width, sc.height, proj, sc.src_depth_cm, sc.mask, 1.0)
+    assert (ref > 0).sum() > 0
+    assert np.array_equal(dbg.cpu().numpy(), ref[:, ::s, ::s])
