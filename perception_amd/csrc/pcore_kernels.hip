@@ -330,6 +330,18 @@ __device__ __forceinline__ int floor_div(int v, int s) {
 // (|bound| <= (16384 + 65536) / 8); the generic stride clamps them to +-32767, which leaves a window of a
 // <= 16384-sample image empty exactly when it was.  A NaN screen coordinate marks the vertex with -32768 lower
 // bounds (a real lower bound is >= 0), and its triangles take the reference's NaN-propagating bbox instead.
+// floor(v + 0.5) and floor(v) of a finite float of magnitude < 2^23 (exact), one instruction each
+__device__ __forceinline__ int cvt_rpi(float v) {
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+__device__ __forceinline__ int cvt_flr(float v) {
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
 typedef short short2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast(short2v, v); }
 constexpr uint32_t kNanBounds = 0x80008000u;
@@ -338,10 +350,13 @@ template <int STRIDE>
 __device__ __forceinline__ uint2 vertex_bounds(float sx, float sy, int s, float cmax0, float cmax1, int H) {
     if (__builtin_isunordered(sx, sy)) return make_uint2(kNanBounds, 0u);
     const int ss = STRIDE > 0 ? STRIDE : s;
-    const int lo0 = (int)(fminf(fmaxf(sx, 0.0f), 65536.0f) + 0.5f);
-    const int lo1 = (int)(fminf(fmaxf(sy, 0.0f), 65536.0f) + 0.5f);
-    const int hi0 = (int)floorf(fmaxf(fminf(sx, cmax0), -65536.0f));
-    const int hi1 = (int)floorf(fmaxf(fminf(sy, cmax1), -65536.0f));
+    // sx, sy are not NaN here, so each clamp is one v_med3_f32, and the clamped values are small enough
+    // (|v| <= 65536 < 2^23) that v + 0.5 is exact: trunc(v + 0.5) = floor(v + 0.5) for v >= 0 is one
+    // v_cvt_rpi_i32_f32, floor(v) one v_cvt_flr_i32_f32 (cvt_rpi / cvt_flr below)
+    const int lo0 = cvt_rpi(__builtin_amdgcn_fmed3f(sx, 0.0f, 65536.0f));
+    const int lo1 = cvt_rpi(__builtin_amdgcn_fmed3f(sy, 0.0f, 65536.0f));
+    const int hi0 = cvt_flr(__builtin_amdgcn_fmed3f(sx, -65536.0f, cmax0));
+    const int hi1 = cvt_flr(__builtin_amdgcn_fmed3f(sy, -65536.0f, cmax1));
     int A0 = floor_div<STRIDE>(lo0 + ss - 1, s), A1 = floor_div<STRIDE>(hi0, s);
     int B0 = floor_div<STRIDE>(H - 1 - hi1 + ss - 1, s), B1 = floor_div<STRIDE>(H - 1 - lo1, s);
     if constexpr (STRIDE == 0) {
@@ -427,6 +442,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
 
     // ---------------- phase 1: raster of the sampled pixels ----------------
     const float Wf = (float)W, Hf = (float)H;
+    const float hw = Wf / 2.0f, hh = Hf / 2.0f;
     const float cmax0 = (float)(W - 1), cmax1 = (float)(H - 1);
     float2* vxy = sm.vxy + wave * kRingSlots;
     float* vz = sm.vz + wave * kRingSlots;
@@ -531,11 +547,22 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         px = row4(a.p00, a.p01, a.p02, a.p03, lx, ly, lz);
                         py = row4(a.p10, a.p11, a.p12, a.p13, lx, ly, lz);
                     }
-                    // px / lz and py / lz, IEEE-exact, sharing one refined reciprocal of lz (pcore_fdiv.h)
-                    float qx, qy;
-                    fdiv2_exact(px, py, lz, qx, qy);
-                    const float sx = qx * Wf / 2.0f + Wf / 2.0f;
-                    const float sy = qy * Hf / 2.0f + Hf / 2.0f;
+                    // px / lz and py / lz sharing one refined reciprocal of lz, IEEE-exact where every exponent is
+                    // in range (pcore_fdiv.h); there |q| < 2^81, so (q * W) / 2 is q * (W / 2) exactly (a power-of-
+                    // two scaling, no overflow or underflow).  Elsewhere the reference's expressions.
+                    const float r1 = recip_refined(lz);
+                    float qx = quot_refined(px, lz, r1), qy = quot_refined(py, lz, r1);
+                    float sx = qx * hw + hw, sy = qy * hh + hh;
+                    {
+                        const uint32_t ex = fexp_bits(px), ey = fexp_bits(py), ez = fexp_bits(lz);
+                        if (!fdiv_range_ok(min(min(ex, ey), ez), max(max(ex, ey), ez))) {
+                            asm volatile("");
+                            qx = px / lz;
+                            qy = py / lz;
+                            sx = qx * Wf / 2.0f + Wf / 2.0f;
+                            sy = qy * Hf / 2.0f + Hf / 2.0f;
+                        }
+                    }
                     vxy[buf * kWave + lane] = make_float2(sx, sy);
                     vz[buf * kWave + lane] = lz;
                     vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H);
