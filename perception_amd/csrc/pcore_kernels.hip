@@ -578,36 +578,46 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
             }
             fp.mark(1);
             if (!(dbg & 2)) {
-                int nk = 0, kx0 = 0, ky0 = 0, nx = 0, ny = 0;
-                const uint32_t tri = ct & 0x7ffffffu;
-                const int i0 = (int)(ct & 511u), i1 = (int)((ct >> 9) & 511u), i2 = (int)((ct >> 18) & 511u);
+                // the triangle's clipped window, packed: pos = first sample (kx0 | ky0 << 16), nxy = its size
+                // (nx | ny << 16), nk = nx * ny samples (0: none)
+                uint32_t pos = 0u, nxy = 0u;
+                int nk = 0;
+                // the vertices' ring slots (9 bits each) and, for the bounds, their pass parity + lane (7 bits);
+                // the slots proper are decoded only where a rare path needs the screen coordinates
+                auto slot_of = [ct](int k) { return (int)((ct >> (9 * k)) & 511u); };
                 // a padding slot names slot 0 three times: its bounds are read (harmless) and nk forced to 0
                 const bool pad = ct >> 31;
-                const uint2 w0 = vbd[i0 & (2 * kWave - 1)], w1 = vbd[i1 & (2 * kWave - 1)], w2 = vbd[i2 & (2 * kWave - 1)];
-                short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
-                short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
-                const bool nan_tri = lo.x < 0 && !pad;
-                lo = __builtin_elementwise_max(lo, wfirst);
-                hi = __builtin_elementwise_min(hi, wlast);
-                kx0 = lo.x;
-                ky0 = lo.y;
-                nx = (int)hi.x - (int)lo.x + 1;
-                ny = (int)hi.y - (int)lo.y + 1;
-                nk = (nx > 0 && ny > 0 && !pad) ? (int)__umul24((uint32_t)nx, (uint32_t)ny) : 0;
-                if (nan_tri) {
-                    // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
-                    const float2 q0 = vxy[i0], q1 = vxy[i1], q2 = vxy[i2];
-                    const float p[3][2] = {{q0.x, q0.y}, {q1.x, q1.y}, {q2.x, q2.y}};
-                    float bmin[2], bmax[2];
-                    bbox_ref(p, cmax0, cmax1, bmin, bmax);
-                    nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
-                    if (nk > 0) {  // clip to the pose window
-                        const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
-                        kx0 = max(kx0, sw.x0);
-                        ky0 = max(ky0, sw.y0);
-                        nx = kx1 - kx0;
-                        ny = ky1 - ky0;
-                        nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+                {
+                    const uint2 w0 = vbd[ct & 127u], w1 = vbd[(ct >> 9) & 127u], w2 = vbd[(ct >> 18) & 127u];
+                    short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
+                    short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
+                    const bool nan_tri = lo.x < 0 && !pad;
+                    lo = __builtin_elementwise_max(lo, wfirst);
+                    hi = __builtin_elementwise_min(hi, wlast);
+                    const short2v d = hi - lo;  // (nx - 1, ny - 1), negative where the window is empty
+                    const short2v one = {1, 1};
+                    pos = __builtin_bit_cast(uint32_t, lo);
+                    nxy = __builtin_bit_cast(uint32_t, d + one);
+                    const bool nonempty = (__builtin_bit_cast(uint32_t, d) & 0x80008000u) == 0u && !pad;
+                    nk = nonempty ? (int)__umul24(nxy & 0xffffu, nxy >> 16) : 0;
+                    if (nan_tri) {
+                        // NaN screen coordinates: the reference's exact bbox with its NaN-propagating clamps
+                        const float2 q0 = vxy[slot_of(0)], q1 = vxy[slot_of(1)], q2 = vxy[slot_of(2)];
+                        const float p[3][2] = {{q0.x, q0.y}, {q1.x, q1.y}, {q2.x, q2.y}};
+                        float bmin[2], bmax[2];
+                        bbox_ref(p, cmax0, cmax1, bmin, bmax);
+                        int kx0 = 0, ky0 = 0, nx = 0, ny = 0;
+                        nk = sample_window<STRIDE>(bmin, bmax, s, H, kx0, ky0, nx, ny);
+                        if (nk > 0) {  // clip to the pose window
+                            const int kx1 = min(kx0 + nx, sw.x0 + sw.nx), ky1 = min(ky0 + ny, sw.y0 + sw.ny);
+                            kx0 = max(kx0, sw.x0);
+                            ky0 = max(ky0, sw.y0);
+                            nx = kx1 - kx0;
+                            ny = ky1 - ky0;
+                            nk = (nx > 0 && ny > 0) ? nx * ny : 0;
+                        }
+                        pos = (uint32_t)kx0 | ((uint32_t)ky0 << 16);
+                        nxy = (uint32_t)nx | ((uint32_t)ny << 16);
                     }
                 }
                 // large triangles: whole-wave cooperative
@@ -628,6 +638,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     float2 q0 = make_float2(0.f, 0.f), q1 = q0, q2 = q0;
                     float z0 = 0.0f, z1 = 0.0f, z2 = 0.0f;
                     if (nk > kSmallK) {
+                        const int i0 = slot_of(0), i1 = slot_of(1), i2 = slot_of(2);
                         q0 = vxy[i0];
                         q1 = vxy[i1];
                         q2 = vxy[i2];
@@ -645,8 +656,10 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         rb.b0 = rl(q1.x); rb.b1 = rl(q1.y);
                         rb.c0 = rl(q2.x); rb.c1 = rl(q2.y);
                         rb.z0 = rl(z0); rb.z1 = rl(z1); rb.z2 = rl(z2);
-                        const int bkx0 = __builtin_amdgcn_readlane(kx0, j), bky0 = __builtin_amdgcn_readlane(ky0, j);
-                        const int bnx = __builtin_amdgcn_readlane(nx, j), bnk = __builtin_amdgcn_readlane(nk, j);
+                        const uint32_t bpos = (uint32_t)__builtin_amdgcn_readlane((int)pos, j);
+                        const int bkx0 = (int)(bpos & 0xffffu), bky0 = (int)(bpos >> 16);
+                        const int bnx = (int)((uint32_t)__builtin_amdgcn_readlane((int)nxy, j) & 0xffffu);
+                        const int bnk = __builtin_amdgcn_readlane(nk, j);
                         const uint32_t bid = IDPASS ? (uint32_t)__builtin_amdgcn_readlane((int)cidt, j) : 0u;
                         // q / bnx without an integer division: the float quotient is within 1e-3 of q / bnx (q / bnx
                         // is at most the sample rows), so one correction step gives the exact row
@@ -663,9 +676,9 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 // ballot round each; full 64-record batches are flushed after every round (<= 127 pending)
                 const bool qd = nk > 0 && nk <= kSmallK;
                 const uint64_t bq = __ballot(qd);
-                if (qd) {
+                if (qd) {  // the record keeps the whole triangle slot word (the flush reads its 27 slot bits)
                     const int slot = (rec_total + mbcnt64(bq)) & (kRecCap - 1);
-                    ring[slot] = make_uint2(tri, (uint32_t)kx0 | ((uint32_t)ky0 << 16));
+                    ring[slot] = make_uint2(ct, pos);
                     if (IDPASS) ring_id[slot] = cidt;
                 }
                 rec_total += __popcll(bq);
@@ -676,9 +689,10 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                         const uint64_t br = __ballot(qr);
                         if (!br) break;
                         if (qr) {  // sample q of the window, row-major (nx * ny <= 4)
+                            const int nx = (int)(nxy & 0xffffu);
                             const int iy = nx == 1 ? q : (nx == 2 ? q >> 1 : 0), ix = q - iy * nx;
                             const int slot = (rec_total + mbcnt64(br)) & (kRecCap - 1);
-                            ring[slot] = make_uint2(tri, (uint32_t)(kx0 + ix) | ((uint32_t)(ky0 + iy) << 16));
+                            ring[slot] = make_uint2(ct, pos + (uint32_t)ix + ((uint32_t)iy << 16));
                             if (IDPASS) ring_id[slot] = cidt;
                         }
                         rec_total += __popcll(br);
