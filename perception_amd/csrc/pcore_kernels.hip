@@ -480,6 +480,9 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     r.b0 = q1.x; r.b1 = q1.y;
                     r.c0 = q2.x; r.c1 = q2.y;
                     r.z0 = vz[i0]; r.z1 = vz[i1]; r.z2 = vz[i2];
+                    // the depths are needed only past the inside test, but reading them with the screen
+                    // coordinates puts all six reads in one LDS round trip instead of two
+                    asm volatile("" : "+v"(r.z0), "+v"(r.z1), "+v"(r.z2));
                     // one record per (triangle, sample): the sample is rec.y = kx | ky << 16
 #ifdef PCORE_FLUSH_STATS
                     atomicAdd(&pcore_flush_stats[2], 1ull);
