@@ -374,6 +374,11 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
         shi[m] = (int)sb.streams.size();
         t0 += T;
     }
+    // one padding step and one padding vertex pass after the last stream: the fused kernel prefetches the step and
+    // the pass after the current ones unconditionally (within a model that is the next stream's first one)
+    sb.stris.insert(sb.stris.end(), kStepSlots, streams::kSlotPadding);
+    sb.sorig.insert(sb.sorig.end(), kStepSlots, 0u);
+    sb.sverts.insert(sb.sverts.end(), kStepSlots, streams::F4{0.0f, 0.0f, 0.0f, 0.0f});
     std::vector<float> soup(tri_xyz, tri_xyz + (size_t)9 * num_tris);
     HIPC(c, dev_upload(c->tris, soup));
     HIPC(c, dev_upload(c->tri_lo, tlo));

@@ -514,21 +514,30 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
 #pragma unroll
         for (int k = 0; k < kVRing - kRefPasses; k++) hist[k] = rec_total;
         int buf = 0;                 // ring buffer of the next vertex pass
-        int vp = sd.z;               // next vertex pass to consume
-        const int vp_last = max(sd.w - 1, sd.z);
+        // wave-uniform stream pointers (SGPRs): the current step's triangle slots and the next unconsumed vertex pass
+        const uint32_t* tp = a.stris + (size_t)sd.x * kStepSlots;
+        const uint32_t* op = IDPASS ? a.stri_orig + (size_t)sd.x * kStepSlots : nullptr;
+        const float4* vq = a.sverts + (size_t)sd.z * kStepSlots;
         // one step: the current step's triangle slots / vertex pass in (cv, ct, cidt); prefetches the next step's
-        // triangle slots and the next unconsumed vertex pass into (ncv, nct, ncid) -- unconditional loads, the last
-        // step re-loads itself.  The loop below alternates two register sets, so no copy of a prefetched register
-        // makes the wave wait for the load at the end of its step.
+        // triangle slots and the next unconsumed vertex pass into (ncv, nct, ncid) -- unconditional loads (after a
+        // stream's last step they read the next stream's first, or the padding step and pass the upload appends).
+        // The loop below alternates two register sets, so no copy of a prefetched register makes the wave wait
+        // for the load at the end of its step.
         auto run_step = [&](int step, const float4& cv, const uint32_t ct, const uint32_t cidt, float4& ncv,
                             uint32_t& nct, uint32_t& ncid) {
-            const int ns = min(step + 1, sd.y - 1);
-            nct = a.stris[(size_t)ns * kStepSlots + lane];
-            ncid = IDPASS ? a.stri_orig[(size_t)ns * kStepSlots + lane] : 0u;
+            (void)step;
+            tp += kStepSlots;
+            nct = tp[lane];
+            if constexpr (IDPASS) {
+                op += kStepSlots;
+                ncid = op[lane];
+            } else {
+                ncid = 0u;
+            }
             // the step's "vertex pass first" flag is in every triangle slot (pcore_internal.h)
             const bool vpass = (__builtin_amdgcn_readfirstlane((int)ct) >> 30) & 1;
-            const int vp_next = vp + (vpass ? 1 : 0);
-            ncv = a.sverts[(size_t)min(vp_next, vp_last) * kStepSlots + lane];
+            if (vpass) vq += kStepSlots;
+            ncv = vq[lane];
             if (vpass) {
                 if (rec_done < hist[kVRing - kRefPasses - 1]) {
 #ifdef PCORE_FLUSH_STATS
@@ -704,11 +713,10 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 }
             }
             fp.mark(2);
-            vp = vp_next;
         };
-        float4 cvA = a.sverts[(size_t)min(vp, vp_last) * kStepSlots + lane], cvB;
-        uint32_t ctA = a.stris[(size_t)sd.x * kStepSlots + lane], ctB, cidA, cidB;
-        cidA = IDPASS ? a.stri_orig[(size_t)sd.x * kStepSlots + lane] : 0u;
+        float4 cvA = vq[lane], cvB;
+        uint32_t ctA = tp[lane], ctB, cidA, cidB;
+        cidA = IDPASS ? op[lane] : 0u;
 #if PCORE_STEP_UNROLL
         for (int step = sd.x; step < sd.y; step += 2) {
             run_step(step, cvA, ctA, cidA, cvB, ctB, cidB);
