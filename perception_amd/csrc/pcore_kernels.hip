@@ -259,6 +259,9 @@ static_assert(kRecCap >= 128 && (kRecCap & (kRecCap - 1)) == 0, "record ring: >=
 // them row-major, sample (kx, ky) at (ky - y0) * nx + (kx - x0).
 struct SampleWin {
     int x0, y0, nx, ny;
+    // every vertex of the pose has 1 <= z < 2^41 and |x|, |y| < 2^41 after the projection (pose_window's bounds),
+    // so the vertex pass needs no per-vertex range check of its unscaled division (see the vertex pass)
+    int fastdiv;
 };
 
 template <bool IDPASS = false>
@@ -561,11 +564,14 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     }
                     // px / lz and py / lz sharing one refined reciprocal of lz, IEEE-exact where every exponent is
                     // in range (pcore_fdiv.h); there |q| < 2^81, so (q * W) / 2 is q * (W / 2) exactly (a power-of-
-                    // two scaling, no overflow or underflow).  Elsewhere the reference's expressions.
+                    // two scaling, no overflow or underflow).  Elsewhere the reference's expressions.  With the pose's
+                    // fastdiv bound (1 <= lz < 2^41, |px|, |py| < 2^41) the only operand out of range is a numerator
+                    // below 2^-40, whose quotient (IEEE or unscaled) is below 2^-40: q * W/2 + W/2 rounds to W/2 either
+                    // way, so no per-vertex check is needed.
                     const float r1 = recip_refined(lz);
                     float qx = quot_refined(px, lz, r1), qy = quot_refined(py, lz, r1);
                     float sx = qx * hw + hw, sy = qy * hh + hh;
-                    {
+                    if (!sw.fastdiv) {
                         const uint32_t ex = fexp_bits(px), ey = fexp_bits(py), ez = fexp_bits(lz);
                         if (!fdiv_range_ok(min(min(ex, ey), ez), max(max(ex, ey), ez))) {
                             asm volatile("");
@@ -739,7 +745,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
 // not finite or comes within 5 % of its depth magnitude of the camera plane.  Wave-uniform; every wave of
 // the workgroup computes the same window.
 __device__ SampleWin pose_window(const FusedArgs& a, int model, const float (&m)[12], int s) {
-    const SampleWin whole = {0, 0, a.ws, a.hs};
+    const SampleWin whole = {0, 0, a.ws, a.hs, 0};
     const float4 lo = a.model_box[2 * model], hi = a.model_box[2 * model + 1];
     const int c = lane_id() & 7;
     const float x = (c & 1) ? hi.x : lo.x, y = (c & 2) ? hi.y : lo.y, z = (c & 4) ? hi.z : lo.z;
@@ -783,7 +789,10 @@ __device__ SampleWin pose_window(const FusedArgs& a, int model, const float (&m)
     const float sf = (float)s;
     const int X0 = max(0, (int)floorf((xlo - 1.0f) / sf)), X1 = min(a.ws - 1, (int)floorf(xhi / sf));
     const int Y0 = max(0, (int)floorf((Hf - 1.0f - yhi) / sf)), Y1 = min(a.hs - 1, (int)floorf((Hf - ylo) / sf));
-    return SampleWin{X0, Y0, max(0, X1 - X0 + 1), max(0, Y1 - Y0 + 1)};
+    // Every vertex's computed z is at least the corners' minimum less the rounding of two dot products
+    // (<= 6 eps Bz); the margin 1e-5 Bz covers that.  |x|, |y| after the projection are below Pbx, Pby.
+    const bool fastdiv = lzmin - 1.0e-5f * Bz >= 1.0f && Bz < 0x1p40f && Pbx < 0x1p40f && Pby < 0x1p40f;
+    return SampleWin{X0, Y0, max(0, X1 - X0 + 1), max(0, Y1 - Y0 + 1), fastdiv ? 1 : 0};
 }
 
 // One pose of stage COST on the workgroup's LDS tile (sw.nx * sw.ny <= tile capacity).
@@ -1023,7 +1032,7 @@ fused_cost_kernel(FusedArgs a) {
 #endif
     const FusedSmem sm = carve_smem(smem_raw, a.tcap, a.bitmap_words, COLOUR);
     const int model = a.pose_model[pose];
-    SampleWin sw = {0, 0, 0, 0};  // invalid model: nothing is rendered
+    SampleWin sw = {0, 0, 0, 0, 0};  // invalid model: nothing is rendered
     if (model >= 0 && model < a.num_models) {
         float m[12];
         load_pose_rows(a.poses, pose, m);
@@ -1069,7 +1078,7 @@ __global__ void __launch_bounds__(kThreads) fused_cost_ovf_kernel(FusedArgs a) {
         float m[12];
         load_pose_rows(a.poses, pose, m);
         const SampleWin sw = (model >= 0 && model < a.num_models) ? pose_window(a, model, m, STRIDE > 0 ? STRIDE : a.stride)
-                                                                  : SampleWin{0, 0, 0, 0};
+                                                                  : SampleWin{0, 0, 0, 0, 0};
         fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
         __syncthreads();  // the next pose re-initialises the LDS
     }
@@ -1095,7 +1104,7 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
     const int ws = a.ws, nsamp = a.ws * a.hs;
     const FusedSmem sm = carve_smem(smem_raw, nsamp, 0);
     const int model = a.pose_model[pose];
-    SampleWin sw = {0, 0, 0, 0};
+    SampleWin sw = {0, 0, 0, 0, 0};
     if (model >= 0 && model < a.num_models) {
         float m[12];
         load_pose_rows(a.poses, pose, m);
