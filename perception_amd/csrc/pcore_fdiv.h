@@ -92,8 +92,10 @@ __device__ __forceinline__ int32_t frag_depth_ieee(float alpha, float beta, floa
 // factor-2 margin that also covers the rounding of f -/+ e), and where d(f - e) == d(f + e) that value is d(Q).
 // Anywhere else -- a half-integer within e, depths out of range, a NaN -- the lane takes the IEEE divisions in an
 // exec-masked branch.
+// z_known_ok: the caller guarantees every z_i in [1, 2^41] (the fused kernel's pose-level bound), so only the
+// NaN barycentric and the bracket are tested.
 __device__ __forceinline__ int32_t frag_depth_certified(float alpha, float beta, float gamma, float z0, float z1,
-                                                        float z2) {
+                                                        float z2, bool z_known_ok = false) {
     const float num = alpha + beta + gamma;
     const float oxa = alpha * __builtin_amdgcn_rcpf(z0), oya = beta * __builtin_amdgcn_rcpf(z1),
                 oza = gamma * __builtin_amdgcn_rcpf(z2);
@@ -102,8 +104,12 @@ __device__ __forceinline__ int32_t frag_depth_certified(float alpha, float beta,
     int32_t d = cvt_i32_rz_sat((f - e) + 0.5f);
     const int32_t dh = cvt_i32_rz_sat((f + e) + 0.5f);
     // fminf / fmaxf skip a NaN operand; a NaN depth makes zs NaN, a NaN barycentric makes num NaN
-    const float zmin = fminf(fminf(z0, z1), z2), zmax = fmaxf(fmaxf(z0, z1), z2), zs = z0 + z1 + z2;
-    if (!(zmin >= 0x1p-100f) || !(zmax <= 0x1p100f) || zs != zs || num != num || d != dh) {
+    bool z_ok = z_known_ok;
+    if (!z_known_ok) {
+        const float zmin = fminf(fminf(z0, z1), z2), zmax = fmaxf(fmaxf(z0, z1), z2), zs = z0 + z1 + z2;
+        z_ok = zmin >= 0x1p-100f && zmax <= 0x1p100f && zs == zs;
+    }
+    if (!z_ok || num != num || d != dh) {
         asm volatile("");
         d = frag_depth_ieee(alpha, beta, gamma, z0, z1, z2);
     }

@@ -117,7 +117,7 @@ __device__ __forceinline__ bool loop_bounds(float bmin, float bmax, int& lo, int
 // One fragment test at raster pixel (P0, P1) (image_renderer.cuh:44-57, 112-129).  Returns true and the
 // int depth if the pixel is inside the triangle (NaN barycentrics count as inside, as in the reference).
 __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1, float C0, float C1, float z0,
-                                         float z1, float z2, float P0, float P1, int32_t& depth) {
+                                         float z1, float z2, float P0, float P1, int32_t& depth, bool z_ok = false) {
     const float area = 0.5f * ((C0 - A0) * (B1 - A1) - (B0 - A0) * (C1 - A1));
 #if PCORE_FRAG_FDIV == 2
     // The five quotients through the unscaled steps of pcore_fdiv.h, each IEEE-exact when its operands' exponents
@@ -164,7 +164,7 @@ __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1,
     const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
     const float alpha = 1.0f - beta - gamma;
     if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
-    depth = frag_depth_certified(alpha, beta, gamma, z0, z1, z2);
+    depth = frag_depth_certified(alpha, beta, gamma, z0, z1, z2, z_ok);
     return true;
 #else
 #if PCORE_FRAG_FDIV == 1
@@ -270,7 +270,7 @@ __device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, i
     const float P0 = (float)(kx * s);
     const float P1 = (float)(H - 1 - ky * s);
     int32_t d;
-    if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d)) {
+    if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d, w.fastdiv != 0)) {
         const int k = (int)__umul24((uint32_t)(ky - w.y0), (uint32_t)w.nx) + (kx - w.x0);
         if constexpr (IDPASS) {
             if (d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
@@ -350,8 +350,9 @@ __device__ __forceinline__ short2v as_s2(uint32_t v) { return __builtin_bit_cast
 constexpr uint32_t kNanBounds = 0x80008000u;
 
 template <int STRIDE>
-__device__ __forceinline__ uint2 vertex_bounds(float sx, float sy, int s, float cmax0, float cmax1, int H) {
-    if (__builtin_isunordered(sx, sy)) return make_uint2(kNanBounds, 0u);
+__device__ __forceinline__ uint2 vertex_bounds(float sx, float sy, int s, float cmax0, float cmax1, int H,
+                                              bool finite = false) {
+    if (!finite && __builtin_isunordered(sx, sy)) return make_uint2(kNanBounds, 0u);
     const int ss = STRIDE > 0 ? STRIDE : s;
     // sx, sy are not NaN here, so each clamp is one v_med3_f32, and the clamped values are small enough
     // (|v| <= 65536 < 2^23) that v + 0.5 is exact: trunc(v + 0.5) = floor(v + 0.5) for v >= 0 is one
@@ -583,7 +584,7 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     }
                     vxy[buf * kWave + lane] = make_float2(sx, sy);
                     vz[buf * kWave + lane] = lz;
-                    vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H);
+                    vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H, sw.fastdiv != 0);
                 }
 #pragma unroll
                 for (int k = kVRing - kRefPasses - 1; k > 0; k--) hist[k] = hist[k - 1];
@@ -609,7 +610,8 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     const uint2 w0 = vbd[ct & 127u], w1 = vbd[(ct >> 9) & 127u], w2 = vbd[(ct >> 18) & 127u];
                     short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
                     short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
-                    const bool nan_tri = lo.x < 0 && !pad;
+                    // (fastdiv poses have finite screen coordinates: no NaN vertex)
+                    const bool nan_tri = !sw.fastdiv && lo.x < 0 && !pad;
                     lo = __builtin_elementwise_max(lo, wfirst);
                     hi = __builtin_elementwise_min(hi, wlast);
                     const short2v d = hi - lo;  // (nx - 1, ny - 1), negative where the window is empty
