@@ -94,8 +94,9 @@ __device__ __forceinline__ int32_t frag_depth_ieee(float alpha, float beta, floa
 // exec-masked branch.
 // z_known_ok: the caller guarantees every z_i in [1, 2^41] (the fused kernel's pose-level bound), so only the
 // NaN barycentric and the bracket are tested.
+// active = false: the caller discards the result (a pixel outside the triangle), so the fallback is not taken.
 __device__ __forceinline__ int32_t frag_depth_certified(float alpha, float beta, float gamma, float z0, float z1,
-                                                        float z2, bool z_known_ok = false) {
+                                                        float z2, bool z_known_ok = false, bool active = true) {
     const float num = alpha + beta + gamma;
     const float oxa = alpha * __builtin_amdgcn_rcpf(z0), oya = beta * __builtin_amdgcn_rcpf(z1),
                 oza = gamma * __builtin_amdgcn_rcpf(z2);
@@ -109,7 +110,7 @@ __device__ __forceinline__ int32_t frag_depth_certified(float alpha, float beta,
         const float zmin = fminf(fminf(z0, z1), z2), zmax = fmaxf(fmaxf(z0, z1), z2), zs = z0 + z1 + z2;
         z_ok = zmin >= 0x1p-100f && zmax <= 0x1p100f && zs == zs;
     }
-    if (!z_ok || num != num || d != dh) {
+    if (active && (!z_ok || num != num || d != dh)) {
         asm volatile("");
         d = frag_depth_ieee(alpha, beta, gamma, z0, z1, z2);
     }

@@ -26,8 +26,8 @@
 
 #pragma clang fp contract(off)
 
-// fragment depth quotients: 0 IEEE divisions, 1 / 2 unscaled exact divisions (measured slower), 3 reciprocal
-// estimates with an error certificate and IEEE fallback (pcore_fdiv.h, frag_depth_certified)
+// fragment depth quotients: 0 IEEE divisions, 3 reciprocal estimates with an error certificate and IEEE fallback
+// (pcore_fdiv.h, frag_depth_certified); unscaled exact divisions for all five quotients measured slower
 #ifndef PCORE_FRAG_FDIV
 #define PCORE_FRAG_FDIV 3
 #endif
@@ -44,6 +44,9 @@ constexpr int kThreads = kWaves * kWave;
 // 64 remain and a batch appends at most 64, so 128 never overflows; phase 2 reuses it as a point queue of
 // up to 127 (tile index, kx | ky << 16) pairs
 constexpr int kRecCap = 128;
+// per-wave record ring stride: kRecCap records + a discard record (lanes with nothing to queue write there, so the
+// queue store needs no branch) + one for 16-byte alignment
+constexpr int kRecStride = kRecCap + 2;
 constexpr int64_t PCORE_KEY_NONE_DEV = 0x7fffffffffffffffLL;
 constexpr int kSmallK = 4;    // triangles touching <= kSmallK samples are queued; larger ones are
                               // processed cooperatively by the whole wave
@@ -116,77 +119,31 @@ __device__ __forceinline__ bool loop_bounds(float bmin, float bmax, int& lo, int
 
 // One fragment test at raster pixel (P0, P1) (image_renderer.cuh:44-57, 112-129).  Returns true and the
 // int depth if the pixel is inside the triangle (NaN barycentrics count as inside, as in the reference).
+// Returns whether the pixel is inside (NaN barycentrics count as inside, as in the reference) and sets the depth
+// for inside pixels; every lane runs the same instructions (no branch on the inside test), so a batch of
+// fragment tests is one straight-line block plus the depth's rare IEEE fallback.
 __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1, float C0, float C1, float z0,
                                          float z1, float z2, float P0, float P1, int32_t& depth, bool z_ok = false) {
     const float area = 0.5f * ((C0 - A0) * (B1 - A1) - (B0 - A0) * (C1 - A1));
-#if PCORE_FRAG_FDIV == 2
-    // The five quotients through the unscaled steps of pcore_fdiv.h, each IEEE-exact when its operands' exponents
-    // are in range; an exec-masked IEEE branch takes the lanes where one is not.  alpha / beta / gamma may also be
-    // zero: a zero quotient may then come out with the other sign, but the three quotients are only summed and
-    // never all zero (alpha = 1 - beta - gamma), so the sum -- and the depth -- is the IEEE one bit for bit.
-    float base_inv = quot_refined(1.0f, area, recip_refined(area));
-    {
-        const uint32_t ua = __float_as_uint(area) & 0x7fffffffu;
-        if (!absbits_range_ok(ua, ua)) {
-            asm volatile("");
-            base_inv = 1.0f / area;
-        }
-    }
-    const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
-    const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
-    const float alpha = 1.0f - beta - gamma;
-    if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
-    const float num = alpha + beta + gamma;
-    const float ox = quot_refined(alpha, z0, recip_refined(z0));
-    const float oy = quot_refined(beta, z1, recip_refined(z1));
-    const float oz = quot_refined(gamma, z2, recip_refined(z2));
-    const float den = ox + oy + oz;
-    float frag = quot_refined(num, den, recip_refined(den));
-    {
-        const uint32_t m = 0x7fffffffu;
-        const uint32_t uz0 = __float_as_uint(z0) & m, uz1 = __float_as_uint(z1) & m, uz2 = __float_as_uint(z2) & m;
-        const uint32_t ub0 = absbits_zero_as_one(alpha), ub1 = absbits_zero_as_one(beta), ub2 = absbits_zero_as_one(gamma);
-        const uint32_t un = __float_as_uint(num) & m, ud = __float_as_uint(den) & m;
-        const uint32_t umin = min(min(min(uz0, uz1), min(uz2, ub0)), min(min(ub1, ub2), min(un, ud)));
-        const uint32_t umax = max(max(max(uz0, uz1), max(uz2, ub0)), max(max(ub1, ub2), max(un, ud)));
-        if (!absbits_range_ok(umin, umax)) {
-            asm volatile("");
-            frag = (alpha + beta + gamma) / (alpha / z0 + beta / z1 + gamma / z2);
-        }
-    }
-    depth = cvt_i32_rz_sat(frag + 0.5f);
-    return true;
-#elif PCORE_FRAG_FDIV == 3
-    // IEEE barycentrics and inside test; the depth quotient chain through frag_depth_certified (pcore_fdiv.h):
-    // reciprocal estimates with an error certificate, the IEEE divisions only where the certificate fails
     const float base_inv = 1.0f / area;
     const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
     const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
     const float alpha = 1.0f - beta - gamma;
-    if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
-    depth = frag_depth_certified(alpha, beta, gamma, z0, z1, z2, z_ok);
-    return true;
+    const bool inside =
+        !(alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f);
+#if PCORE_FRAG_FDIV == 3
+    // the depth quotient chain through reciprocal estimates with an error certificate, the IEEE divisions only
+    // where the certificate fails (pcore_fdiv.h, frag_depth_certified); outside lanes never take the fallback
+    depth = frag_depth_certified(alpha, beta, gamma, z0, z1, z2, z_ok, inside);
 #else
-#if PCORE_FRAG_FDIV == 1
-    // IEEE-exact quotients without the range-scaling steps (pcore_fdiv.h)
-    const float base_inv = fdiv_exact(1.0f, area);
-#else
-    const float base_inv = 1.0f / area;
+    (void)z_ok;
+    depth = 0;
+    if (inside) {
+        const float ox = alpha / z0, oy = beta / z1, oz = gamma / z2;
+        depth = cvt_i32_rz_sat((alpha + beta + gamma) / (ox + oy + oz) + 0.5f);
+    }
 #endif
-    const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
-    const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
-    const float alpha = 1.0f - beta - gamma;
-    if (alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f) return false;
-#if PCORE_FRAG_FDIV == 1
-    const float ox = fdiv_exact(alpha, z0), oy = fdiv_exact(beta, z1), oz = fdiv_exact(gamma, z2);
-    const float frag = fdiv_exact(alpha + beta + gamma, ox + oy + oz);
-#else
-    const float ox = alpha / z0, oy = beta / z1, oz = gamma / z2;
-    const float frag = (alpha + beta + gamma) / (ox + oy + oz);
-#endif
-    depth = cvt_i32_rz_sat(frag + 0.5f);
-    return true;
-#endif
+    return inside;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -242,8 +199,8 @@ struct FusedSmem {
     float2* vxy;    // kWaves * kVRing * 64: screen (x, y) of the wave's vertex ring
     float* vz;      // kWaves * kVRing * 64: camera z (cm)
     uint2* vbd;     // kWaves * 2 * 64: packed int16 sample-window bounds of the last two passes
-    uint2* ring;    // kWaves * kRecCap queued triangle records (phase 1); int32 point queues in phase 2
-    uint32_t* ring_id;  // kWaves * kRecCap original triangle ids (colour id pass only)
+    uint2* ring;    // kWaves * kRecStride queued triangle records (phase 1); int32 point queues in phase 2
+    uint32_t* ring_id;  // kWaves * kRecStride original triangle ids (colour id pass only)
     uint32_t* bitmap;
     int32_t* counters;  // [0] bad, [1] explained, [2] points
 };
@@ -270,13 +227,12 @@ __device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, i
     const float P0 = (float)(kx * s);
     const float P1 = (float)(H - 1 - ky * s);
     int32_t d;
-    if (fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d, w.fastdiv != 0)) {
-        const int k = (int)__umul24((uint32_t)(ky - w.y0), (uint32_t)w.nx) + (kx - w.x0);
-        if constexpr (IDPASS) {
-            if (d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
-        } else {
-            atomicMin(&zbuf[k], d);
-        }
+    const bool in = fragment(r.a0, r.a1, r.b0, r.b1, r.c0, r.c1, r.z0, r.z1, r.z2, P0, P1, d, w.fastdiv != 0);
+    const int k = (int)__umul24((uint32_t)(ky - w.y0), (uint32_t)w.nx) + (kx - w.x0);  // inside the window
+    if constexpr (IDPASS) {
+        if (in && d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
+    } else {
+        atomicMin(&zbuf[k], in ? d : INT_MAX);  // INT_MAX leaves the sample as it is
     }
 }
 
@@ -286,8 +242,8 @@ size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour) {
     b += al((size_t)kWaves * kRingSlots * 8);
     b += al((size_t)kWaves * kRingSlots * 4);
     b += al((size_t)kWaves * 2 * kWave * 8);
-    b += al((size_t)kWaves * kRecCap * 8);
-    if (colour) b += al((size_t)kWaves * kRecCap * 4);
+    b += al((size_t)kWaves * kRecStride * 8);
+    if (colour) b += al((size_t)kWaves * kRecStride * 4);
     b += al((size_t)bitmap_words * 4);
     b += 16;
     return b;
@@ -302,9 +258,9 @@ __device__ __forceinline__ FusedSmem carve_smem(unsigned char* smem_raw, int nsa
     sm.vxy = (float2*)p; p += al((size_t)kWaves * kRingSlots * 8);
     sm.vz = (float*)p; p += al((size_t)kWaves * kRingSlots * 4);
     sm.vbd = (uint2*)p; p += al((size_t)kWaves * 2 * kWave * 8);
-    sm.ring = (uint2*)p; p += al((size_t)kWaves * kRecCap * 8);
+    sm.ring = (uint2*)p; p += al((size_t)kWaves * kRecStride * 8);
     sm.ring_id = nullptr;
-    if (colour) { sm.ring_id = (uint32_t*)p; p += al((size_t)kWaves * kRecCap * 4); }
+    if (colour) { sm.ring_id = (uint32_t*)p; p += al((size_t)kWaves * kRecStride * 4); }
     sm.bitmap = (uint32_t*)p; p += al((size_t)bitmap_words * 4);
     sm.counters = (int32_t*)p;
     return sm;
@@ -454,8 +410,8 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     // the pose window as int16 pairs (first sample, last sample); an empty window has last < first
     const short2v wfirst = {(short)sw.x0, (short)sw.y0};
     const short2v wlast = {(short)(sw.x0 + sw.nx - 1), (short)(sw.y0 + sw.ny - 1)};
-    uint2* ring = sm.ring + wave * kRecCap;
-    uint32_t* ring_id = IDPASS ? sm.ring_id + wave * kRecCap : nullptr;
+    uint2* ring = sm.ring + wave * kRecStride;
+    uint32_t* ring_id = IDPASS ? sm.ring_id + wave * kRecStride : nullptr;
     // record ring: wave-uniform monotone counters of appended and flushed records; record i lives in slot
     // i mod kRecCap.  Full 64-record batches are flushed as soon as they exist; a partial batch only when a
     // vertex pass would overwrite vertices a pending record may reference, at a stream switch and at the end.
@@ -551,7 +507,8 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 }
                 // vertex stage: model transform, keep camera z, projection rows 0/1, viewport
                 // (image_renderer.cuh:296-305, 82-84)
-                if (cv.w != 0.0f && !(dbg & 8)) {
+                // every lane transforms its slot: a padding lane (cv.w == 0) writes a slot no triangle names
+                if (!(dbg & 8)) {
                     const float lx = row4(m00, m01, m02, m03, cv.x, cv.y, cv.z);
                     const float ly = row4(m10, m11, m12, m13, cv.x, cv.y, cv.z);
                     const float lz = row4(m20, m21, m22, m23, cv.x, cv.y, cv.z);
@@ -696,8 +653,9 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 // ballot round each; full 64-record batches are flushed after every round (<= 127 pending)
                 const bool qd = nk > 0 && nk <= kSmallK;
                 const uint64_t bq = __ballot(qd);
-                if (qd) {  // the record keeps the whole triangle slot word (the flush reads its 27 slot bits)
-                    const int slot = (rec_total + mbcnt64(bq)) & (kRecCap - 1);
+                {  // the record keeps the whole triangle slot word (the flush reads its 27 slot bits); lanes with
+                   // nothing to queue write the discard record instead of branching around the store
+                    const int slot = qd ? (rec_total + mbcnt64(bq)) & (kRecCap - 1) : kRecCap;
                     ring[slot] = make_uint2(ct, pos);
                     if (IDPASS) ring_id[slot] = cidt;
                 }
@@ -832,7 +790,7 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
 
     // ---------------- phase 2: occlusion, unprojection, 1-NN, counts ----------------
     // per-wave point queue in the (now free) triangle ring: (tile index, kx | ky << 16) pairs
-    int32_t* queue = reinterpret_cast<int32_t*>(sm.ring + wave * kRecCap);  // <= 127 pairs (kRecCap >= 128)
+    int32_t* queue = reinterpret_cast<int32_t*>(sm.ring + wave * kRecStride);  // <= 127 pairs (kRecCap >= 128)
     int qcount = 0;
     const int grid_id = use_seg ? pl : a.num_grids;
     const bool grid_ok = use_seg ? (pl >= 0 && pl < a.num_grids) : true;
