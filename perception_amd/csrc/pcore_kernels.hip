@@ -823,20 +823,21 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
                         const int ix0 = (int)floorf(fmaxf(lx, 0.0f)), ix1 = min(g.nx - 1, (int)floorf(hx));
                         const int iy0 = (int)floorf(fmaxf(ly, 0.0f)), iy1 = min(g.ny - 1, (int)floorf(hy));
                         const int iz0 = (int)floorf(fmaxf(lz, 0.0f)), iz1 = min(g.nz - 1, (int)floorf(hz));
-                        // the radius box spans <= 2 cells per axis (cell >= 2 r): fetch the <= 8 cell ranges
-                        // with independent loads, then each cell's points four at a time (clamped loads
-                        // issued together) -- the (distance, index) minimum does not depend on the order
-                        int cb[8], ce[8];
+                        // the radius box spans <= 2 cells per axis (cell >= 2.02 r): the <= 2 cells along x of one
+                        // (y, z) row are adjacent in the CSR order, so their points form ONE range -- <= 4 ranges,
+                        // fetched with independent loads, then each range's points four at a time (clamped loads
+                        // issued together); the (distance, index) minimum does not depend on the order
+                        int cb[4], ce[4];
 #pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            const int ix = ix0 + (q & 1), iy = iy0 + ((q >> 1) & 1), iz = iz0 + (q >> 2);
-                            const bool ok = ix <= ix1 && iy <= iy1 && iz <= iz1;
-                            const int c = g.cell_base + (iz * g.ny + iy) * g.nx + ix;
+                        for (int q = 0; q < 4; q++) {
+                            const int iy = iy0 + (q & 1), iz = iz0 + (q >> 1);
+                            const bool ok = iy <= iy1 && iz <= iz1;
+                            const int c = g.cell_base + (iz * g.ny + iy) * g.nx + ix0;
                             cb[q] = ok ? a.cell_start[c] : 0;
-                            ce[q] = ok ? a.cell_start[c + 1] : 0;
+                            ce[q] = ok ? a.cell_start[c + 1 + (ix1 - ix0)] : 0;
                         }
 #pragma unroll
-                        for (int q = 0; q < 8; q++) {
+                        for (int q = 0; q < 4; q++) {
                             for (int pi = cb[q]; pi < ce[q]; pi += 4) {
                                 float4 o[4];
 #pragma unroll
