@@ -129,8 +129,14 @@ __device__ __forceinline__ bool fragment(float A0, float A1, float B0, float B1,
     const float beta = 0.5f * ((C0 - A0) * (P1 - A1) - (P0 - A0) * (C1 - A1)) * base_inv;
     const float gamma = 0.5f * ((P0 - A0) * (B1 - A1) - (B0 - A0) * (P1 - A1)) * base_inv;
     const float alpha = 1.0f - beta - gamma;
-    const bool inside =
-        !(alpha < -0.0f || beta < -0.0f || gamma < -0.0f || alpha > 1.0f || beta > 1.0f || gamma > 1.0f);
+    // !(alpha < -0 || beta < -0 || gamma < -0 || alpha > 1 || beta > 1 || gamma > 1) as one v_min3 / v_max3 each:
+    // the three are arithmetic results (quiet NaNs at most), on which v_min3 / v_max3 follow IEEE minNum / maxNum
+    // -- a NaN operand is skipped, as in the comparisons, and an all-NaN triple gives NaN (inside, as in the
+    // reference) -- so the compiler's canonicalising v_max per operand (it cannot know there is no sNaN) is not needed
+    float mn, mx;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(mn) : "v"(alpha), "v"(beta), "v"(gamma));
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(mx) : "v"(alpha), "v"(beta), "v"(gamma));
+    const bool inside = !(mn < -0.0f) && !(mx > 1.0f);
 #if PCORE_FRAG_FDIV == 3
     // the depth quotient chain through reciprocal estimates with an error certificate, the IEEE divisions only
     // where the certificate fails (pcore_fdiv.h, frag_depth_certified); outside lanes never take the fallback
