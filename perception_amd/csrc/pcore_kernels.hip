@@ -208,7 +208,7 @@ struct FusedSmem {
     uint2* ring;    // kWaves * kRecStride queued triangle records (phase 1); int32 point queues in phase 2
     uint32_t* ring_id;  // kWaves * kRecStride original triangle ids (colour id pass only)
     uint32_t* bitmap;
-    int32_t* counters;  // [0] bad, [1] explained, [2] points
+    int32_t* counters;  // [0] bad, [1] explained, [2] points; [4..8] the pose window (x0, y0, nx, ny, fastdiv)
 };
 constexpr int kRingSlots = kVRing * kWave;
 static_assert(kRingSlots <= (1 << kRingSlotBits), "vertex ring slots must fit the 9-bit triangle indices");
@@ -251,7 +251,7 @@ size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour) {
     b += al((size_t)kWaves * kRecStride * 8);
     if (colour) b += al((size_t)kWaves * kRecStride * 4);
     b += al((size_t)bitmap_words * 4);
-    b += 16;
+    b += 48;  // counters: [0] bad, [1] explained, [2] points; [4..8] the pose window (fused_cost_kernel)
     return b;
 }
 
@@ -998,13 +998,27 @@ fused_cost_kernel(FusedArgs a) {
     } end_clock{pose};
 #endif
     const FusedSmem sm = carve_smem(smem_raw, a.tcap, a.bitmap_words, COLOUR);
-    const int model = a.pose_model[pose];
-    SampleWin sw = {0, 0, 0, 0, 0};  // invalid model: nothing is rendered
-    if (model >= 0 && model < a.num_models) {
-        float m[12];
-        load_pose_rows(a.poses, pose, m);
-        sw = pose_window(a, model, m, STRIDE > 0 ? STRIDE : a.stride);
+    // the pose window, by wave 0 only (every wave would compute the same one), shared through LDS
+    if (threadIdx.x < kWave) {
+        const int model = a.pose_model[pose];
+        SampleWin w = {0, 0, 0, 0, 0};  // invalid model: nothing is rendered
+        if (model >= 0 && model < a.num_models) {
+            float m[12];
+            load_pose_rows(a.poses, pose, m);
+            w = pose_window(a, model, m, STRIDE > 0 ? STRIDE : a.stride);
+        }
+        if (threadIdx.x == 0) {
+            sm.counters[4] = w.x0;
+            sm.counters[5] = w.y0;
+            sm.counters[6] = w.nx;
+            sm.counters[7] = w.ny;
+            sm.counters[8] = w.fastdiv;
+        }
     }
+    __syncthreads();
+    const SampleWin sw = {__builtin_amdgcn_readfirstlane(sm.counters[4]), __builtin_amdgcn_readfirstlane(sm.counters[5]),
+                          __builtin_amdgcn_readfirstlane(sm.counters[6]), __builtin_amdgcn_readfirstlane(sm.counters[7]),
+                          __builtin_amdgcn_readfirstlane(sm.counters[8])};
     const int tn = sw.nx * sw.ny;
     if (threadIdx.x == 0) {
         int b = 0;
