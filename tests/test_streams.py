@@ -1,0 +1,79 @@
+"""Host-side invariants of the fused kernel's vertex-ring streams (perception_amd/csrc/pcore_streams.h, the mesh
+format pcore_upload_meshes builds): every triangle in exactly one slot, each vertex slot naming a ring entry that
+holds that vertex's exact position and was written by one of the last two vertex passes, one pass per flagged step.
+The GPU parity tests catch a broken stream only through wrong depths; these check the builder directly, on the CPU,
+through tools/stream_stats.cpp compiled with g++ (no GPU, no HIP)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from perception_amd import synthetic as syn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VRING, REF_PASSES, WAVES = 4, 2, 4  # pcore_internal.h: kVRing, kRefPasses, kFusedWaves
+
+
+@pytest.fixture(scope="module")
+def lib(tmp_path_factory):
+    out = tmp_path_factory.mktemp("streams") / "libstreamcheck.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", os.path.join(ROOT, "tools", "stream_stats.cpp"),
+                    "-o", str(out)], check=True)
+    L = ctypes.CDLL(str(out))
+    L.stream_check.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_void_p]
+    L.stream_check.restype = ctypes.c_int
+    return L
+
+
+def check(lib, tris, streams=WAVES, vring=VRING, ref=REF_PASSES, chunks=1):
+    t = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    info = np.zeros(4, np.int64)
+    rc = lib.stream_check(t.ctypes.data, t.shape[0], streams, vring, ref, chunks, info.ctypes.data)
+    assert rc == 0, f"stream invariant {-rc} broken"
+    return dict(zip(["passes", "steps", "verts", "streams"], info.tolist()))
+
+
+@pytest.mark.parametrize("k", [1, 4, 32])
+def test_box_streams(lib, k):
+    info = check(lib, syn.box_mesh((0.06, 0.158, 0.21), k))
+    assert info["verts"] == 6 * (k + 1) ** 2 - 12 * (k - 1) - 16 if k > 1 else info["verts"] == 8
+    if k == 32:  # the C2 mesh: about one vertex load per two triangles ("Vertex-ring streams")
+        assert info["passes"] * 64 < 1.2 * info["verts"]
+        assert info["steps"] < 1.05 * (12 * k * k) / 64 + 2 * WAVES
+
+
+def test_cylinder_streams(lib):
+    check(lib, syn.cylinder_mesh(0.066, 0.101))
+
+
+@pytest.mark.parametrize("name", ["006_mustard_bottle", "024_bowl", "040_large_marker"])
+def test_ycb_proxy_streams(lib, name):
+    check(lib, syn.ycb_proxy(name).tris)
+
+
+def test_random_soup_with_shared_degenerate_and_nan_vertices(lib):
+    """Unstructured triangles over a small vertex pool (heavy sharing, no adjacency order to exploit), triangles
+    repeating a vertex, duplicated triangles and NaN coordinates (exact-bit vertex identity)."""
+    rng = np.random.default_rng(7)
+    pool = rng.normal(size=(300, 3)).astype(np.float32)
+    pool[5] = np.nan
+    pool[6] = [np.inf, 0.0, -np.inf]
+    ids = rng.integers(0, len(pool), size=(5000, 3))
+    ids[::17, 1] = ids[::17, 0]  # degenerate: a repeated vertex
+    ids[1::23] = ids[::23][: len(ids[1::23])]  # duplicated triangles
+    check(lib, pool[ids].reshape(-1, 9))
+
+
+@pytest.mark.parametrize("T", [1, 2, 63, 64, 65, 257])
+def test_small_meshes(lib, T):
+    rng = np.random.default_rng(T)
+    check(lib, rng.normal(size=(T, 9)))
+
+
+def test_stream_and_ring_parameters(lib):
+    tris = syn.box_mesh((0.06, 0.158, 0.21), 16)
+    for streams, vring, chunks in [(1, 4, 1), (4, 6, 1), (8, 4, 4), (4, 4, 4)]:
+        check(lib, tris, streams=streams, vring=vring, chunks=chunks)
