@@ -3,7 +3,8 @@
 // experiments on the CPU.
 //
 // Input: one model's triangles as unique-vertex ids (tv, 3 per triangle) and the vertex positions.  The
-// triangles are put in a locality order (greedy adjacency growth), cut into `num_streams` contiguous streams
+// triangles are put in a locality order (greedy adjacency growth, or a sweep of normal-binned surface patches when
+// that needs fewer vertex passes), cut into `num_streams` contiguous streams
 // of near-equal length, and every stream is turned into steps by simulating the kernel's vertex ring:
 //   - a vertex pass loads the vertices the next triangles miss -- those not loaded by the previous pass --
 //     in order of first use, up to 64;
@@ -16,6 +17,7 @@
 // A triangle names each vertex by the ring slot of its latest load: (pass mod kVRing) * 64 + lane.
 #pragma once
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -87,21 +89,78 @@ inline std::vector<int> locality_order(const std::vector<int>& tv, int num_verts
     return order;
 }
 
+// Sweep order: triangles binned by the dominant axis (and sign) of their normal, each bin swept along the principal
+// axis of its triangle centroids (stable for equal keys), so a bin is traversed in rows across its short extent.
+// On the tessellated cylinders of the YCB proxies this halves the vertex reloads of the greedy growth order (the
+// side's rows wrap around the axis and outgrow the two-pass window); on the boxes the greedy order stays ahead, so
+// build_model keeps whichever order needs fewer vertex passes.
+inline std::vector<int> sweep_order(const std::vector<int>& tv, const std::vector<float>& vxyz) {
+    const int T = (int)tv.size() / 3;
+    std::vector<int> bin(T);
+    std::vector<float> cx(T), cy(T), cz(T);
+    for (int t = 0; t < T; t++) {
+        const float* a = &vxyz[3 * tv[3 * t]];
+        const float* b = &vxyz[3 * tv[3 * t + 1]];
+        const float* c = &vxyz[3 * tv[3 * t + 2]];
+        const double ux = b[0] - a[0], uy = b[1] - a[1], uz = b[2] - a[2];
+        const double vx = c[0] - a[0], vy = c[1] - a[1], vz = c[2] - a[2];
+        const double nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
+        const double ax = std::fabs(nx), ay = std::fabs(ny), az = std::fabs(nz);
+        int bb;
+        if (!(ax == ax && ay == ay && az == az)) bb = 6;
+        else if (ax >= ay && ax >= az) bb = nx >= 0 ? 0 : 1;
+        else if (ay >= az) bb = ny >= 0 ? 2 : 3;
+        else bb = nz >= 0 ? 4 : 5;
+        bin[t] = bb;
+        cx[t] = (a[0] + b[0] + c[0]) / 3.0f; cy[t] = (a[1] + b[1] + c[1]) / 3.0f; cz[t] = (a[2] + b[2] + c[2]) / 3.0f;
+        if (!(cx[t] == cx[t] && cy[t] == cy[t] && cz[t] == cz[t])) { cx[t] = cy[t] = cz[t] = 0.0f; bin[t] = 6; }
+    }
+    std::vector<int> order;
+    order.reserve(T);
+    for (int bb = 0; bb < 7; bb++) {
+        std::vector<int> ts;
+        for (int t = 0; t < T; t++) if (bin[t] == bb) ts.push_back(t);
+        if (ts.empty()) continue;
+        // principal axis of the centroids (power iteration on the covariance)
+        double m[3] = {0, 0, 0};
+        for (int t : ts) { m[0] += cx[t]; m[1] += cy[t]; m[2] += cz[t]; }
+        for (double& v : m) v /= ts.size();
+        double C[3][3] = {{0}};
+        for (int t : ts) {
+            const double d[3] = {cx[t] - m[0], cy[t] - m[1], cz[t] - m[2]};
+            for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) C[i][j] += d[i] * d[j];
+        }
+        double e[3] = {1.0, 0.7, 0.4};
+        for (int it = 0; it < 50; it++) {
+            double f[3] = {0, 0, 0};
+            for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) f[i] += C[i][j] * e[j];
+            const double n = std::sqrt(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+            if (!(n > 0)) break;
+            for (int i = 0; i < 3; i++) e[i] = f[i] / n;
+        }
+        std::vector<std::pair<double, int>> key;
+        for (int t : ts) key.push_back({cx[t] * e[0] + cy[t] * e[1] + cz[t] * e[2], t});
+        std::stable_sort(key.begin(), key.end(),
+                         [](const std::pair<double, int>& p, const std::pair<double, int>& q) { return p.first < q.first; });
+        for (auto& k : key) order.push_back(k.second);
+    }
+    return order;
+}
+
 constexpr int kNever = -(1 << 20);
 constexpr uint32_t kStepVertexPass = 1u << 30;  // every triangle slot of a step that begins with a vertex pass
 constexpr uint32_t kSlotPadding = 1u << 31;     // a triangle slot past the batch  // "latest pass" of a vertex no pass of the stream has loaded
 
-// Append the streams of one model.  tri_base: index of the model's first triangle in the upload.  The
-// locality order is cut into num_streams * chunks chunks and stream s concatenates chunks s, s + num_streams,
+// Append the streams of one model in the triangle order order0.  tri_base: index of the model's first triangle in the
+// upload.  The order is cut into num_streams * chunks chunks and stream s concatenates chunks s, s + num_streams,
 // ...: every wave's triangles are spread over the whole model, so the waves of a pose see similar numbers of
 // visible (fragment-producing) triangles and meet at the end-of-raster barrier at similar times.  A chunk
 // boundary only costs the reuse of one vertex pass.
-inline void build_model(const std::vector<int>& tv, const std::vector<float>& vxyz, int tri_base, int num_streams,
-                        int vring, int ref_passes, Built& out, int chunks = 4) {
+inline void build_model_order(const std::vector<int>& tv, const std::vector<float>& vxyz, const std::vector<int>& order0,
+                              int tri_base, int num_streams, int vring, int ref_passes, Built& out, int chunks) {
     const int T = (int)tv.size() / 3;
     if (T == 0) return;
     const int num_verts = (int)vxyz.size() / 3;
-    const std::vector<int> order0 = locality_order(tv, num_verts);
     const int S = std::max(1, std::min(num_streams, (T + 63) / 64));
     const int C = std::max(1, std::min(S * std::max(chunks, 1), (T + 255) / 256));  // chunks of >= ~256 triangles
     std::vector<int> order;
@@ -213,6 +272,32 @@ inline void build_model(const std::vector<int>& tv, const std::vector<float>& vx
         sd.w = (int)(out.sverts.size() / 64);
         out.streams.push_back(sd);
     }
+}
+
+// Append the streams of one model, from the greedy growth order or the sweep order, whichever needs fewer vertex
+// passes (then fewer steps; ties: the growth order).
+inline void build_model(const std::vector<int>& tv, const std::vector<float>& vxyz, int tri_base, int num_streams,
+                        int vring, int ref_passes, Built& out, int chunks = 4) {
+    if (tv.empty()) return;
+    Built a, b;
+    build_model_order(tv, vxyz, locality_order(tv, (int)vxyz.size() / 3), tri_base, num_streams, vring, ref_passes, a,
+                      chunks);
+    build_model_order(tv, vxyz, sweep_order(tv, vxyz), tri_base, num_streams, vring, ref_passes, b, chunks);
+    const Built& w = (b.passes < a.passes || (b.passes == a.passes && b.steps < a.steps)) ? b : a;
+    const int step0 = (int)(out.stris.size() / 64), pass0 = (int)(out.sverts.size() / 64);
+    out.sverts.insert(out.sverts.end(), w.sverts.begin(), w.sverts.end());
+    out.stris.insert(out.stris.end(), w.stris.begin(), w.stris.end());
+    out.sorig.insert(out.sorig.end(), w.sorig.begin(), w.sorig.end());
+    for (I4 sd : w.streams) {
+        sd.x += step0;
+        sd.y += step0;
+        sd.z += pass0;
+        sd.w += pass0;
+        out.streams.push_back(sd);
+    }
+    out.passes += w.passes;
+    out.steps += w.steps;
+    out.filled += w.filled;
 }
 
 }  // namespace streams
