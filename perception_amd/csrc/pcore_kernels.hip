@@ -547,7 +547,12 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                     }
                     vxy[buf * kWave + lane] = make_float2(sx, sy);
                     vz[buf * kWave + lane] = lz;
-                    vbd[(buf & 1) * kWave + lane] = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H, sw.fastdiv != 0);
+                    // a wave-uniform branch, so a fastdiv pose's pass carries no NaN test, default bounds or exec
+                    // masking (the screen coordinates are finite there)
+                    uint2 vb;
+                    if (sw.fastdiv) vb = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H, true);
+                    else vb = vertex_bounds<STRIDE>(sx, sy, s, cmax0, cmax1, H, false);
+                    vbd[(buf & 1) * kWave + lane] = vb;
                 }
 #pragma unroll
                 for (int k = kVRing - kRefPasses - 1; k > 0; k--) hist[k] = hist[k - 1];
@@ -570,7 +575,12 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 // a padding slot names slot 0 three times: its bounds are read (harmless) and nk forced to 0
                 const bool pad = ct >> 31;
                 {
-                    const uint2 w0 = vbd[ct & 127u], w1 = vbd[(ct >> 9) & 127u], w2 = vbd[(ct >> 18) & 127u];
+                    // bit-field extracts as v_bfe (asm: the compiler turns them back into shift / mask / add, three
+                    // instructions per address instead of v_bfe + v_lshl_add)
+                    uint32_t i1, i2;
+                    asm("v_bfe_u32 %0, %1, 9, 7" : "=v"(i1) : "v"(ct));
+                    asm("v_bfe_u32 %0, %1, 18, 7" : "=v"(i2) : "v"(ct));
+                    const uint2 w0 = vbd[ct & 127u], w1 = vbd[i1], w2 = vbd[i2];
                     short2v lo = __builtin_elementwise_min(__builtin_elementwise_min(as_s2(w0.x), as_s2(w1.x)), as_s2(w2.x));
                     short2v hi = __builtin_elementwise_max(__builtin_elementwise_max(as_s2(w0.y), as_s2(w1.y)), as_s2(w2.y));
                     // (fastdiv poses have finite screen coordinates: no NaN vertex)
