@@ -64,6 +64,27 @@ def test_all_21_proxies_build():
     assert bank.tris.shape[0] == bank.tris_model_count.sum()
 
 
+def test_c4_scene_every_object_visible():
+    """C4's 21-object scene (workloads.object_centers, the GT rotation of workloads.build), rendered by the
+    oracle: every object keeps most of its unoccluded stride-8 samples, so every model has a findable pose."""
+    import oracle
+    from perception_amd import workloads
+
+    def rf(tris, cnt, p16, pm, W, H, proj):
+        return oracle.render_depth(tris, cnt, p16, pm, None, W, H, proj, np.zeros((H, W), np.int32), None)
+
+    names = list(syn.YCB_PROXIES)
+    rng = np.random.default_rng(syn.SEED)
+    gts = np.stack([syn.default_gt_pose(rng, c) for c in workloads.object_centers(len(names))])
+    sc = syn.make_scene(names, gts, rf, rng=rng)
+    alone = rf(sc.bank.tris, sc.bank.tris_model_count, init_from_eigen_batch(gts), np.arange(len(names), dtype=np.int32),
+               sc.width, sc.height, sc.proj)
+    for k in range(len(names)):
+        vis = int((sc.mask[::8, ::8] == k + 1).sum())
+        tot = int((alone[k][::8, ::8] > 0).sum())
+        assert vis >= 5 and vis >= 0.9 * tot, (names[k], vis, tot)
+
+
 def test_candidate_poses_include_gt_and_are_rigid():
     rng = np.random.default_rng(1)
     gt = syn.default_gt_pose(rng)
