@@ -509,17 +509,31 @@ void covariance_one(const float* xyz, int n, int i, int k, double* out6) {
 }
 
 // per-point Gauss-Newton contribution: acc[0..20] = upper(H) row-major, [21..26] = b, [27] = error
+// Correspondence: the first strict minimum of the key of pcore_gicp_math.h over the segment (keys / org non-null:
+// segments of <= kKeyScanMax targets), else of the float squared distance (larger segments; the GPU's exact
+// grid search reproduces it).
 bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const double* cs, const float* tgt,
-                  const double* tcov, int nt, double acc[pcore::gicpm::kTerms]) {
+                  const double* tcov, int nt, const pcore::gicpm::NNTarget* keys, const float* org,
+                  double acc[pcore::gicpm::kTerms]) {
     const double s0 = (double)s[0], s1 = (double)s[1], s2 = (double)s[2];
     double q[3];
     for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
     const float qf[3] = {(float)q[0], (float)q[1], (float)q[2]};
     int j = -1;
     float best = INFINITY;
-    for (int o = 0; o < nt; o++) {
-        const float d = sqdist(qf, tgt + (size_t)3 * o);
-        if (d < best) { best = d; j = o; }
+    if (keys) {
+        const float qx = qf[0] - org[0], qy = qf[1] - org[1], qz = qf[2] - org[2];
+        if (std::isfinite(qx) && std::isfinite(qy) && std::isfinite(qz))
+            for (int o = 0; o < nt; o++) {
+                const pcore::gicpm::NNTarget& k = keys[o];
+                const float d = pcore::gicpm::nn_key(k.m2x, k.m2y, k.m2z, k.tt, qx, qy, qz);
+                if (d < best) { best = d; j = o; }
+            }
+    } else {
+        for (int o = 0; o < nt; o++) {
+            const float d = sqdist(qf, tgt + (size_t)3 * o);
+            if (d < best) { best = d; j = o; }
+        }
     }
     if (j < 0) return false;
     const double* ctp = tcov + (size_t)6 * j;
@@ -586,10 +600,22 @@ int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* t
     int it = 0;
     if (ns > 0 && nt > 0) {
         std::vector<double> part((size_t)kGicpThreads * pcore::gicpm::kTerms);
+        std::vector<pcore::gicpm::NNTarget> keys;
+        float org[3] = {0.0f, 0.0f, 0.0f};
+        if (nt <= pcore::gicpm::kKeyScanMax) {
+            pcore::gicpm::nn_origin(nt, [&](int i, float* p) {
+                for (int a = 0; a < 3; a++) p[a] = tgt_xyz[(size_t)3 * i + a];
+            }, org);
+            keys.resize(nt);
+            for (int i = 0; i < nt; i++)
+                keys[i] = pcore::gicpm::nn_target(tgt_xyz[3 * (size_t)i], tgt_xyz[3 * (size_t)i + 1],
+                                                  tgt_xyz[3 * (size_t)i + 2], org[0], org[1], org[2]);
+        }
         for (it = 0; it < max_iter;) {
             std::fill(part.begin(), part.end(), 0.0);
             for (int i = 0; i < ns; i++)
                 gicp_contrib(R, t, src_xyz + (size_t)3 * i, src_cov + (size_t)6 * i, tgt_xyz, tgt_cov, nt,
+                             keys.empty() ? nullptr : keys.data(), org,
                              part.data() + (size_t)pcore::gicpm::kTerms * (i % kGicpThreads));
             // fixed reduction: per wave shuffle-down tree to lane 0, then the 4 waves in order
             double tot[pcore::gicpm::kTerms];

@@ -5,6 +5,7 @@
 #include "../../include/pcore.h"
 #include "pcore_internal.h"
 #include "pcore_streams.h"
+#include "pcore_gicp_math.h"
 
 #include <algorithm>
 #include <climits>
@@ -581,24 +582,33 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
         HIPC(c, dev_upload(c->seg_cnt, scnt));
         c->seg_lo_h = slo;
         c->seg_cnt_h = scnt;
-        // quad-SoA copy of every segment (labels, then the whole cloud) for the scalar-cache scan
+        // quad-SoA copy of every segment (labels, then the whole cloud) for the scalar-cache scan: a header quad
+        // (the segment's key origin c in [0..2]), then quads of four targets as correspondence keys
+        // (-2 t'x [4], -2 t'y [4], -2 t'z [4], |t'|^2 [4]; padding: 0, 0, 0, +inf), pcore_gicp_math.h
         std::vector<int32_t> qoff(num_labels + 1);
         std::vector<float> quads;
         for (int L = 0; L <= num_labels; L++) {
             qoff[L] = (int32_t)(quads.size() / 16);
             const int n = scnt[L], nq = (n + 3) / 4;
+            float org[3];
+            gicpm::nn_origin(n, [&](int i, float* p) {
+                const float4 v = tp[slo[L] + i];
+                p[0] = v.x; p[1] = v.y; p[2] = v.z;
+            }, org);
             const size_t q0 = quads.size();
-            quads.resize(q0 + (size_t)16 * nq, INFINITY);
+            quads.resize(q0 + (size_t)16 * (nq + 1), 0.0f);
+            quads[q0] = org[0]; quads[q0 + 1] = org[1]; quads[q0 + 2] = org[2];
+            for (int i = n; i < 4 * nq; i++) quads[q0 + 16 + (size_t)16 * (i / 4) + 12 + i % 4] = INFINITY;
             for (int i = 0; i < n; i++) {
                 const float4 p = tp[slo[L] + i];
-                const bool fin = std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z);
-                float* Q = &quads[q0 + (size_t)16 * (i / 4)];
-                Q[i % 4] = fin ? p.x : INFINITY;
-                Q[4 + i % 4] = fin ? p.y : INFINITY;
-                Q[8 + i % 4] = fin ? p.z : INFINITY;
+                const gicpm::NNTarget t = gicpm::nn_target(p.x, p.y, p.z, org[0], org[1], org[2]);
+                float* Q = &quads[q0 + 16 + (size_t)16 * (i / 4)];
+                Q[i % 4] = t.m2x;
+                Q[4 + i % 4] = t.m2y;
+                Q[8 + i % 4] = t.m2z;
+                Q[12 + i % 4] = t.tt;
             }
         }
-        if (quads.empty()) quads.assign(16, INFINITY);
         HIPC(c, dev_upload(c->tgt_quads, quads));
         HIPC(c, dev_upload(c->seg_qoff, qoff));
         c->num_obs = num_obs;

@@ -403,33 +403,39 @@ __device__ __forceinline__ void grid_nn(const LabelGrid& G, const int32_t* cell_
     }
 }
 
-// Nearest of a segment's targets read through the scalar cache: the segment is stored as quads of
-// 16 floats (x0..x3, y0..y3, z0..z3, 4 pad; non-finite and padding targets +inf), every lane scans the
-// same quads, so the loads are wave-uniform s_loads and the targets reach the VALU as SGPR operands --
-// no LDS traffic (an LDS broadcast read still moves 64 lanes x 16 B through the LDS pipe).  Packed f32
-// arithmetic with the same IEEE operations, per element, as sqdist3.  The index work stays out of the
-// per-quad loop: alternate quads feed two chains that keep only their smallest quad minimum and the first
-// quad reaching it (strict <); the chains merge by (distance, quad), and the winning quad's element is found
-// once at the end by recomputing its four distances (the same operations, so one of them equals the minimum
-// bit for bit) and taking the first equal one -- the lexicographic minimum of (distance, index), i.e. the
-// oracle's first strict minimum.  (A per-quad tournament carrying the index cost 29 instead of 23 VALU per quad:
-// C3 GICP 21.9 -> 21.2 ms.)  NaN distances need a non-finite query, and then no distance is finite, so minNum's
-// NaN handling never decides a comparison against a finite value.
+// Nearest of a segment's targets read through the scalar cache: every lane scans the same quads of four targets
+// stored as correspondence keys (pcore_gicp_math.h: -2 t'x [4], -2 t'y [4], -2 t'z [4], |t'|^2 [4] about the
+// segment's origin, which the header quad before them holds), so the loads are wave-uniform s_loads and the
+// targets reach the VALU as SGPR operands -- no LDS traffic (an LDS broadcast read still moves 64 lanes x 16 B
+// through the LDS pipe).  A pair of targets costs three packed FMAs.  The index work stays out of the per-quad
+// loop: alternate quads feed two chains that keep only their smallest quad minimum and the first quad reaching it
+// (strict <); the chains merge by (key, quad), and the winning quad's element is found once at the end by
+// recomputing its four keys (the same FMAs, so one of them equals the minimum bit for bit) and taking the first
+// equal one -- the lexicographic minimum of (key, index), i.e. the oracle's first strict minimum.  Measured on
+// C3's GICP call: a per-quad (distance, index) tournament over x / y / z quads 21.9 ms, the index-free scan of
+// float squared distances 21.2 ms.  Keys of finite targets and a finite query are finite, so minNum's NaN
+// handling never decides a comparison.
 typedef __attribute__((address_space(4))) const f4v cf4v;
 
-__device__ __forceinline__ void scan_quads(const float* tq_generic, int nq, float qx, float qy, float qz, float& best,
+__device__ __forceinline__ void scan_quads(const float* seg_quads, int nq, float qx, float qy, float qz, float& best,
                                            int& j) {
-    const cf4v* tq = (const cf4v*)tq_generic;
+    const cf4v* hq = (const cf4v*)seg_quads;
+    const f4v org = hq[0];
+    qx = qx - org.x;
+    qy = qy - org.y;
+    qz = qz - org.z;
+    if (!(__builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz))) return;  // no correspondence
+    const cf4v* tq = hq + 4;
     const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
     float bA = INFINITY, bB = INFINITY;
     int oA = -1, oB = -1;
     auto qmin = [&](const cf4v* q) {
-        const f4v X = q[0], Y = q[1], Z = q[2];
-        const f2v dxa = qx2 - X.xy, dya = qy2 - Y.xy, dza = qz2 - Z.xy;
-        const f2v dxb = qx2 - X.zw, dyb = qy2 - Y.zw, dzb = qz2 - Z.zw;
-        const f2v da = dxa * dxa + dya * dya + dza * dza;
-        const f2v db = dxb * dxb + dyb * dyb + dzb * dzb;
-        return fminf(fminf(fminf(da.x, da.y), db.x), db.y);
+        const f4v X = q[0], Y = q[1], Z = q[2], T = q[3];
+        const f2v ka = __builtin_elementwise_fma(X.xy, qx2, __builtin_elementwise_fma(Y.xy, qy2,
+                                                  __builtin_elementwise_fma(Z.xy, qz2, T.xy)));
+        const f2v kb = __builtin_elementwise_fma(X.zw, qx2, __builtin_elementwise_fma(Y.zw, qy2,
+                                                  __builtin_elementwise_fma(Z.zw, qz2, T.zw)));
+        return fminf(fminf(fminf(ka.x, ka.y), kb.x), kb.y);
     };
     int o = 0;
     const cf4v* q = tq;  // wave-uniform: the quads' addresses stay scalar
@@ -447,12 +453,12 @@ __device__ __forceinline__ void scan_quads(const float* tq_generic, int nq, floa
     if (bB < bA || (bB == bA && oB >= 0 && oB < oA)) { bA = bB; oA = oB; }
     if (bA < best) {
         // the winning quad, per lane (a vector load), its first element at the minimum
-        const float* Q = tq_generic + 16 * oA;
+        const float* Q = seg_quads + 16 + 16 * oA;
         const float4 X = *reinterpret_cast<const float4*>(Q), Y = *reinterpret_cast<const float4*>(Q + 4);
-        const float4 Z = *reinterpret_cast<const float4*>(Q + 8);
-        const int k = sqdist3(qx, qy, qz, X.x, Y.x, Z.x) == bA ? 0
-                    : sqdist3(qx, qy, qz, X.y, Y.y, Z.y) == bA ? 1
-                    : sqdist3(qx, qy, qz, X.z, Y.z, Z.z) == bA ? 2 : 3;
+        const float4 Z = *reinterpret_cast<const float4*>(Q + 8), T = *reinterpret_cast<const float4*>(Q + 12);
+        const int k = gicpm::nn_key(X.x, Y.x, Z.x, T.x, qx, qy, qz) == bA ? 0
+                    : gicpm::nn_key(X.y, Y.y, Z.y, T.y, qx, qy, qz) == bA ? 1
+                    : gicpm::nn_key(X.z, Y.z, Z.z, T.z, qx, qy, qz) == bA ? 2 : 3;
         best = bA;
         j = 4 * oA + k;
     }

@@ -22,6 +22,50 @@
 namespace pcore {
 namespace gicpm {
 
+// Correspondence key (segments of at most kKeyScanMax targets; larger ones use the plain float squared distance
+// and the exact grid search).  With the segment's origin c (float midpoint of its finite targets' bounding box),
+// q' = q - c and t' = t - c, a target is stored as (-2 t'x, -2 t'y, -2 t'z, |t'|^2) and scored by
+//   key = fma(-2 t'x, q'x, fma(-2 t'y, q'y, fma(-2 t'z, q'z, |t'|^2)))  =  |q' - t'|^2 - |q'|^2  (+ rounding),
+// three FMAs instead of three subtractions, three products and two sums; |q'|^2 is the same for every target,
+// so the nearest target is the first strict minimum of the key.  Centring keeps |q'|^2 small (objects are
+// ~0.1 m across), so the cancellation costs ~1e-9 m^2.  Non-finite targets never win (key +inf); a non-finite
+// query has no correspondence.
+constexpr int kKeyScanMax = 2048;
+
+struct NNTarget {
+    float m2x, m2y, m2z, tt;
+};
+
+PCORE_GHD NNTarget nn_target(float x, float y, float z, float cx, float cy, float cz) {
+    if (!(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z))) return {0.0f, 0.0f, 0.0f, __builtin_inff()};
+    const float dx = x - cx, dy = y - cy, dz = z - cz;
+    return {-2.0f * dx, -2.0f * dy, -2.0f * dz, __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz))};
+}
+
+PCORE_GHD float nn_key(float m2x, float m2y, float m2z, float tt, float qx, float qy, float qz) {
+    return __builtin_fmaf(m2x, qx, __builtin_fmaf(m2y, qy, __builtin_fmaf(m2z, qz, tt)));
+}
+
+// the origin c of a segment: float midpoint of the bounding box of its finite targets (0 when there are none);
+// get(i, p) fills p[3] with target i
+template <class Get>
+inline void nn_origin(int n, Get get, float (&c)[3]) {
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    bool any = false;
+    for (int i = 0; i < n; i++) {
+        float p[3];
+        get(i, p);
+        if (!(__builtin_isfinite(p[0]) && __builtin_isfinite(p[1]) && __builtin_isfinite(p[2]))) continue;
+        any = true;
+        for (int a = 0; a < 3; a++) {
+            lo[a] = p[a] < lo[a] ? p[a] : lo[a];
+            hi[a] = p[a] > hi[a] ? p[a] : hi[a];
+        }
+    }
+    for (int a = 0; a < 3; a++) c[a] = any ? (lo[a] + hi[a]) * 0.5f : 0.0f;
+}
+
 // J^T v (the 6-vector above)
 PCORE_GHD void jt_mul(const double (&q)[3], const double (&v)[3], double (&o)[6]) {
     o[0] = q[2] * v[1] - q[1] * v[2];

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pcore_gicp_math.h"
+
 namespace pcore {
 
 // Vertex-ring streams ("Vertex-ring streams").  A model's triangles are cut into streams, one
@@ -153,8 +155,9 @@ struct GicpArgs {
     const LabelGrid* grids;
     const int32_t* cell_start;
     const float4* grid_pts;
-    // the segments as quads of 16 floats (x0..3, y0..3, z0..3, pad; non-finite / padding = +inf), quad
-    // offset of segment s = seg_qoff[s]: the scalar-cache nearest-target scan
+    // the segments as quads of 16 floats for the scalar-cache nearest-target scan, from quad seg_qoff[s]: a header
+    // quad (the key origin in [0..2]), then four targets per quad as correspondence keys (-2 t'x [4], -2 t'y [4],
+    // -2 t'z [4], |t'|^2 [4]; padding 0, 0, 0, +inf; pcore_gicp_math.h)
     const float* tgt_quads;
     const int32_t* seg_qoff;
 };
@@ -162,6 +165,7 @@ struct GicpArgs {
 // segments above this many points use the exact shell search of their neighbour grid (GICP
 // correspondences and target covariances); smaller ones the brute-force scans
 constexpr int kGridNNMin = 2048;
+static_assert(kGridNNMin == gicpm::kKeyScanMax, "the key scan covers exactly the segments without the grid search");
 
 // gfx950 allocates a workgroup's LDS in 1,280-byte granules (160 KiB = 128 of them), not the 512 bytes of
 // earlier CDNA parts: a census of resident fused_cost_kernel workgroups (tools/wg_timeline.py,
