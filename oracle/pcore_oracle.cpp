@@ -555,16 +555,17 @@ bool ldlt_solve6(const double Hu[21], const double b[6], double d[6]) {
     int h = 0;
     for (int a = 0; a < 6; a++)
         for (int c = a; c < 6; c++) { H[a][c] = Hu[h]; H[c][a] = Hu[h]; h++; }
-    double L[6][6] = {}, D[6];
+    double L[6][6] = {}, D[6], iD[6];
     for (int j = 0; j < 6; j++) {
         double v = H[j][j];
         for (int k = 0; k < j; k++) v = v - L[j][k] * L[j][k] * D[k];
         if (!(v > 0.0) || !std::isfinite(v)) return false;
         D[j] = v;
+        iD[j] = 1.0 / v;  // one division per column; the column and the back substitution multiply by it
         for (int i = j + 1; i < 6; i++) {
             double w = H[i][j];
             for (int k = 0; k < j; k++) w = w - L[i][k] * L[j][k] * D[k];
-            L[i][j] = w / D[j];
+            L[i][j] = w * iD[j];
         }
     }
     double y[6];
@@ -574,7 +575,7 @@ bool ldlt_solve6(const double Hu[21], const double b[6], double d[6]) {
         y[i] = v;
     }
     for (int i = 5; i >= 0; i--) {
-        double v = y[i] / D[i];
+        double v = y[i] * iD[i];
         for (int k = i + 1; k < 6; k++) v = v - L[k][i] * d[k];
         d[i] = v;
     }

@@ -492,7 +492,7 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
     int h = 0;
     for (int a = 0; a < 6; a++)
         for (int c = a; c < 6; c++) { H[a][c] = Hu[h]; H[c][a] = Hu[h]; h++; }
-    double L[6][6], D[6];
+    double L[6][6], D[6], iD[6];
     for (int a = 0; a < 6; a++)
         for (int c = 0; c < 6; c++) L[a][c] = 0.0;
     for (int j = 0; j < 6; j++) {
@@ -500,10 +500,11 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
         for (int k = 0; k < j; k++) v = v - L[j][k] * L[j][k] * D[k];
         if (!(v > 0.0) || !isfinite(v)) return false;
         D[j] = v;
+        iD[j] = 1.0 / v;  // one division per column; the column and the back substitution multiply by it
         for (int i = j + 1; i < 6; i++) {
             double w = H[i][j];
             for (int k = 0; k < j; k++) w = w - L[i][k] * L[j][k] * D[k];
-            L[i][j] = w / D[j];
+            L[i][j] = w * iD[j];
         }
     }
     double y[6];
@@ -513,7 +514,7 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
         y[i] = v;
     }
     for (int i = 5; i >= 0; i--) {
-        double v = y[i] / D[i];
+        double v = y[i] * iD[i];
         for (int k = i + 1; k < 6; k++) v = v - L[k][i] * d[k];
         d[i] = v;
     }
