@@ -184,3 +184,36 @@ def test_knn_ties_pick_lowest_index():
     d2, idx = oracle.knn1(np.zeros((1, 3), np.float32), np.array([5], np.int32), o,
                           np.array([0], np.int32), np.array([3], np.int32))
     assert idx[0] == -1 and np.isinf(d2[0])
+
+
+def _box_cloud(n=300, seed=0):
+    from perception_amd import synthetic as syn
+    rng = np.random.default_rng(seed)
+    m = syn.ycb_proxy("003_cracker_box", 8)
+    pts = np.unique(m.tris.reshape(-1, 3), axis=0).astype(np.float32) + np.float32([0.05, -0.02, 0.8])
+    return pts[rng.choice(len(pts), n, replace=False)]
+
+
+@pytest.mark.parametrize("offset", [(0.01, -0.005, 0.008), (-0.004, 0.012, -0.006)])
+def test_gicp_recovers_a_translation(offset):
+    """GICP spec (correspondences by the three-FMA key): a cloud shifted by a centimetre-scale
+    offset is registered back onto itself -- T's translation is minus the offset, its rotation the identity."""
+    tgt = _box_cloud()
+    src = tgt + np.float32(offset)
+    T, it = oracle.gicp(src, oracle.covariances(src), tgt, oracle.covariances(tgt))
+    assert 1 <= it < 150
+    assert np.allclose(T[:3, 3], -np.asarray(offset), atol=1e-5)
+    assert np.abs(T[:3, :3] - np.eye(3)).max() < 1e-5
+
+
+def test_gicp_recovers_a_small_rigid_motion():
+    """A 3-degree rotation about the cloud's centre plus a 5 mm shift is undone to within 1e-4."""
+    tgt = _box_cloud(seed=1)
+    c = tgt.mean(0)
+    a = np.deg2rad(3.0)
+    Rz = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+    src = ((tgt - c) @ Rz.T + c + np.array([0.005, 0.0, -0.003])).astype(np.float32)
+    T, it = oracle.gicp(src, oracle.covariances(src), tgt, oracle.covariances(tgt))
+    back = src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]
+    assert it < 150
+    assert np.abs(back - tgt).max() < 1e-4
