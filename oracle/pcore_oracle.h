@@ -93,10 +93,12 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
  *  - covariance: k nearest points of the same cloud (float squared distance, ties -> lower index,
  *    list ordered by (distance, index)), double mean / covariance over k_eff = min(k, n), PLANE
  *    regularisation C = U diag(1, 1, 1e-3) U^T from 6 cyclic Jacobi sweeps (double, sqrt/div only);
- *  - Gauss-Newton on SE(3): correspondences = float 1-NN of (float)(R s + t) in the target segment,
+ *  - Gauss-Newton on SE(3): correspondence of q = (float)(R s + t) = the first strict minimum over the
+ *    target segment of the three-FMA key of pcore_gicp_math.h (|q'-t'|^2 - |q'|^2 about the segment's
+ *    origin; segments of <= 2048 targets) or of the float squared distance (larger segments),
  *    Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I], H / b reduced in the GPU's fixed order
  *    (64 per-lane sequential partials, then the wave shuffle-down tree), 6x6 LDLT
- *    without pivoting, left update T <- [R(q(w)) | rho] T with q = normalise(1, w/2), stop when
+ *    without pivoting (one reciprocal per column), left update T <- [R(q(w)) | rho] T with q = normalise(1, w/2), stop when
  *    max|dR - I| < rot_eps and max|dt| < trans_eps or after max_iter iterations.
  * Covariances: double[6] (xx, xy, xz, yy, yz, zz) per point. */
 void orc_covariances(const float* xyz, int n, int k, double* out_cov6);
