@@ -657,7 +657,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
 #pragma unroll
                 for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
                 const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
-                // nearest target: first strict minimum of the float squared distance (orc gicp_nn)
+                // correspondence: first strict minimum of the key (segments <= kKeyScanMax) or of the float squared
+                // distance (grid search of larger segments), as orc gicp_contrib
                 int j = -1;
                 float best = INFINITY;
                 if (use_grid) {
