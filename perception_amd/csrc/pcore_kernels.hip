@@ -841,8 +841,8 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
                         const int iz0 = (int)floorf(fmaxf(lz, 0.0f)), iz1 = min(g.nz - 1, (int)floorf(hz));
                         // the radius box spans <= 2 cells per axis (cell >= 2.02 r): the <= 2 cells along x of one
                         // (y, z) row are adjacent in the CSR order, so their points form ONE range -- <= 4 ranges,
-                        // fetched with independent loads, then each range's points four at a time (clamped loads
-                        // issued together); the (distance, index) minimum does not depend on the order
+                        // fetched with independent loads, then their points as one flattened sequence four at a time
+                        // (clamped loads issued together); the (distance, index) minimum does not depend on the order
                         int cb[4], ce[4];
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
@@ -852,21 +852,27 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
                             cb[q] = ok ? a.cell_start[c] : 0;
                             ce[q] = ok ? a.cell_start[c + 1 + (ix1 - ix0)] : 0;
                         }
+                        // the <= 4 ranges as one flattened candidate sequence, four at a time: the wave loops over its
+                        // lanes' largest total instead of the sum of the per-range maxima
+                        const int l0 = ce[0] - cb[0], l1 = l0 + (ce[1] - cb[1]), l2 = l1 + (ce[2] - cb[2]);
+                        const int ltot = l2 + (ce[3] - cb[3]);
+                        for (int k0 = 0; k0 < ltot; k0 += 4) {
+                            float4 o[4];
 #pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            for (int pi = cb[q]; pi < ce[q]; pi += 4) {
-                                float4 o[4];
+                            for (int u = 0; u < 4; u++) {
+                                const int k = min(k0 + u, ltot - 1);
+                                const int pi = k < l0 ? cb[0] + k : k < l1 ? cb[1] + (k - l0)
+                                             : k < l2 ? cb[2] + (k - l1) : cb[3] + (k - l2);
+                                o[u] = a.grid_pts[pi];
+                            }
 #pragma unroll
-                                for (int u = 0; u < 4; u++) o[u] = a.grid_pts[min(pi + u, ce[q] - 1)];
-#pragma unroll
-                                for (int u = 0; u < 4; u++) {
-                                    const float dx = xp - o[u].x, dy = yp - o[u].y, dz = zp - o[u].z;
-                                    const float d = dx * dx + dy * dy + dz * dz;
-                                    const int oi = __float_as_int(o[u].w);
-                                    const bool take = pi + u < ce[q] && (d < best || (d == best && oi < bidx));
-                                    best = take ? d : best;
-                                    bidx = take ? oi : bidx;
-                                }
+                            for (int u = 0; u < 4; u++) {
+                                const float dx = xp - o[u].x, dy = yp - o[u].y, dz = zp - o[u].z;
+                                const float d = dx * dx + dy * dy + dz * dz;
+                                const int oi = __float_as_int(o[u].w);
+                                const bool take = k0 + u < ltot && (d < best || (d == best && oi < bidx));
+                                best = take ? d : best;
+                                bidx = take ? oi : bidx;
                             }
                         }
                     }
