@@ -523,6 +523,34 @@ __device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
     return true;
 }
 
+// The same shuffle-down tree through LDS, a transposed layout instead of 6 x 27 ds_bpermute rounds: every lane
+// stores its partial sums (14 values, then the other 13), lane k adds up value k's 64 entries in the tree's own
+// order -- node(l, off) = node(l, 2 off) + node(l + off, 2 off), leaves node(l, 64) = lane l's entry, so lane 0's
+// level-by-level sums ((x0 + x32) + (x16 + x48)) + ... come out bit-identical -- and the 27 sums return through LDS
+// to every lane.  One wave per workgroup (gicp_kernel<1>): ~7 KB of LDS.
+constexpr int kRedHalf = 14;
+template <int L, int OFF, int NV>
+__device__ __forceinline__ double tree_node(const double* col) {
+    if constexpr (OFF == 64) return col[L * NV];
+    else return tree_node<L, 2 * OFF, NV>(col) + tree_node<L + OFF, 2 * OFF, NV>(col);
+}
+__device__ __forceinline__ void lds_tree_sum(double (&acc)[gicpm::kTerms], double* red, int lane) {
+    constexpr int NA = kRedHalf, NB = gicpm::kTerms - kRedHalf;
+    double* out = red + kRedHalf * 64;
+#pragma unroll
+    for (int v = 0; v < NA; v++) red[lane * NA + v] = acc[v];
+    wave_lds_sync();
+    if (lane < NA) out[lane] = tree_node<0, 1, NA>(red + lane);
+    wave_lds_sync();
+#pragma unroll
+    for (int v = 0; v < NB; v++) red[lane * NB + v] = acc[NA + v];
+    wave_lds_sync();
+    if (lane < NB) out[NA + lane] = tree_node<0, 1, NB>(red + lane);
+    wave_lds_sync();
+#pragma unroll
+    for (int v = 0; v < gicpm::kTerms; v++) acc[v] = out[v];
+}
+
 // Lane-0 step of an iteration: LDLT of the reduced normal equations, the left update of (R, t) into RT and
 // fast_gicp's convergence test.  Returns 0 continue, 1 stop without update (H not positive definite),
 // 2 stop after the update.
@@ -591,6 +619,9 @@ __device__ __forceinline__ void group_sync() {
 #ifndef PCORE_GICP_WPP
 #define PCORE_GICP_WPP 1
 #endif
+#ifndef PCORE_GICP_LDS_RED
+#define PCORE_GICP_LDS_RED 1
+#endif
 constexpr int kGicpWpp = PCORE_GICP_WPP;  // must match kGicpThreads / 64 of orc_gicp
 
 template <int WPP>
@@ -600,6 +631,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ double RT[12];
     __shared__ double sPart[WPP][gicpm::kTerms];
     __shared__ int sPose, sFlag;
+#if PCORE_GICP_LDS_RED
+    __shared__ double sRed[kRedHalf * 64 + gicpm::kTerms];
+#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     GPROF_DECL;
     for (;;) {
@@ -678,12 +712,19 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 GPROF_ADD(1, t_r1, t_r2);
             }
             GPROF_TD(t_b, acc[gicpm::kTerms - 1]);
+#if PCORE_GICP_LDS_RED
+            if constexpr (WPP == 1) {
+                lds_tree_sum(acc, sRed, lane);
+            } else
+#endif
+            {
 #pragma unroll
             for (int v = 0; v < gicpm::kTerms; v++) {
                 double x = acc[v];
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
                 acc[v] = x;
+            }
             }
             if constexpr (WPP > 1) {
                 if (lane == 0) {
