@@ -416,6 +416,9 @@ __device__ __forceinline__ void grid_nn(const LabelGrid& G, const int32_t* cell_
 // float squared distances 21.2 ms.  Keys of finite targets and a finite query are finite, so minNum's NaN
 // handling never decides a comparison.
 typedef __attribute__((address_space(4))) const f4v cf4v;
+#ifndef PCORE_SCAN_UNROLL
+#define PCORE_SCAN_UNROLL 4  // quad pairs per loop trip (C3: 2 -> 4: 20.60 -> 20.45 ms per step; 1: 21.25)
+#endif
 
 __device__ __forceinline__ void scan_quads(const float* seg_quads, int nq, float qx, float qy, float qz, float& best,
                                            int& j) {
@@ -439,7 +442,7 @@ __device__ __forceinline__ void scan_quads(const float* seg_quads, int nq, float
     };
     int o = 0;
     const cf4v* q = tq;  // wave-uniform: the quads' addresses stay scalar
-#pragma unroll 2
+#pragma unroll PCORE_SCAN_UNROLL
     for (; o + 2 <= nq; o += 2, q += 8) {
         const float ma = qmin(q);
         if (ma < bA) { bA = ma; oA = o; }
