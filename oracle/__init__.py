@@ -200,14 +200,22 @@ def _gicp_lib():
                                        c_float, _f32p, _f64p, c_int, _opt(_i32p), _opt(_i32p), c_int, _opt(_f32p),
                                        c_int, c_int, c_float, c_int, c_int, c_double, c_double, _f32p, _opt(_i32p),
                                        _f32p, _f32p, _f32p, c_int]
+        L.orc_gicp_linearize.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, _f64p, c_int, _i32p, _f64p]
+        L.orc_gicp_se3_exp.argtypes = [_f64p, _f64p]
+        L.orc_gicp_lm_solve.argtypes = [_f64p, c_double, _f64p]
+        L.orc_sin_d.restype = c_double
+        L.orc_sin_d.argtypes = [c_double]
+        L.orc_cos_d.restype = c_double
+        L.orc_cos_d.argtypes = [c_double]
+        L.orc_gicp_nn.argtypes = [_f32p, c_int, _f32p, c_int, _i32p]
         L._gicp_typed = True
     return L
 
 
 GICP_K = 10            # renderer.cu:1697 k_correspondences_
 GICP_MAX_ITER = 150    # renderer.cu:1696
-GICP_ROT_EPS = 2e-3    # renderer.cu:1698
-GICP_TRANS_EPS = 5e-4  # renderer.cu:1699
+GICP_ROT_EPS = float(np.float32(2e-3))    # renderer.cu:1698 (a float widened to double)
+GICP_TRANS_EPS = float(np.float32(5e-4))  # renderer.cu:1699 (a float widened to double)
 
 
 def covariances(xyz, k=GICP_K):
@@ -228,6 +236,53 @@ def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EP
                               _c(tgt_cov, np.float64).reshape(-1) if len(tgt) else z6, len(tgt), max_iter, rot_eps,
                               trans_eps, T)
     return T.reshape(4, 4), it
+
+
+def gicp_linearize(src, src_cov, tgt, tgt_cov, T, textbook=False):
+    """The GICP linearisation at T: (corr (ns,), H (6,6), b (6,), error) -- the spec's arithmetic (textbook=False)
+    or the independent long-double 4x4 restatement (textbook=True), both on the spec's correspondences."""
+    src = _c(src, np.float32).reshape(-1, 3)
+    tgt = _c(tgt, np.float32).reshape(-1, 3)
+    corr = np.zeros(max(len(src), 1), np.int32)
+    sys = np.zeros(28, np.float64)
+    _gicp_lib().orc_gicp_linearize(src.reshape(-1), _c(src_cov, np.float64).reshape(-1), len(src), tgt.reshape(-1),
+                                   _c(tgt_cov, np.float64).reshape(-1), len(tgt), _c(T, np.float64).reshape(-1),
+                                   int(bool(textbook)), corr, sys)
+    H = np.zeros((6, 6))
+    iu = np.triu_indices(6)
+    H[iu] = sys[:21]
+    H = H + np.triu(H, 1).T
+    return corr[:len(src)], H, sys[21:27].copy(), float(sys[27])
+
+
+def gicp_se3_exp(a):
+    out = np.zeros(16, np.float64)
+    _gicp_lib().orc_gicp_se3_exp(_c(a, np.float64).reshape(-1), out)
+    return out.reshape(4, 4)
+
+
+def gicp_lm_solve(H, b, lam):
+    iu = np.triu_indices(6)
+    sys = np.concatenate([np.asarray(H, np.float64)[iu], np.asarray(b, np.float64), [0.0]])
+    d = np.zeros(6, np.float64)
+    _gicp_lib().orc_gicp_lm_solve(sys, float(lam), d)
+    return d
+
+
+def sin_d(x):
+    return _gicp_lib().orc_sin_d(float(x))
+
+
+def cos_d(x):
+    return _gicp_lib().orc_cos_d(float(x))
+
+
+def gicp_nn(q, tgt):
+    q = _c(q, np.float32).reshape(-1, 3)
+    tgt = _c(tgt, np.float32).reshape(-1, 3)
+    out = np.zeros(max(len(q), 1), np.int32)
+    _gicp_lib().orc_gicp_nn(q.reshape(-1), len(q), tgt.reshape(-1), len(tgt), out)
+    return out[:len(q)]
 
 
 def concat_pose(T, pose):

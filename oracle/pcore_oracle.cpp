@@ -508,17 +508,10 @@ void covariance_one(const float* xyz, int n, int i, int k, double* out6) {
     plane_regularize(c, out6);
 }
 
-// per-point Gauss-Newton contribution: acc[0..20] = upper(H) row-major, [21..26] = b, [27] = error
-// Correspondence: the first strict minimum of the key of pcore_gicp_math.h over the segment (keys / org non-null:
-// segments of <= kKeyScanMax targets), else of the float squared distance (larger segments; the GPU's exact
-// grid search reproduces it).
-bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const double* cs, const float* tgt,
-                  const double* tcov, int nt, const pcore::gicpm::NNTarget* keys, const float* org,
-                  double acc[pcore::gicpm::kTerms]) {
-    const double s0 = (double)s[0], s1 = (double)s[1], s2 = (double)s[2];
-    double q[3];
-    for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
-    const float qf[3] = {(float)q[0], (float)q[1], (float)q[2]};
+// Correspondence of the float query qf (fast_gicp update_correspondences): the first strict minimum of the key of
+// pcore_gicp_math.h over the segment (keys / org non-null: segments of <= kKeyScanMax targets), else of the float
+// squared distance (larger segments; the GPU's exact grid search reproduces it).  -1: no correspondence.
+int gicp_nn(const float qf[3], const float* tgt, int nt, const pcore::gicpm::NNTarget* keys, const float* org) {
     int j = -1;
     float best = INFINITY;
     if (keys) {
@@ -535,53 +528,209 @@ bool gicp_contrib(const double R[3][3], const double t[3], const float* s, const
             if (d < best) { best = d; j = o; }
         }
     }
-    if (j < 0) return false;
-    const double* ctp = tcov + (size_t)6 * j;
-    const double ct[6] = {ctp[0], ctp[1], ctp[2], ctp[3], ctp[4], ctp[5]};
-    const double csa[6] = {cs[0], cs[1], cs[2], cs[3], cs[4], cs[5]};
-    const double Rm[3][3] = {{R[0][0], R[0][1], R[0][2]}, {R[1][0], R[1][1], R[1][2]}, {R[2][0], R[2][1], R[2][2]}};
-    const double qa[3] = {q[0], q[1], q[2]};
-    const double tj[3] = {(double)tgt[3 * (size_t)j + 0], (double)tgt[3 * (size_t)j + 1], (double)tgt[3 * (size_t)j + 2]};
-    double a27[pcore::gicpm::kTerms];
-    for (int v = 0; v < pcore::gicpm::kTerms; v++) a27[v] = acc[v];
-    pcore::gicpm::contrib(Rm, qa, csa, tj, ct, a27);
-    for (int v = 0; v < pcore::gicpm::kTerms; v++) acc[v] = a27[v];
-    return true;
+    return j;
 }
 
-// 6x6 LDLT without pivoting; returns false if not positive definite.
-bool ldlt_solve6(const double Hu[21], const double b[6], double d[6]) {
-    double H[6][6];
-    int h = 0;
-    for (int a = 0; a < 6; a++)
-        for (int c = a; c < 6; c++) { H[a][c] = Hu[h]; H[c][a] = Hu[h]; h++; }
-    double L[6][6] = {}, D[6], iD[6];
-    for (int j = 0; j < 6; j++) {
-        double v = H[j][j];
-        for (int k = 0; k < j; k++) v = v - L[j][k] * L[j][k] * D[k];
-        if (!(v > 0.0) || !std::isfinite(v)) return false;
-        D[j] = v;
-        iD[j] = 1.0 / v;  // one division per column; the column and the back substitution multiply by it
-        for (int i = j + 1; i < 6; i++) {
-            double w = H[i][j];
-            for (int k = 0; k < j; k++) w = w - L[i][k] * L[j][k] * D[k];
-            L[i][j] = w * iD[j];
+// The segment's correspondence keys (empty for segments above kKeyScanMax)
+void gicp_keys(const float* tgt_xyz, int nt, std::vector<pcore::gicpm::NNTarget>& keys, float org[3]) {
+    keys.clear();
+    org[0] = org[1] = org[2] = 0.0f;
+    if (nt > pcore::gicpm::kKeyScanMax) return;
+    float o3[3];
+    pcore::gicpm::nn_origin(nt, [&](int i, float* p) {
+        for (int a = 0; a < 3; a++) p[a] = tgt_xyz[(size_t)3 * i + a];
+    }, o3);
+    for (int a = 0; a < 3; a++) org[a] = o3[a];
+    keys.resize(nt);
+    for (int i = 0; i < nt; i++)
+        keys[i] = pcore::gicpm::nn_target(tgt_xyz[3 * (size_t)i], tgt_xyz[3 * (size_t)i + 1], tgt_xyz[3 * (size_t)i + 2],
+                                          org[0], org[1], org[2]);
+}
+
+struct OXform {
+    double R[3][3];
+    double t[3];
+};
+
+// the GPU's reduction: 64 per-lane sequential partials (point i -> lane i % 64), then the wave shuffle-down tree
+double lane_tree(const double* part, int stride, int v) {
+    double lane[64];
+    for (int l = 0; l < 64; l++) lane[l] = part[(size_t)stride * l + v];
+    for (int off = 32; off > 0; off >>= 1)
+        for (int l = 0; l < off; l++) lane[l] = lane[l] + lane[l + off];
+    return lane[0];
+}
+
+// Linearisation at x (fast_gicp linearize): correspondences, per-point Mahalanobis matrices and the 28 reduced
+// terms (upper H, b, error), in the GPU's order.
+void gicp_linearize_spec(const OXform& x, const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz,
+                         const double* tgt_cov, int nt, const pcore::gicpm::NNTarget* keys, const float* org,
+                         int32_t* corr, double* mah, double sys[pcore::gicpm::kTerms]) {
+    constexpr int NT = pcore::gicpm::kTerms;
+    std::vector<double> part((size_t)64 * NT, 0.0);
+    float Rf[3][3], tf[3];
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) Rf[r][c] = (float)x.R[r][c];
+        tf[r] = (float)x.t[r];
+    }
+    for (int i = 0; i < ns; i++) {
+        const float* s = src_xyz + (size_t)3 * i;
+        float qf[3];
+        pcore::gicpm::query_f(Rf, tf, s[0], s[1], s[2], qf);
+        const int j = gicp_nn(qf, tgt_xyz, nt, keys, org);
+        corr[i] = j;
+        if (j < 0) continue;
+        const double s0 = (double)s[0], s1 = (double)s[1], s2 = (double)s[2];
+        double q[3];
+        for (int r = 0; r < 3; r++) q[r] = x.R[r][0] * s0 + x.R[r][1] * s1 + x.R[r][2] * s2 + x.t[r];
+        double cs[6], ct[6], M6[6], acc[NT];
+        for (int e = 0; e < 6; e++) { cs[e] = src_cov[(size_t)6 * i + e]; ct[e] = tgt_cov[(size_t)6 * j + e]; }
+        const double tj[3] = {(double)tgt_xyz[3 * (size_t)j + 0], (double)tgt_xyz[3 * (size_t)j + 1],
+                              (double)tgt_xyz[3 * (size_t)j + 2]};
+        double* pl = part.data() + (size_t)NT * (i % 64);
+        for (int v = 0; v < NT; v++) acc[v] = pl[v];
+        pcore::gicpm::contrib(x.R, q, cs, tj, ct, acc, M6);
+        for (int v = 0; v < NT; v++) pl[v] = acc[v];
+        for (int e = 0; e < 6; e++) mah[(size_t)6 * i + e] = M6[e];
+    }
+    for (int v = 0; v < NT; v++) sys[v] = lane_tree(part.data(), NT, v);
+}
+
+// One LM iteration (LsqRegistration::step_lm) on the reduced system, as the GPU's lm_iteration
+int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double& lambda, const float* src_xyz, int ns,
+                      const float* tgt_xyz, const int32_t* corr, const double* mah, double rot_eps, double trans_eps) {
+    namespace gm = pcore::gicpm;
+    const double y0 = sys[gm::kErr];
+    if (lambda < 0.0) lambda = gm::lm_init_lambda(sys);
+    double nu = 2.0;
+    std::vector<double> part(64);
+    for (int trial = 0; trial < gm::kLmMaxTrials; trial++) {
+        double d[6];
+        gm::lm_solve(sys, lambda, d);
+        if (!gm::all_finite6(d)) return gm::kLmFailed;
+        double Rd[3][3], td[3];
+        gm::se3_exp(d, Rd, td);
+        OXform xi;
+        gm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
+        std::fill(part.begin(), part.end(), 0.0);
+        for (int i = 0; i < ns; i++) {
+            const int j = corr[i];
+            if (j < 0) continue;
+            const double s0 = (double)src_xyz[3 * (size_t)i], s1 = (double)src_xyz[3 * (size_t)i + 1],
+                         s2 = (double)src_xyz[3 * (size_t)i + 2];
+            double e[3];
+            for (int r = 0; r < 3; r++) {
+                const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
+                e[r] = (double)tgt_xyz[3 * (size_t)j + r] - q;
+            }
+            double M6[6];
+            for (int k = 0; k < 6; k++) M6[k] = mah[(size_t)6 * i + k];
+            part[i % 64] += gm::mahal_err(M6, e);
+        }
+        const double yi = lane_tree(part.data(), 1, 0);
+        const double rho = gm::lm_rho(sys, lambda, d, y0, yi);
+        if (rho < 0.0) {
+            if (gm::is_converged(Rd, td, rot_eps, trans_eps)) return gm::kLmConverged;
+            lambda = nu * lambda;
+            nu = 2.0 * nu;
+            continue;
+        }
+        x = xi;
+        lambda = gm::lm_accept_lambda(lambda, rho);
+        return gm::is_converged(Rd, td, rot_eps, trans_eps) ? gm::kLmConverged : gm::kLmAccepted;
+    }
+    return gm::kLmFailed;
+}
+
+// ---- independent textbook restatement of one point's linearisation (test reference; shares nothing with
+// pcore_gicp_math.h): fast_gicp's 4x4 homogeneous form in long double,
+//   RCR = C_B + T C_A T^T, RCR(3,3) = 1, M = RCR^-1 (Gauss-Jordan, partial pivoting), M(3,3) = 0,
+//   e = mean_B - T mean_A, J = [[skew(T mean_A), -I], [0, 0]] (4 x 6), H += J^T M J, b += J^T M e, y += e^T M e.
+typedef long double ld;
+
+void inverse4(const ld A[4][4], ld out[4][4]) {
+    ld M[4][8];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 8; c++) M[r][c] = c < 4 ? A[r][c] : (c - 4 == r ? 1.0L : 0.0L);
+    for (int k = 0; k < 4; k++) {
+        int p = k;
+        for (int r = k + 1; r < 4; r++)
+            if (std::fabs(M[r][k]) > std::fabs(M[p][k])) p = r;
+        if (p != k)
+            for (int c = 0; c < 8; c++) std::swap(M[k][c], M[p][c]);
+        const ld piv = M[k][k];
+        for (int c = 0; c < 8; c++) M[k][c] /= piv;
+        for (int r = 0; r < 4; r++) {
+            if (r == k) continue;
+            const ld f = M[r][k];
+            for (int c = 0; c < 8; c++) M[r][c] -= f * M[k][c];
         }
     }
-    double y[6];
-    for (int i = 0; i < 6; i++) {
-        double v = -b[i];
-        for (int k = 0; k < i; k++) v = v - L[i][k] * y[k];
-        y[i] = v;
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) out[r][c] = M[r][c + 4];
+}
+
+void textbook_point(const ld T[4][4], const float* s, const double* cs6, const float* tj, const double* ct6, ld H[6][6],
+                    ld b[6], ld& err) {
+    const ld mA[4] = {(ld)s[0], (ld)s[1], (ld)s[2], 1.0L};
+    const ld mB[4] = {(ld)tj[0], (ld)tj[1], (ld)tj[2], 1.0L};
+    ld CA[4][4] = {}, CB[4][4] = {};
+    const int sym[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            CA[r][c] = (ld)cs6[sym[r][c]];
+            CB[r][c] = (ld)ct6[sym[r][c]];
+        }
+    ld tA[4];
+    for (int r = 0; r < 4; r++) {
+        tA[r] = 0.0L;
+        for (int k = 0; k < 4; k++) tA[r] += T[r][k] * mA[k];
     }
-    for (int i = 5; i >= 0; i--) {
-        double v = y[i] * iD[i];
-        for (int k = i + 1; k < 6; k++) v = v - L[k][i] * d[k];
-        d[i] = v;
+    ld TC[4][4], RCR[4][4];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            TC[r][c] = 0.0L;
+            for (int k = 0; k < 4; k++) TC[r][c] += T[r][k] * CA[k][c];
+        }
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            ld v = 0.0L;
+            for (int k = 0; k < 4; k++) v += TC[r][k] * T[c][k];
+            RCR[r][c] = CB[r][c] + v;
+        }
+    RCR[3][3] = 1.0L;
+    ld M[4][4];
+    inverse4(RCR, M);
+    M[3][3] = 0.0L;
+    ld e[4];
+    for (int r = 0; r < 4; r++) e[r] = mB[r] - tA[r];
+    ld J[4][6] = {};
+    J[0][1] = -tA[2]; J[0][2] = tA[1];
+    J[1][0] = tA[2];  J[1][2] = -tA[0];
+    J[2][0] = -tA[1]; J[2][1] = tA[0];
+    J[0][3] = -1.0L; J[1][4] = -1.0L; J[2][5] = -1.0L;
+    ld MJ[4][6], Me[4];
+    for (int r = 0; r < 4; r++) {
+        for (int c = 0; c < 6; c++) {
+            MJ[r][c] = 0.0L;
+            for (int k = 0; k < 4; k++) MJ[r][c] += M[r][k] * J[k][c];
+        }
+        Me[r] = 0.0L;
+        for (int k = 0; k < 4; k++) Me[r] += M[r][k] * e[k];
     }
-    for (int i = 0; i < 6; i++)
-        if (!std::isfinite(d[i])) return false;
-    return true;
+    for (int a = 0; a < 6; a++) {
+        for (int c = 0; c < 6; c++) {
+            ld v = 0.0L;
+            for (int k = 0; k < 4; k++) v += J[k][a] * MJ[k][c];
+            H[a][c] += v;
+        }
+        ld v = 0.0L;
+        for (int k = 0; k < 4; k++) v += J[k][a] * Me[k];
+        b[a] += v;
+    }
+    ld y = 0.0L;
+    for (int k = 0; k < 4; k++) y += e[k] * Me[k];
+    err += y;
 }
 
 }  // namespace
@@ -596,80 +745,105 @@ void orc_covariances(const float* xyz, int n, int k, double* out_cov6) {
 
 int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov, int nt,
              int max_iter, double rot_eps, double trans_eps, double* out_T) {
-    double R[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
-    double t[3] = {0.0, 0.0, 0.0};
+    OXform x;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) x.R[r][c] = r == c ? 1.0 : 0.0;
+        x.t[r] = 0.0;
+    }
     int it = 0;
     if (ns > 0 && nt > 0) {
-        std::vector<double> part((size_t)kGicpThreads * pcore::gicpm::kTerms);
         std::vector<pcore::gicpm::NNTarget> keys;
-        float org[3] = {0.0f, 0.0f, 0.0f};
-        if (nt <= pcore::gicpm::kKeyScanMax) {
-            pcore::gicpm::nn_origin(nt, [&](int i, float* p) {
-                for (int a = 0; a < 3; a++) p[a] = tgt_xyz[(size_t)3 * i + a];
-            }, org);
-            keys.resize(nt);
-            for (int i = 0; i < nt; i++)
-                keys[i] = pcore::gicpm::nn_target(tgt_xyz[3 * (size_t)i], tgt_xyz[3 * (size_t)i + 1],
-                                                  tgt_xyz[3 * (size_t)i + 2], org[0], org[1], org[2]);
-        }
+        float org[3];
+        gicp_keys(tgt_xyz, nt, keys, org);
+        std::vector<int32_t> corr(ns);
+        std::vector<double> mah((size_t)6 * ns);
+        double lambda = -1.0;
         for (it = 0; it < max_iter;) {
-            std::fill(part.begin(), part.end(), 0.0);
-            for (int i = 0; i < ns; i++)
-                gicp_contrib(R, t, src_xyz + (size_t)3 * i, src_cov + (size_t)6 * i, tgt_xyz, tgt_cov, nt,
-                             keys.empty() ? nullptr : keys.data(), org,
-                             part.data() + (size_t)pcore::gicpm::kTerms * (i % kGicpThreads));
-            // fixed reduction: per wave shuffle-down tree to lane 0, then the 4 waves in order
-            double tot[pcore::gicpm::kTerms];
-            for (int v = 0; v < pcore::gicpm::kTerms; v++) {
-                double wsum[kGicpThreads / 64];
-                for (int w = 0; w < kGicpThreads / 64; w++) {
-                    double lane[64];
-                    for (int l = 0; l < 64; l++) lane[l] = part[(size_t)pcore::gicpm::kTerms * (w * 64 + l) + v];
-                    for (int off = 32; off > 0; off >>= 1)
-                        for (int l = 0; l < off; l++) lane[l] = lane[l] + lane[l + off];
-                    wsum[w] = lane[0];
-                }
-                double s = wsum[0];
-                for (int w = 1; w < kGicpThreads / 64; w++) s = s + wsum[w];
-                tot[v] = s;
-            }
-            double d[6];
-            if (!ldlt_solve6(tot, tot + 21, d)) break;
             it++;
-            double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
-            const double nrm = std::sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
-            const double inv = 1.0 / nrm;
-            qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
-            const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
-            const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
-            const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
-                                     {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
-                                     {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
-            double Rn[3][3], tn[3];
-            for (int r = 0; r < 3; r++) {
-                for (int c = 0; c < 3; c++) Rn[r][c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
-                tn[r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
-            }
-            double dr = 0.0, dt = 0.0;
-            for (int r = 0; r < 3; r++) {
-                for (int c = 0; c < 3; c++) {
-                    const double v = std::fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
-                    dr = v > dr ? v : dr;
-                }
-                const double v = std::fabs(d[3 + r]);
-                dt = v > dt ? v : dt;
-            }
-            std::memcpy(R, Rn, sizeof(R));
-            std::memcpy(t, tn, sizeof(t));
-            if (dr < rot_eps && dt < trans_eps) break;
+            double sys[pcore::gicpm::kTerms];
+            gicp_linearize_spec(x, src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, keys.empty() ? nullptr : keys.data(),
+                                org, corr.data(), mah.data(), sys);
+            const int st = gicp_lm_iteration(sys, x, lambda, src_xyz, ns, tgt_xyz, corr.data(), mah.data(), rot_eps,
+                                             trans_eps);
+            if (st != pcore::gicpm::kLmAccepted) break;
         }
     }
     for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) out_T[4 * r + c] = R[r][c];
-        out_T[4 * r + 3] = t[r];
+        for (int c = 0; c < 3; c++) out_T[4 * r + c] = x.R[r][c];
+        out_T[4 * r + 3] = x.t[r];
     }
     out_T[12] = 0.0; out_T[13] = 0.0; out_T[14] = 0.0; out_T[15] = 1.0;
     return it;
+}
+
+// The linearisation at T (double 4x4 row-major) two ways, on the spec's correspondences (out_corr, ns):
+// textbook = 0: the spec's (pcore_gicp_math.h contrib, the GPU's reduction order); textbook = 1: the independent
+// long-double 4x4 restatement summed in point order.  out_sys: 28 terms (upper H row-major, b, error).
+void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz,
+                        const double* tgt_cov, int nt, const double* T, int textbook, int32_t* out_corr,
+                        double* out_sys) {
+    OXform x;
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) x.R[r][c] = T[4 * r + c];
+        x.t[r] = T[4 * r + 3];
+    }
+    std::vector<pcore::gicpm::NNTarget> keys;
+    float org[3];
+    gicp_keys(tgt_xyz, nt, keys, org);
+    std::vector<double> mah((size_t)6 * (ns > 0 ? ns : 1));
+    double sys[pcore::gicpm::kTerms];
+    gicp_linearize_spec(x, src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, keys.empty() ? nullptr : keys.data(), org,
+                        out_corr, mah.data(), sys);
+    if (!textbook) {
+        for (int v = 0; v < pcore::gicpm::kTerms; v++) out_sys[v] = sys[v];
+        return;
+    }
+    ld TT[4][4];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) TT[r][c] = (ld)T[4 * r + c];
+    ld H[6][6] = {}, b[6] = {}, err = 0.0L;
+    for (int i = 0; i < ns; i++) {
+        const int j = out_corr[i];
+        if (j < 0) continue;
+        textbook_point(TT, src_xyz + (size_t)3 * i, src_cov + (size_t)6 * i, tgt_xyz + (size_t)3 * j,
+                       tgt_cov + (size_t)6 * j, H, b, err);
+    }
+    int h = 0;
+    for (int a = 0; a < 6; a++)
+        for (int c = a; c < 6; c++) out_sys[h++] = (double)H[a][c];
+    for (int a = 0; a < 6; a++) out_sys[21 + a] = (double)b[a];
+    out_sys[27] = (double)err;
+}
+
+// The step's pieces, for the CPU tests of the spec: se3_exp -> 4x4 row-major; the damped LDLT solve of a 28-term
+// system; the double sin / cos.
+void orc_gicp_se3_exp(const double* a6, double* out_T) {
+    const double a[6] = {a6[0], a6[1], a6[2], a6[3], a6[4], a6[5]};
+    double Rd[3][3], td[3];
+    pcore::gicpm::se3_exp(a, Rd, td);
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) out_T[4 * r + c] = Rd[r][c];
+        out_T[4 * r + 3] = td[r];
+    }
+    out_T[12] = 0.0; out_T[13] = 0.0; out_T[14] = 0.0; out_T[15] = 1.0;
+}
+
+void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d) {
+    double d[6];
+    pcore::gicpm::lm_solve(sys, lambda, d);
+    for (int a = 0; a < 6; a++) out_d[a] = d[a];
+}
+
+double orc_sin_d(double x) { return pcore::dmath::sin_d(x); }
+double orc_cos_d(double x) { return pcore::dmath::cos_d(x); }
+
+// The spec's correspondence of float queries (n x 3) in a target segment: key scan (segments <= kKeyScanMax) or
+// plain float squared distance; out_j: -1 for none.
+void orc_gicp_nn(const float* q, int n, const float* tgt_xyz, int nt, int32_t* out_j) {
+    std::vector<pcore::gicpm::NNTarget> keys;
+    float org[3];
+    gicp_keys(tgt_xyz, nt, keys, org);
+    for (int i = 0; i < n; i++) out_j[i] = gicp_nn(q + (size_t)3 * i, tgt_xyz, nt, keys.empty() ? nullptr : keys.data(), org);
 }
 
 void orc_concat_pose(const double* T, const float* pose, float* out_pose) {

@@ -88,24 +88,42 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
 
 
 /* ---- GICP (a9/a10): build-owned spec, parity unpinned vs fast_gicp (un-vendored fork) --------------
- * Restates the public fast_gicp GICP at the settings of renderer.cu:1696-1705 with a deterministic
- * arithmetic order that the GPU kernels follow exactly (DESIGN.md "GICP spec"):
+ * fast_gicp's published FastGICP + LsqRegistration algorithm at the settings of renderer.cu:1693-1720, with a
+ * deterministic arithmetic order that the GPU kernels follow exactly (DESIGN.md "GICP spec"; the arithmetic is
+ * pcore_gicp_math.h, shared with the kernels, and held to the independent textbook restatement below):
  *  - covariance: k nearest points of the same cloud (float squared distance, ties -> lower index,
  *    list ordered by (distance, index)), double mean / covariance over k_eff = min(k, n), PLANE
  *    regularisation C = U diag(1, 1, 1e-3) U^T from 6 cyclic Jacobi sweeps (double, sqrt/div only);
- *  - Gauss-Newton on SE(3): correspondence of q = (float)(R s + t) = the first strict minimum over the
- *    target segment of the three-FMA key of pcore_gicp_math.h (|q'-t'|^2 - |q'|^2 about the segment's
- *    origin; segments of <= 2048 targets) or of the float squared distance (larger segments),
- *    Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I], H / b reduced in the GPU's fixed order
- *    (64 per-lane sequential partials, then the wave shuffle-down tree), 6x6 LDLT
- *    without pivoting (one reciprocal per column), left update T <- [R(q(w)) | rho] T with q = normalise(1, w/2), stop when
- *    max|dR - I| < rot_eps and max|dt| < trans_eps or after max_iter iterations.
+ *  - per iteration: correspondence of the float query float(T) s = the first strict minimum over the target
+ *    segment of the three-FMA key (|q'-t'|^2 - |q'|^2 about the segment's origin; segments of <= 2048 targets) or
+ *    of the float squared distance (larger segments); Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I];
+ *    H, b and the error e^T M e reduced in the GPU's fixed order (64 per-lane sequential partials, then the wave
+ *    shuffle-down tree);
+ *  - Levenberg-Marquardt (LsqRegistration::step_lm): lambda0 = 1e-9 max|diag H|, <= 10 trials of Eigen's pivoted
+ *    LDLT of H + lambda I, se3_exp (exact so3_exp + V rho), errors of the trials with the iteration's
+ *    correspondences, accept / reject by rho, lambda update; stop on a converged step
+ *    (max(|dR - I| / rot_eps, |dt| / trans_eps) < 1), ten rejections or max_iter iterations.
  * Covariances: double[6] (xx, xy, xz, yy, yz, zz) per point. */
 void orc_covariances(const float* xyz, int n, int k, double* out_cov6);
 
-/* Returns iterations run; out_T: double 4x4 row-major (source -> target, metres). */
+/* Returns iterations run (linearisations); out_T: double 4x4 row-major (source -> target, metres). */
 int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
              int nt, int max_iter, double rot_eps, double trans_eps, double* out_T);
+
+/* The linearisation at T (4x4 row-major double) on the spec's correspondences (out_corr: ns, -1 = none):
+ * textbook = 0 the spec's arithmetic and reduction order, textbook = 1 an independent long-double restatement of
+ * fast_gicp's 4x4 homogeneous form (RCR = C_B + T C_A T^T, RCR(3,3) = 1, M = RCR^-1 by Gauss-Jordan, M(3,3) = 0,
+ * dense J^T M J / J^T M e / e^T M e).  out_sys: 28 doubles (upper H row-major, b, error). */
+void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz,
+                        const double* tgt_cov, int nt, const double* T, int textbook, int32_t* out_corr,
+                        double* out_sys);
+/* Pieces of the step for the CPU spec tests: se3_exp(a6) -> 4x4; d = LDLT(H + lambda I).solve(-b) of a 28-term
+ * system; the double sin / cos of pcore_dmath.h; the spec's correspondences of n float queries. */
+void orc_gicp_se3_exp(const double* a6, double* out_T);
+void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d);
+double orc_sin_d(double x);
+double orc_cos_d(double x);
+void orc_gicp_nn(const float* q, int n, const float* tgt_xyz, int nt, int32_t* out_j);
 
 /* concatenate_transforms (renderer.cu:1412-1429): pose' = init_from_eigen((float(T) * to_eigen(pose,100)), 100). */
 void orc_concat_pose(const double* T, const float* pose, float* out_pose);

@@ -8,6 +8,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
+
 from . import build as _build
 
 PCORE_OK = 0
@@ -57,8 +59,9 @@ class IcpParams(ctypes.Structure):
 # renderer.cu:1696-1699
 ICP_K = 10
 ICP_MAX_ITER = 150
-ICP_ROT_EPS = 2e-3
-ICP_TRANS_EPS = 5e-4
+# renderer.cu:1698-1699 declares both as float and passes them to set_*_epsilon(double): the float values widened
+ICP_ROT_EPS = float(np.float32(2e-3))
+ICP_TRANS_EPS = float(np.float32(5e-4))
 
 _lib = None
 

@@ -77,6 +77,8 @@ struct pcore_ctx {
     DevBuf<float4> icp_cloud;
     DevBuf<int32_t> icp_count;
     DevBuf<double> icp_cov;
+    DevBuf<int32_t> icp_corr;   // GicpArgs::corr
+    DevBuf<double> icp_mahal;   // GicpArgs::mahal
     DevBuf<int32_t> icp_counter;
     DevBuf<uint32_t> icp_order_keys;  // 2 x chunk keys (in, out)
     DevBuf<int32_t> icp_order_idx;    // 2 x chunk indices (in, out = GicpArgs::pose_order)
@@ -302,7 +304,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part);
     delete c;
@@ -880,10 +882,10 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         c->cov_k_all = k;
     }
     const int nsamp = ws * hs;
-    // GICP scratch per pose: nsamp cloud slots (16 B) + covariances (48 B).  Chunks are as large as the
-    // budget below allows and equal in size: every chunk ends with
-    // the tail of its slowest pose, so fewer chunks mean fewer tails.
-    const size_t per_pose = (size_t)nsamp * 64;
+    // GICP scratch per pose: nsamp cloud slots (16 B) + covariances (48 B) + the iteration's correspondences (4 B)
+    // and Mahalanobis matrices (48 B).  Chunks are as large as the budget below allows and equal in size: every
+    // chunk ends with the tail of its slowest pose, so fewer chunks mean fewer tails.
+    const size_t per_pose = (size_t)nsamp * 116;
     // Up to 32 GiB (and at most 40 % of the free HBM): one chunk for 100k poses at 640x480 / stride 8.
     // Each chunk ends with the tail of its slowest pose, so on C3 (50k poses) one chunk instead of two
     // saves ~5 ms of a 37 ms step.
@@ -900,6 +902,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, dev_reserve(c->icp_cloud, (size_t)chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_count, (size_t)chunk));
     HIPC(c, dev_reserve(c->icp_cov, (size_t)6 * chunk * nsamp));
+    HIPC(c, dev_reserve(c->icp_corr, (size_t)chunk * nsamp));
+    HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 1));
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
@@ -911,6 +915,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.src = c->icp_cloud.p;
     g.src_count = c->icp_count.p;
     g.src_cov = c->icp_cov.p;
+    g.corr = c->icp_corr.p;
+    g.mahal = c->icp_mahal.p;
     g.src_cap = nsamp;
     g.tgt = c->tgt.p;
     g.tgt_cov = six ? c->tgt_cov_label.p : c->tgt_cov_all.p;

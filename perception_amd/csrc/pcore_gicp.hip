@@ -1,19 +1,21 @@
 // pcore_gicp.hip -- per-pose GICP refinement on gfx950.
 //
-// Build-owned spec (fast_gicp is an un-vendored fork; see DESIGN.md "GICP spec"), at the reference's
-// settings (renderer.cu:1696-1705): k = 10 covariance neighbours with PLANE regularisation,
-// nearest-neighbour correspondences inside the pose's label segment, Mahalanobis (C_t + R C_s R^T)^-1,
-// Gauss-Newton on SE(3), <= 150 iterations, rotation / translation epsilons 2e-3 / 5e-4.
-// The arithmetic order -- including the reduction tree of the 6x6 normal equations -- is fixed, and
-// the CPU oracle (oracle/pcore_oracle.cpp, orc_gicp) follows the same order, so the refined transforms
-// are reproducible bit for bit.
+// Build-owned spec (fast_gicp is an un-vendored fork; see DESIGN.md "GICP spec"): fast_gicp's published
+// FastGICP + LsqRegistration algorithm at the reference's settings (renderer.cu:1693-1720): k = 10 covariance
+// neighbours with PLANE regularisation, nearest-neighbour correspondences inside the pose's label segment,
+// Mahalanobis (C_t + R C_s R^T)^-1, Levenberg-Marquardt steps on SE(3) through the exact se3_exp, <= 150
+// iterations, rotation / translation epsilons 2e-3 / 5e-4.  The arithmetic lives in pcore_gicp_math.h; its
+// order -- including the reduction tree of the normal equations and of the trial errors -- is fixed, and the
+// CPU oracle (oracle/pcore_oracle.cpp, orc_gicp) follows the same order, so the refined transforms are
+// reproducible bit for bit.
 //
 //   covariance_kernel  one wave per segment (a pose's rendered cloud or an observed label): brute-force
 //                      k-NN of every point inside its segment (candidates staged through LDS), double
 //                      mean / covariance, 6-sweep Jacobi, PLANE regularisation.
-//   gicp_kernel        one wave per pose (4 per workgroup): per-lane sequential partial sums of J^T M J /
-//                      J^T M e, wave shuffle-down tree, one-lane 6x6 LDLT and update, then
+//   gicp_kernel        one wave per pose: per-lane sequential partial sums of J^T M J / J^T M e / e^T M e,
+//                      the LDS-transposed shuffle-down tree, the LM iteration on every lane (uniform), then
 //                      concatenate_transforms (renderer.cu:1412-1429).
+//   gicp_wide_kernel   small batches: eight waves search a pose's correspondences, wave 0 as gicp_kernel.
 #include "pcore_internal.h"
 
 #include <hipcub/hipcub.hpp>
@@ -473,71 +475,30 @@ __device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6
     c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y; c[4] = d.x; c[5] = d.y;
 }
 
-// One point's Gauss-Newton contribution: the shared spec of pcore_gicp_math.h (the oracle calls the same
-// function), given the transformed point q, its correspondence tj and both covariances.
-__device__ __forceinline__ void gicp_contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6],
-                                             float4 tj, const double (&ct)[6], double (&acc)[gicpm::kTerms]) {
-    const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
-    gicpm::contrib(R, q, cs, t3, ct, acc);
-}
-
-// a wave-uniform double moved to SGPRs (R, t of the pose being refined)
+// a wave-uniform double moved to SGPRs (R, t of the pose being refined, the LM scalars)
 __device__ __forceinline__ double uniform_d(double x) {
     const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-
-// 6x6 LDLT without pivoting (orc ldlt_solve6).  Single lane.
-__device__ bool ldlt_solve6(const double* Hu, const double* b, double* d) {
-    double H[6][6];
-    int h = 0;
-    for (int a = 0; a < 6; a++)
-        for (int c = a; c < 6; c++) { H[a][c] = Hu[h]; H[c][a] = Hu[h]; h++; }
-    double L[6][6], D[6], iD[6];
-    for (int a = 0; a < 6; a++)
-        for (int c = 0; c < 6; c++) L[a][c] = 0.0;
-    for (int j = 0; j < 6; j++) {
-        double v = H[j][j];
-        for (int k = 0; k < j; k++) v = v - L[j][k] * L[j][k] * D[k];
-        if (!(v > 0.0) || !isfinite(v)) return false;
-        D[j] = v;
-        iD[j] = 1.0 / v;  // one division per column; the column and the back substitution multiply by it
-        for (int i = j + 1; i < 6; i++) {
-            double w = H[i][j];
-            for (int k = 0; k < j; k++) w = w - L[i][k] * L[j][k] * D[k];
-            L[i][j] = w * iD[j];
-        }
-    }
-    double y[6];
-    for (int i = 0; i < 6; i++) {
-        double v = -b[i];
-        for (int k = 0; k < i; k++) v = v - L[i][k] * y[k];
-        y[i] = v;
-    }
-    for (int i = 5; i >= 0; i--) {
-        double v = y[i] * iD[i];
-        for (int k = i + 1; k < 6; k++) v = v - L[k][i] * d[k];
-        d[i] = v;
-    }
-    for (int i = 0; i < 6; i++)
-        if (!isfinite(d[i])) return false;
-    return true;
+__device__ __forceinline__ float uniform_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, x)));
 }
 
-// The same shuffle-down tree through LDS, a transposed layout instead of 6 x 27 ds_bpermute rounds: every lane
-// stores its partial sums (14 values, then the other 13), lane k adds up value k's 64 entries in the tree's own
+// The wave shuffle-down tree through LDS, a transposed layout instead of 6 x 28 ds_bpermute rounds: every lane
+// stores its partial sums (14 values, then the other 14), lane k adds up value k's 64 entries in the tree's own
 // order -- node(l, off) = node(l, 2 off) + node(l + off, 2 off), leaves node(l, 64) = lane l's entry, so lane 0's
-// level-by-level sums ((x0 + x32) + (x16 + x48)) + ... come out bit-identical -- and the 27 sums return through LDS
-// to every lane.  One wave per workgroup (gicp_kernel<1>): ~7 KB of LDS.
-constexpr int kRedHalf = 14;
+// level-by-level sums ((x0 + x32) + (x16 + x48)) + ... come out bit-identical -- and the 28 sums land in
+// red[kRedHalf * 64 ...], where every lane reads them.  ~7.4 KB of LDS per wave.
+constexpr int kRedHalf = gicpm::kTerms / 2;
+constexpr int kRedDoubles = kRedHalf * 64 + gicpm::kTerms;
 template <int L, int OFF, int NV>
 __device__ __forceinline__ double tree_node(const double* col) {
     if constexpr (OFF == 64) return col[L * NV];
     else return tree_node<L, 2 * OFF, NV>(col) + tree_node<L + OFF, 2 * OFF, NV>(col);
 }
-__device__ __forceinline__ void lds_tree_sum(double (&acc)[gicpm::kTerms], double* red, int lane) {
+__device__ __forceinline__ const double* lds_tree_sum(const double (&acc)[gicpm::kTerms], double* red, int lane) {
     constexpr int NA = kRedHalf, NB = gicpm::kTerms - kRedHalf;
     double* out = red + kRedHalf * 64;
 #pragma unroll
@@ -550,48 +511,142 @@ __device__ __forceinline__ void lds_tree_sum(double (&acc)[gicpm::kTerms], doubl
     wave_lds_sync();
     if (lane < NB) out[NA + lane] = tree_node<0, 1, NB>(red + lane);
     wave_lds_sync();
-#pragma unroll
-    for (int v = 0; v < gicpm::kTerms; v++) acc[v] = out[v];
+    return out;
 }
 
-// Lane-0 step of an iteration: LDLT of the reduced normal equations, the left update of (R, t) into RT and
-// fast_gicp's convergence test.  Returns 0 continue, 1 stop without update (H not positive definite),
-// 2 stop after the update.
-__device__ __forceinline__ int solve_update(const double (&acc)[gicpm::kTerms], const double (&R)[3][3], const double (&t)[3],
-                                        double* RT, double rot_eps, double trans_eps) {
-    double d[6];
-    if (!ldlt_solve6(acc, acc + 21, d)) return 1;
-    double qw = 1.0, qx = d[0] * 0.5, qy = d[1] * 0.5, qz = d[2] * 0.5;
-    const double nrm = sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
-    const double inv = 1.0 / nrm;
-    qw = qw * inv; qx = qx * inv; qy = qy * inv; qz = qz * inv;
-    const double xx = qx * qx, yy = qy * qy, zz = qz * qz, xy = qx * qy, xz = qx * qz, yz = qy * qz;
-    const double wx = qw * qx, wy = qw * qy, wz = qw * qz;
-    const double Rd[3][3] = {{1.0 - 2.0 * (yy + zz), 2.0 * (xy - wz), 2.0 * (xz + wy)},
-                             {2.0 * (xy + wz), 1.0 - 2.0 * (xx + zz), 2.0 * (yz - wx)},
-                             {2.0 * (xz - wy), 2.0 * (yz + wx), 1.0 - 2.0 * (xx + yy)}};
-    double dr = 0.0, dt = 0.0;
+// the pose's state in double: rotation and translation of the GICP transform (source -> target, metres)
+struct Xform {
+    double R[3][3];
+    double t[3];
+};
+
+__device__ __forceinline__ void xform_identity(Xform& x) {
+#pragma unroll
     for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) {
-            RT[3 * r + c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
-            const double v = fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
-            dr = v > dr ? v : dr;
-        }
-        RT[9 + r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + d[3 + r];
-        const double v = fabs(d[3 + r]);
-        dt = v > dt ? v : dt;
+#pragma unroll
+        for (int c = 0; c < 3; c++) x.R[r][c] = r == c ? 1.0 : 0.0;
+        x.t[r] = 0.0;
     }
-    return (dr < rot_eps && dt < trans_eps) ? 2 : 0;
+}
+
+// Linearisation of one round of 64 source points (point i on lane i % 64), fast_gicp linearize /
+// update_correspondences: the correspondence of the float query, then -- for points with one -- the shared
+// contribution into acc; the correspondence and M go to the iteration's scratch (corr[i], mah[6 i ..]) for the
+// trials' errors.
+template <bool STORE_CORR>
+__device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf)[3][3], const float (&tf)[3],
+                                                const float4* src, const double* scov, const float4* tgt,
+                                                const double* tcov, int ns, int i, bool use_grid, const LabelGrid& G,
+                                                const GicpArgs& g, const float* tquads, int nt, int j_in,
+                                                int32_t* corr, double* mah, double (&acc)[gicpm::kTerms]) {
+    const bool act = i < ns;
+    const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int j = j_in;
+    if (STORE_CORR) {
+        float qf[3];
+        gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
+        // correspondence: first strict minimum of the key (segments <= kKeyScanMax) or of the float squared
+        // distance (grid search of larger segments), as orc_gicp
+        float best = INFINITY;
+        j = -1;
+        if (use_grid) {
+            if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qf[0], qf[1], qf[2], best, j);
+        } else {
+            scan_quads(tquads, (nt + 3) >> 2, qf[0], qf[1], qf[2], best, j);
+        }
+        if (act) corr[i] = j;
+    }
+    if (act && j >= 0) {
+        const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+        double q[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) q[r] = x.R[r][0] * s0 + x.R[r][1] * s1 + x.R[r][2] * s2 + x.t[r];
+        double cs[6], ct[6], M6[6];
+        load_cov(scov, i, cs);
+        load_cov(tcov, j, ct);
+        const float4 tj = tgt[j];
+        const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
+        gicpm::contrib(x.R, q, cs, t3, ct, acc, M6);
+        double2* m2 = reinterpret_cast<double2*>(mah + (size_t)6 * i);
+        m2[0] = make_double2(M6[0], M6[1]);
+        m2[1] = make_double2(M6[2], M6[3]);
+        m2[2] = make_double2(M6[4], M6[5]);
+    }
+}
+
+// One Levenberg-Marquardt iteration of one wave (LsqRegistration::step_lm) on the reduced system `sys` (28 sums in
+// LDS: upper H, b, the error y0 at x): up to kLmMaxTrials solves of (H + lambda I) d = -b, each scored by the error
+// at delta * x with the iteration's correspondences and M (point i on lane i % 64, summed by the shuffle-down tree).
+// Every lane runs the same uniform arithmetic; the scalars that steer it are moved to SGPRs.
+template <typename CorrPtr>
+__device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double& lambda, const float4* src,
+                                            CorrPtr corr, const double* mah, const float4* tgt, int ns, int lane,
+                                            double rot_eps, double trans_eps) {
+    const double y0 = uniform_d(sys[gicpm::kErr]);
+    if (lambda < 0.0) lambda = uniform_d(gicpm::lm_init_lambda(sys));
+    double nu = 2.0;
+    for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
+        double d[6];
+        gicpm::lm_solve(sys, lambda, d);
+#pragma unroll
+        for (int a = 0; a < 6; a++) d[a] = uniform_d(d[a]);
+        if (!gicpm::all_finite6(d)) return gicpm::kLmFailed;  // guard: a non-finite system
+        double Rd[3][3], td[3];
+        gicpm::se3_exp(d, Rd, td);
+        Xform xi;
+        gicpm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) xi.R[r][c] = uniform_d(xi.R[r][c]);
+            xi.t[r] = uniform_d(xi.t[r]);
+        }
+        // the error at x_i (FastGICP::compute_error: this iteration's correspondences and Mahalanobis matrices)
+        double ea = 0.0;
+        for (int i0 = 0; i0 < ns; i0 += 64) {
+            const int i = i0 + lane;
+            const int j = i < ns ? corr[i] : -1;
+            if (j >= 0) {
+                const float4 sp = src[i];
+                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+                const float4 tj = tgt[j];
+                double e[3];
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
+                    e[r] = (double)(r == 0 ? tj.x : r == 1 ? tj.y : tj.z) - q;
+                }
+                const double2* m2 = reinterpret_cast<const double2*>(mah + (size_t)6 * i);
+                const double2 a = m2[0], b = m2[1], c = m2[2];
+                const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+                ea += gicpm::mahal_err(M6, e);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) ea = ea + __shfl_down(ea, off, 64);
+        const double yi = uniform_d(ea);  // lane 0: the tree's sum
+        const double rho = uniform_d(gicpm::lm_rho(sys, lambda, d, y0, yi));
+        if (rho < 0.0) {
+            if (gicpm::is_converged(Rd, td, rot_eps, trans_eps)) return gicpm::kLmConverged;
+            lambda = nu * lambda;
+            nu = 2.0 * nu;
+            continue;
+        }
+        x = xi;
+        lambda = uniform_d(gicpm::lm_accept_lambda(lambda, rho));
+        return gicpm::is_converged(Rd, td, rot_eps, trans_eps) ? gicpm::kLmConverged : gicpm::kLmAccepted;
+    }
+    return gicpm::kLmFailed;  // LsqRegistration: "lm not converged"
 }
 
 // concatenate_transforms (renderer.cu:1412-1429): float(T) * to_eigen(pose, 100), init_from_eigen(., 100)
-__device__ __forceinline__ void write_pose(const GicpArgs& g, int gp, const double* RT, int iters) {
+__device__ __forceinline__ void write_pose(const GicpArgs& g, int gp, const Xform& x, int iters) {
     const float* pin = g.poses_in + (size_t)16 * gp;
     float A[4][4], Tf[4][4];
     for (int r = 0; r < 4; r++)
         for (int c = 0; c < 4; c++) {
             A[r][c] = r < 3 ? pin[4 * r + c] / 100.0f : pin[4 * r + c];
-            Tf[r][c] = r < 3 ? (float)(c < 3 ? RT[3 * r + c] : RT[9 + r]) : (c == 3 ? 1.0f : 0.0f);
+            Tf[r][c] = r < 3 ? (float)(c < 3 ? x.R[r][c] : x.t[r]) : (c == 3 ? 1.0f : 0.0f);
         }
     float* pout = g.poses_out + (size_t)16 * gp;
     for (int r = 0; r < 4; r++)
@@ -602,160 +657,110 @@ __device__ __forceinline__ void write_pose(const GicpArgs& g, int gp, const doub
     if (g.iters_out) g.iters_out[gp] = iters;
 }
 
-// Synchronise the WPP waves that share one pose: LDS writes of any lane visible to all of them.
-template <int WPP>
-__device__ __forceinline__ void group_sync() {
-    if constexpr (WPP == 1)
-        wave_lds_sync();
-    else
-        __syncthreads();
+__device__ __forceinline__ void xform_float(const Xform& x, float (&Rf)[3][3], float (&tf)[3]) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) Rf[r][c] = uniform_f((float)x.R[r][c]);
+        tf[r] = uniform_f((float)x.t[r]);
+    }
 }
 
-// One pose per workgroup of WPP waves; persistent workgroups pull poses from a counter.  The group's
-// threads accumulate their points' contributions sequentially (point i -> thread i % (64 WPP)), each
-// wave reduces with a shuffle-down tree, thread 0 adds the wave sums in order, solves and updates.
-// The per-pose iteration chain is latency-bound, so the slowest pose sets a chunk's tail; WPP > 1
-// splits each iteration's scan over more lanes.
+// the pose a GICP workgroup works on next and its target segment
+struct GicpPose {
+    int pose, gp, ns, nt, seg;
+    const float4* src;
+    const double* scov;
+    const double* tcov;
+    const float4* tgt;
+    const float* tquads;
+    int32_t* corr;
+    double* mah;
+    bool use_grid;
+};
+
+__device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
+    GicpPose p;
+    p.pose = pose;
+    p.gp = g.pose_base + pose;
+    p.ns = g.src_count[pose];
+    p.src = g.src + (size_t)pose * g.src_cap;
+    p.scov = g.src_cov + (size_t)6 * pose * g.src_cap;
+    p.corr = g.corr + (size_t)pose * g.src_cap;
+    p.mah = g.mahal + (size_t)6 * pose * g.src_cap;
+    int seg = g.whole_seg;
+    if (g.pose_label) {
+        const int pl = g.pose_label[p.gp];
+        seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
+    }
+    seg = __builtin_amdgcn_readfirstlane(seg);
+    p.seg = seg;
+    const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
+    p.nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
+    p.tcov = g.tgt_cov + (size_t)6 * lo;
+    p.tgt = g.tgt + lo;
+    p.tquads = g.tgt_quads + (seg >= 0 ? (size_t)16 * g.seg_qoff[seg] : 0);
+    p.use_grid = p.nt > kGridNNMin && g.grids != nullptr && seg >= 0;  // exact grid shell search
+    return p;
+}
+
+// One wave per pose; persistent waves pull poses from a counter.  Each iteration linearises in rounds of 64
+// source points (point i -> lane i % 64, contributions added in point order), reduces the 28 terms by the
+// LDS-transposed shuffle-down tree and runs the LM iteration on every lane.  The per-pose iteration chain is
+// latency-bound, so the slowest pose sets a chunk's tail (the queue is ordered longest first).
 #ifndef PCORE_GICP_WAVES_PER_EU
 #define PCORE_GICP_WAVES_PER_EU 3
 #endif
-#ifndef PCORE_GICP_WPP
-#define PCORE_GICP_WPP 1
-#endif
-#ifndef PCORE_GICP_LDS_RED
-#define PCORE_GICP_LDS_RED 1
-#endif
-constexpr int kGicpWpp = PCORE_GICP_WPP;  // must match kGicpThreads / 64 of orc_gicp
 
-template <int WPP>
-__global__ void __launch_bounds__(64 * WPP) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
 gicp_kernel(GicpArgs g, int num_poses) {
-    constexpr int NT = 64 * WPP;
-    __shared__ double RT[12];
-    __shared__ double sPart[WPP][gicpm::kTerms];
-    __shared__ int sPose, sFlag;
-#if PCORE_GICP_LDS_RED
-    __shared__ double sRed[kRedHalf * 64 + gicpm::kTerms];
-#endif
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ double sRed[kRedDoubles];
+    __shared__ int sPose;
+    const int lane = threadIdx.x;
     GPROF_DECL;
     for (;;) {
-        group_sync<WPP>();  // the previous pose's reads of the shared state are done
-        if (tid == 0) {
+        wave_lds_sync();  // the previous pose's reads of sPose are done
+        if (lane == 0) {
             const int q = atomicAdd(g.work_counter, 1);
             sPose = (g.pose_order && q < num_poses) ? g.pose_order[q] : q;
         }
-        group_sync<WPP>();
+        wave_lds_sync();
         const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
         if (pose >= num_poses) break;
-        const int gp = g.pose_base + pose;
-        const int ns = g.src_count[pose];
-        const float4* src = g.src + (size_t)pose * g.src_cap;
-        const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
-        int seg = g.whole_seg;
-        if (g.pose_label) {
-            const int pl = g.pose_label[gp];
-            seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
-        }
-        seg = __builtin_amdgcn_readfirstlane(seg);
-        const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
-        const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
-        const double* tcov = g.tgt_cov + (size_t)6 * lo;
-        const float4* tgt = g.tgt + lo;
-        const float* tquads = g.tgt_quads + (seg >= 0 ? (size_t)16 * g.seg_qoff[seg] : 0);
-        const bool use_grid = nt > kGridNNMin && g.grids != nullptr && seg >= 0;  // exact grid shell search
+        const GicpPose P = gicp_pose(g, pose);
         LabelGrid G{};
-        if (use_grid) G = g.grids[seg];
-        if (tid == 0) {
-            for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
-        }
+        if (P.use_grid) G = g.grids[P.seg];
+        Xform x;
+        xform_identity(x);
+        double lambda = -1.0;
         int iters = 0;
-        bool done = ns <= 0 || nt <= 0;
-        for (int it = 0; it < g.max_iter && !done; it++) {
-            group_sync<WPP>();
-            double R[3][3], t[3];
+        if (P.ns > 0 && P.nt > 0) {
+            for (int it = 0; it < g.max_iter; it++) {
+                iters++;
+                float Rf[3][3], tf[3];
+                xform_float(x, Rf, tf);
+                double acc[gicpm::kTerms];
 #pragma unroll
-            for (int r = 0; r < 3; r++) {
-#pragma unroll
-                for (int c = 0; c < 3; c++) R[r][c] = uniform_d(RT[3 * r + c]);
-                t[r] = uniform_d(RT[9 + r]);
-            }
-            double acc[gicpm::kTerms];
-#pragma unroll
-            for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-            // rounds of NT source points: point i -> thread i % NT, contributions added in point order
-            for (int i0 = 0; i0 < ns; i0 += NT) {
-                GPROF_T(t_r0);
-                const int i = i0 + tid;
-                const bool act = i < ns;
-                const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-                double q[3];
-#pragma unroll
-                for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
-                const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
-                // correspondence: first strict minimum of the key (segments <= kKeyScanMax) or of the float squared
-                // distance (grid search of larger segments), as orc gicp_contrib
-                int j = -1;
-                float best = INFINITY;
-                if (use_grid) {
-                    if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qx, qy, qz, best, j);
-                } else {
-                    scan_quads(tquads, (nt + 3) >> 2, qx, qy, qz, best, j);
+                for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
+                for (int i0 = 0; i0 < P.ns; i0 += 64) {
+                    GPROF_T(t_r0);
+                    linearize_round<true>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
+                                          P.tquads, P.nt, -1, P.corr, P.mah, acc);
+                    GPROF_TD(t_r1, acc[gicpm::kErr]);
+                    GPROF_ADD(0, t_r0, t_r1);
                 }
-                GPROF_TD(t_r1, best);
-                if (act && j >= 0) {
-                    double cs[6], ct[6];
-                    load_cov(scov, i, cs);
-                    load_cov(tcov, j, ct);
-                    gicp_contrib(R, q, cs, tgt[j], ct, acc);
-                }
-                GPROF_TD(t_r2, acc[gicpm::kTerms - 1]);
-                GPROF_ADD(0, t_r0, t_r1);
-                GPROF_ADD(1, t_r1, t_r2);
+                GPROF_T(t_b);
+                const double* sys = lds_tree_sum(acc, sRed, lane);
+                GPROF_TD(t_c, sys[0]);
+                const int st = lm_iteration(sys, x, lambda, P.src, P.corr, P.mah, P.tgt, P.ns, lane, g.rot_eps,
+                                            g.trans_eps);
+                GPROF_TD(t_d, st);
+                GPROF_ADD(2, t_b, t_c);
+                GPROF_ADD(3, t_c, t_d);
+                if (st != gicpm::kLmAccepted) break;
             }
-            GPROF_TD(t_b, acc[gicpm::kTerms - 1]);
-#if PCORE_GICP_LDS_RED
-            if constexpr (WPP == 1) {
-                lds_tree_sum(acc, sRed, lane);
-            } else
-#endif
-            {
-#pragma unroll
-            for (int v = 0; v < gicpm::kTerms; v++) {
-                double x = acc[v];
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
-                acc[v] = x;
-            }
-            }
-            if constexpr (WPP > 1) {
-                if (lane == 0) {
-#pragma unroll
-                    for (int v = 0; v < gicpm::kTerms; v++) sPart[wave][v] = acc[v];
-                }
-                __syncthreads();
-                if (tid == 0) {
-#pragma unroll
-                    for (int v = 0; v < gicpm::kTerms; v++) {
-                        double x = sPart[0][v];
-                        for (int w = 1; w < WPP; w++) x = x + sPart[w][v];
-                        acc[v] = x;
-                    }
-                }
-            }
-            GPROF_TD(t_c, acc[gicpm::kTerms - 1]);
-            if (tid == 0) sFlag = solve_update(acc, R, t, RT, g.rot_eps, g.trans_eps);
-            group_sync<WPP>();
-            const int flag = __builtin_amdgcn_readfirstlane(sFlag);
-            GPROF_TD(t_d, flag);
-            GPROF_ADD(2, t_b, t_c);
-            GPROF_ADD(3, t_c, t_d);
-            if (flag != 1) iters++;
-            done = flag != 0;
         }
-        group_sync<WPP>();
-        if (tid == 0) write_pose(g, gp, RT, iters);
+        if (lane == 0) write_pose(g, P.gp, x, iters);
     }
     GPROF_FLUSH;
 }
@@ -763,14 +768,15 @@ gicp_kernel(GicpArgs g, int num_poses) {
 
 // Small batches (C1: 128 poses fill 128 of 1024 SIMDs) with large target segments: WPP waves per pose.
 // All waves search the correspondences of the iteration's source points (round r -> wave r % WPP), the
-// indices go to LDS, and wave 0 then adds the contributions exactly as gicp_kernel<1> does -- point i on
-// lane i % 64, in point order -- so the refined poses are bit-identical; only the nearest-target
-// searches, the expensive part against a whole-scene target, run in parallel.
+// indices go to LDS, and wave 0 then adds the contributions and runs the LM iteration exactly as gicp_kernel
+// does -- point i on lane i % 64, in point order -- so the refined poses are bit-identical; only the
+// nearest-target searches, the expensive part against a whole-scene target, run in parallel.
 template <int WPP>
 __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num_poses) {
     constexpr int NT = 64 * WPP;
     extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
-    __shared__ double RT[12];
+    __shared__ double sRed[kRedDoubles];
+    __shared__ double sX[12];
     __shared__ int sPose, sFlag;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     for (;;) {
@@ -782,54 +788,31 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
         __syncthreads();
         const int pose = __builtin_amdgcn_readfirstlane(sPose);
         if (pose >= num_poses) break;
-        const int gp = g.pose_base + pose;
-        const int ns = g.src_count[pose];
-        const float4* src = g.src + (size_t)pose * g.src_cap;
-        const double* scov = g.src_cov + (size_t)6 * pose * g.src_cap;
-        int seg = g.whole_seg;
-        if (g.pose_label) {
-            const int pl = g.pose_label[gp];
-            seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
-        }
-        seg = __builtin_amdgcn_readfirstlane(seg);
-        const int lo = seg >= 0 ? g.seg_lo[seg] : 0;
-        const int nt = seg >= 0 ? g.seg_hi[seg] - lo : 0;
-        const double* tcov = g.tgt_cov + (size_t)6 * lo;
-        const float4* tgt = g.tgt + lo;
-        const float* tquads = g.tgt_quads + (seg >= 0 ? (size_t)16 * g.seg_qoff[seg] : 0);
-        const bool use_grid = nt > kGridNNMin && g.grids != nullptr && seg >= 0;
+        const GicpPose P = gicp_pose(g, pose);
         LabelGrid G{};
-        if (use_grid) G = g.grids[seg];
-        if (tid == 0) {
-            for (int i = 0; i < 12; i++) RT[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
-        }
+        if (P.use_grid) G = g.grids[P.seg];
+        Xform x;
+        xform_identity(x);
+        double lambda = -1.0;  // wave 0's
         int iters = 0;
-        bool done = ns <= 0 || nt <= 0;
-        for (int it = 0; it < g.max_iter && !done; it++) {
-            __syncthreads();
-            double R[3][3], t[3];
-#pragma unroll
-            for (int r = 0; r < 3; r++) {
-#pragma unroll
-                for (int c = 0; c < 3; c++) R[r][c] = uniform_d(RT[3 * r + c]);
-                t[r] = uniform_d(RT[9 + r]);
-            }
+        const bool run = P.ns > 0 && P.nt > 0;
+        for (int it = 0; run && it < g.max_iter; it++) {
+            iters++;
+            float Rf[3][3], tf[3];
+            xform_float(x, Rf, tf);
             // correspondences, all waves
-            for (int i0 = wave * 64; i0 < ns; i0 += NT) {
+            for (int i0 = wave * 64; i0 < P.ns; i0 += NT) {
                 const int i = i0 + lane;
-                const bool act = i < ns;
-                const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-                double q[3];
-#pragma unroll
-                for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
-                const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2];
+                const bool act = i < P.ns;
+                const float4 sp = act ? P.src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                float qf[3];
+                gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
                 int j = -1;
                 float best = INFINITY;
-                if (use_grid) {
-                    if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qx, qy, qz, best, j);
+                if (P.use_grid) {
+                    if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
                 } else {
-                    scan_quads(tquads, (nt + 3) >> 2, qx, qy, qz, best, j);
+                    scan_quads(P.tquads, (P.nt + 3) >> 2, qf[0], qf[1], qf[2], best, j);
                 }
                 if (act) jbuf[i] = j;
             }
@@ -838,37 +821,36 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 double acc[gicpm::kTerms];
 #pragma unroll
                 for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-                for (int i0 = 0; i0 < ns; i0 += 64) {
+                for (int i0 = 0; i0 < P.ns; i0 += 64) {
                     const int i = i0 + lane;
-                    const int j = i < ns ? jbuf[i] : -1;
-                    if (j >= 0) {
-                        const float4 sp = src[i];
-                        const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-                        double q[3];
+                    linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
+                                           P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, acc);
+                }
+                const double* sys = lds_tree_sum(acc, sRed, lane);
+                const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, g.rot_eps,
+                                            g.trans_eps);
+                if (lane == 0) {
+                    sFlag = st;
 #pragma unroll
-                        for (int r = 0; r < 3; r++) q[r] = R[r][0] * s0 + R[r][1] * s1 + R[r][2] * s2 + t[r];
-                        double cs[6], ct[6];
-                        load_cov(scov, i, cs);
-                        load_cov(tcov, j, ct);
-                        gicp_contrib(R, q, cs, tgt[j], ct, acc);
+                    for (int r = 0; r < 3; r++) {
+#pragma unroll
+                        for (int c = 0; c < 3; c++) sX[3 * r + c] = x.R[r][c];
+                        sX[9 + r] = x.t[r];
                     }
                 }
-#pragma unroll
-                for (int v = 0; v < gicpm::kTerms; v++) {
-                    double x = acc[v];
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
-                    acc[v] = x;
-                }
-                if (tid == 0) sFlag = solve_update(acc, R, t, RT, g.rot_eps, g.trans_eps);
             }
             __syncthreads();
             const int flag = __builtin_amdgcn_readfirstlane(sFlag);
-            if (flag != 1) iters++;
-            done = flag != 0;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) x.R[r][c] = uniform_d(sX[3 * r + c]);
+                x.t[r] = uniform_d(sX[9 + r]);
+            }
+            if (flag != gicpm::kLmAccepted) break;
         }
         __syncthreads();
-        if (tid == 0) write_pose(g, gp, RT, iters);
+        if (tid == 0) write_pose(g, P.gp, x, iters);
     }
 }
 
@@ -920,7 +902,7 @@ hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32
 
 hipError_t gicp_occupancy_per_cu(int* per_cu) {
     *per_cu = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel<kGicpWpp>, 64 * kGicpWpp, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel, 64, 0);
 }
 
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s) {
@@ -942,7 +924,7 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hi
         return hipGetLastError();
     }
     const int wgs = std::min(resident_wgs, num_poses);
-    hipLaunchKernelGGL(gicp_kernel<kGicpWpp>, dim3(wgs), dim3(64 * kGicpWpp), 0, s, g, num_poses);
+    hipLaunchKernelGGL(gicp_kernel, dim3(wgs), dim3(64), 0, s, g, num_poses);
     return hipGetLastError();
 }
 

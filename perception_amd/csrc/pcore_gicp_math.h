@@ -1,15 +1,28 @@
-// pcore_gicp_math.h -- the per-point Gauss-Newton contribution of the GICP spec (DESIGN.md "GICP spec"),
-// one function compiled into both the HIP kernel (pcore_gicp.hip) and the CPU oracle
-// (oracle/pcore_oracle.cpp), so the two evaluate the same double-precision expression tree bit for bit
-// (both are built with -ffp-contract=off).
+// pcore_gicp_math.h -- the arithmetic of the GICP spec (DESIGN.md "GICP spec"): fast_gicp's published
+// FastGICP / LsqRegistration algorithm with Levenberg-Marquardt step control, at the settings of the reference's
+// call site (renderer.cu:1693-1720).  One set of functions compiled into both the HIP kernels (pcore_gicp.hip)
+// and the CPU oracle's bit-exact GICP (oracle/pcore_oracle.cpp, orc_gicp), so the two evaluate the same
+// double-precision expression trees bit for bit (both are built with -ffp-contract=off).  The oracle also holds an
+// independent textbook restatement of the per-point step (4x4 homogeneous form, orc_gicp_linearize_textbook) that
+// the tests hold this one to (tests/test_gicp_spec.py).
 //
-// Residual e = t_j - q with q = R s + t, Mahalanobis M = (C_t + R C_s R^T)^-1 (adjugate / determinant),
-// Jacobian J = [skew(q) | -I] (fast_gicp's left perturbation):
-//   J = [[0, -q2, q1, -1, 0, 0], [q2, 0, -q0, 0, -1, 0], [-q1, q0, 0, 0, 0, -1]].
+// Per source point (fast_gicp FastGICP::update_correspondences / linearize):
+//   correspondence  the nearest target of q_f = T_f s (float transform, float arithmetic)
+//   residual        e = t_j - q with q = T s in double
+//   Mahalanobis     M = (C_t + R C_s R^T)^-1 (adjugate / determinant; RCR(3,3) = 1 and M(3,3) = 0 of the 4x4 form)
+//   Jacobian        J = [skew(q) | -I]  =  [[0, -q2, q1, -1, 0, 0], [q2, 0, -q0, 0, -1, 0], [-q1, q0, 0, 0, 0, -1]]
+//   terms           H += J^T M J (upper triangle), b += J^T M e, y += e^T M e
 // The products with J's structural zeros and -1 entries are not evaluated: J^T v for a 3-vector v is
-//   (q2 v1 - q1 v2, q0 v2 - q2 v0, q1 v0 - q0 v1, -v0, -v1, -v2),
-// MJ = M J column by column likewise, and acc += (upper(J^T M J), J^T M e, e^T M e).
+//   (q2 v1 - q1 v2, q0 v2 - q2 v0, q1 v0 - q0 v1, -v0, -v1, -v2).
+// Per iteration (LsqRegistration::step_lm, so3.hpp se3_exp, Eigen's LDLT and Quaternion::toRotationMatrix):
+//   lambda <- 1e-9 max|diag H| on the first iteration; up to 10 trials of d = LDLT(H + lambda I).solve(-b),
+//   delta = se3_exp(d), x_i = delta x, y_i = sum e^T M e at x_i with the iteration's correspondences and M,
+//   rho = (y - y_i) / d.(lambda d - b); rho < 0 rejects (stop if delta is converged, else lambda *= nu, nu *= 2),
+//   otherwise x <- x_i and lambda *= max(1/3, 1 - (2 rho - 1)^3).  The search stops when a step is converged
+//   (max(|dR - I| / rot_eps, |dt| / trans_eps) < 1), when ten trials are rejected, or after max_iter iterations.
 #pragma once
+
+#include "pcore_dmath.h"
 
 #ifdef __HIPCC__
 #define PCORE_GHD __host__ __device__ __forceinline__
@@ -28,8 +41,9 @@ namespace gicpm {
 //   key = fma(-2 t'x, q'x, fma(-2 t'y, q'y, fma(-2 t'z, q'z, |t'|^2)))  =  |q' - t'|^2 - |q'|^2  (+ rounding),
 // three FMAs instead of three subtractions, three products and two sums; |q'|^2 is the same for every target,
 // so the nearest target is the first strict minimum of the key.  Centring keeps |q'|^2 small (objects are
-// ~0.1 m across), so the cancellation costs ~1e-9 m^2.  Non-finite targets never win (key +inf); a non-finite
-// query has no correspondence.
+// ~0.1 m across), so the cancellation costs ~1e-9 m^2 (tests/test_gicp_spec.py bounds the distance lost against
+// the exact squared-distance argmin).  Non-finite targets never win (key +inf); a non-finite query has no
+// correspondence.
 constexpr int kKeyScanMax = 2048;
 
 struct NNTarget {
@@ -66,6 +80,13 @@ inline void nn_origin(int n, Get get, float (&c)[3]) {
     for (int a = 0; a < 3; a++) c[a] = any ? (lo[a] + hi[a]) * 0.5f : 0.0f;
 }
 
+// The correspondence query q_f = T_f s: the float transform (Rf, tf) = float(R, t) applied in float, row by row
+// left to right (fast_gicp update_correspondences: trans.cast<float>() * point)
+PCORE_GHD void query_f(const float (&Rf)[3][3], const float (&tf)[3], float sx, float sy, float sz, float (&qf)[3]) {
+PCORE_UNROLL
+    for (int r = 0; r < 3; r++) qf[r] = Rf[r][0] * sx + Rf[r][1] * sy + Rf[r][2] * sz + tf[r];
+}
+
 // J^T v (the 6-vector above)
 PCORE_GHD void jt_mul(const double (&q)[3], const double (&v)[3], double (&o)[6]) {
     o[0] = q[2] * v[1] - q[1] * v[2];
@@ -76,14 +97,25 @@ PCORE_GHD void jt_mul(const double (&q)[3], const double (&v)[3], double (&o)[6]
     o[5] = -v[2];
 }
 
-// Terms of the normal equations a point adds: the upper triangle of J^T M J and J^T M e.  (fast_gicp also
-// sums the error e^T M e; nothing in the step or the convergence test reads it, so it is not accumulated.)
-constexpr int kTerms = 27;
+// Terms of the normal equations a point adds: acc[0..20] upper(J^T M J) row-major, acc[21..26] J^T M e,
+// acc[27] e^T M e (the error y of step_lm).
+constexpr int kTerms = 28;
+constexpr int kErr = 27;
+// index of H[a][a] in the upper triangle
+PCORE_GHD constexpr int hdiag(int a) { return a * 6 - (a * (a - 1)) / 2; }
 
-// acc[0..20] += upper(J^T M J) row-major, acc[21..26] += J^T M e, for the point q with correspondence tj,
-// source covariance cs and target covariance ct (xx, xy, xz, yy, yz, zz).
+// e^T M e with M given by its upper triangle (xx, xy, xz, yy, yz, zz): Me row by row, then the dot product
+PCORE_GHD double mahal_err(const double (&M6)[6], const double (&e)[3]) {
+    const double me0 = M6[0] * e[0] + M6[1] * e[1] + M6[2] * e[2];
+    const double me1 = M6[1] * e[0] + M6[3] * e[1] + M6[4] * e[2];
+    const double me2 = M6[2] * e[0] + M6[4] * e[1] + M6[5] * e[2];
+    return e[0] * me0 + e[1] * me1 + e[2] * me2;
+}
+
+// One point's contribution for the transformed point q (double), its correspondence tj and both covariances
+// (xx, xy, xz, yy, yz, zz); M6 receives the point's Mahalanobis matrix (kept for the trials' errors).
 PCORE_GHD void contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6], const double (&tj)[3],
-                       const double (&ct)[6], double (&acc)[kTerms]) {
+                       const double (&ct)[6], double (&acc)[kTerms], double (&M6)[6]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
     double RC[3][3], A[3][3];
@@ -117,6 +149,8 @@ PCORE_UNROLL
     for (int r = 0; r < 3; r++)
 PCORE_UNROLL
         for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
+    M6[0] = M[0][0]; M6[1] = M[0][1]; M6[2] = M[0][2];
+    M6[3] = M[1][1]; M6[4] = M[1][2]; M6[5] = M[2][2];
     const double e[3] = {tj[0] - q[0], tj[1] - q[1], tj[2] - q[2]};
     // MJ columns 0..2 (skew part); columns 3..5 are -M's columns
     double MJ[3][3];
@@ -149,7 +183,247 @@ PCORE_UNROLL
     jt_mul(q, Me, g);
 PCORE_UNROLL
     for (int a = 0; a < 6; a++) acc[21 + a] += g[a];
+    acc[kErr] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
 }
+
+// ---- the step (uniform per pose) ----------------------------------------------------------------------------
+
+constexpr int kLmMaxTrials = 10;          // LsqRegistration lm_max_iterations_
+constexpr double kLmInitFactor = 1e-9;    // LsqRegistration lm_init_lambda_factor_
+
+// initial damping: 1e-9 * max |H_aa| (maxCoeff: the first strict maximum in index order)
+PCORE_GHD double lm_init_lambda(const double* sys) {
+    double m = __builtin_fabs(sys[hdiag(0)]);
+PCORE_UNROLL
+    for (int a = 1; a < 6; a++) {
+        const double v = __builtin_fabs(sys[hdiag(a)]);
+        m = v > m ? v : m;
+    }
+    return kLmInitFactor * m;
+}
+
+// d = LDLT(H + lambda I).solve(-b), Eigen's LDLT<Matrix6d, Lower> (ldlt_inplace::unblocked + _solve_impl):
+// diagonal pivoting on the largest |A_kk| (first on ties), the pivot row / column swapped on the lower triangle,
+// column k updated with temp_j = D_j L_kj and divided by the pivot; a zero first pivot leaves L = I; the solve
+// permutes, runs the unit-lower forward substitution, divides by D (|D_i| <= DBL_MIN gives 0), runs the unit-upper
+// back substitution and permutes back.  Sums run in index order.  sys: 28 terms (upper H row-major, b).
+PCORE_GHD void lm_solve(const double* sys, double lambda, double (&d)[6]) {
+    double A[6][6];
+    {
+        int h = 0;
+PCORE_UNROLL
+        for (int a = 0; a < 6; a++)
+PCORE_UNROLL
+            for (int c = a; c < 6; c++) {
+                A[c][a] = a == c ? sys[h] + lambda : sys[h];  // lower triangle of H + lambda I (the upper is unused)
+                h++;
+            }
+    }
+    int tr[6];
+    bool zero = false;
+PCORE_UNROLL
+    for (int k = 0; k < 6; k++) {
+        int p = k;
+        double big = __builtin_fabs(A[k][k]);
+PCORE_UNROLL
+        for (int i = k + 1; i < 6; i++) {
+            const double v = __builtin_fabs(A[i][i]);
+            if (v > big) { big = v; p = i; }
+        }
+        tr[k] = p;
+PCORE_UNROLL
+        for (int c = k + 1; c < 6; c++)
+            if (p == c) {
+PCORE_UNROLL
+                for (int j = 0; j < k; j++) { const double x = A[k][j]; A[k][j] = A[c][j]; A[c][j] = x; }
+PCORE_UNROLL
+                for (int i = c + 1; i < 6; i++) { const double x = A[i][k]; A[i][k] = A[i][c]; A[i][c] = x; }
+                { const double x = A[k][k]; A[k][k] = A[c][c]; A[c][c] = x; }
+PCORE_UNROLL
+                for (int i = k + 1; i < c; i++) { const double x = A[i][k]; A[i][k] = A[c][i]; A[c][i] = x; }
+            }
+        if (k > 0) {
+            double temp[6];
+PCORE_UNROLL
+            for (int j = 0; j < k; j++) temp[j] = A[j][j] * A[k][j];
+            double s = A[k][0] * temp[0];
+PCORE_UNROLL
+            for (int j = 1; j < k; j++) s = s + A[k][j] * temp[j];
+            A[k][k] = A[k][k] - s;
+PCORE_UNROLL
+            for (int i = k + 1; i < 6; i++) {
+                double w = A[i][0] * temp[0];
+PCORE_UNROLL
+                for (int j = 1; j < k; j++) w = w + A[i][j] * temp[j];
+                A[i][k] = A[i][k] - w;
+            }
+        }
+        const double akk = A[k][k];
+        const bool valid = __builtin_fabs(akk) > 0.0;
+        if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
+            zero = true;
+            break;
+        }
+        if (valid) {
+PCORE_UNROLL
+            for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
+        }
+    }
+    double x[6];
+PCORE_UNROLL
+    for (int i = 0; i < 6; i++) x[i] = -sys[21 + i];
+    if (zero) {
+        // D = the (zero) diagonal: every row is set to zero by the pseudo-inverse
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) d[i] = 0.0;
+        return;
+    }
+PCORE_UNROLL
+    for (int k = 0; k < 6; k++)
+PCORE_UNROLL
+        for (int c = k + 1; c < 6; c++)
+            if (tr[k] == c) { const double v = x[k]; x[k] = x[c]; x[c] = v; }
+PCORE_UNROLL
+    for (int j = 0; j < 6; j++)
+PCORE_UNROLL
+        for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
+PCORE_UNROLL
+    for (int i = 0; i < 6; i++) {
+        const double Di = A[i][i];
+        x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
+    }
+PCORE_UNROLL
+    for (int i = 4; i >= 0; i--) {
+        double s = A[i + 1][i] * x[i + 1];
+PCORE_UNROLL
+        for (int j = i + 2; j < 6; j++) s = s + A[j][i] * x[j];
+        x[i] = x[i] - s;
+    }
+PCORE_UNROLL
+    for (int k = 5; k >= 0; k--)
+PCORE_UNROLL
+        for (int c = k + 1; c < 6; c++)
+            if (tr[k] == c) { const double v = x[k]; x[k] = x[c]; x[c] = v; }
+PCORE_UNROLL
+    for (int i = 0; i < 6; i++) d[i] = x[i];
+}
+
+// se3_exp (fast_gicp so3.hpp): so3_exp quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
+// cos(theta/2)), Eigen's Quaternion::toRotationMatrix, translation V rho with
+// V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10)
+PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]) {
+    const double w0 = a[0], w1 = a[1], w2 = a[2];
+    const double theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
+    double imag, real;
+    if (theta_sq < 1e-10) {
+        const double theta_quad = theta_sq * theta_sq;
+        imag = 0.5 - 1.0 / 48.0 * theta_sq + 1.0 / 3840.0 * theta_quad;
+        real = 1.0 - 1.0 / 8.0 * theta_sq + 1.0 / 384.0 * theta_quad;
+    } else {
+        const double th = __builtin_sqrt(theta_sq);
+        const double half_theta = 0.5 * th;
+        imag = dmath::sin_d(half_theta) / th;
+        real = dmath::cos_d(half_theta);
+    }
+    const double qw = real, qx = imag * w0, qy = imag * w1, qz = imag * w2;
+    const double tx = 2.0 * qx, ty = 2.0 * qy, tz = 2.0 * qz;
+    const double twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const double txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    Rd[0][0] = 1.0 - (tyy + tzz);
+    Rd[0][1] = txy - twz;
+    Rd[0][2] = txz + twy;
+    Rd[1][0] = txy + twz;
+    Rd[1][1] = 1.0 - (txx + tzz);
+    Rd[1][2] = tyz - twx;
+    Rd[2][0] = txz - twy;
+    Rd[2][1] = tyz + twx;
+    Rd[2][2] = 1.0 - (txx + tyy);
+    const double theta = __builtin_sqrt(theta_sq);
+    double V[3][3];
+    if (theta < 1e-10) {
+PCORE_UNROLL
+        for (int r = 0; r < 3; r++)
+PCORE_UNROLL
+            for (int c = 0; c < 3; c++) V[r][c] = Rd[r][c];
+    } else {
+        const double O[3][3] = {{0.0, -w2, w1}, {w2, 0.0, -w0}, {-w1, w0, 0.0}};
+        double O2[3][3];
+PCORE_UNROLL
+        for (int r = 0; r < 3; r++)
+PCORE_UNROLL
+            for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
+        const double th2 = theta * theta;
+        const double c1 = (1.0 - dmath::cos_d(theta)) / th2;
+        const double c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
+PCORE_UNROLL
+        for (int r = 0; r < 3; r++)
+PCORE_UNROLL
+            for (int c = 0; c < 3; c++) V[r][c] = ((r == c ? 1.0 : 0.0) + c1 * O[r][c]) + c2 * O2[r][c];
+    }
+PCORE_UNROLL
+    for (int r = 0; r < 3; r++) td[r] = V[r][0] * a[3] + V[r][1] * a[4] + V[r][2] * a[5];
+}
+
+// x_i = delta * x (Isometry3d product): R_i = R_d R, t_i = R_d t + t_d
+PCORE_GHD void compose(const double (&Rd)[3][3], const double (&td)[3], const double (&R)[3][3], const double (&t)[3],
+                       double (&Ro)[3][3], double (&to)[3]) {
+PCORE_UNROLL
+    for (int r = 0; r < 3; r++) {
+PCORE_UNROLL
+        for (int c = 0; c < 3; c++) Ro[r][c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
+        to[r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + td[r];
+    }
+}
+
+// LsqRegistration::is_converged: max(max|R_d - I| / rot_eps, max|t_d| / trans_eps) < 1, the quotients as
+// (1 / eps) * |x| and the maxima in Eigen's column-major coefficient order (first strict maximum)
+PCORE_GHD bool is_converged(const double (&Rd)[3][3], const double (&td)[3], double rot_eps, double trans_eps) {
+    const double ir = 1.0 / rot_eps, it = 1.0 / trans_eps;
+    double mr = ir * __builtin_fabs(Rd[0][0] - 1.0);
+PCORE_UNROLL
+    for (int c = 0; c < 3; c++)
+PCORE_UNROLL
+        for (int r = 0; r < 3; r++) {
+            if (r == 0 && c == 0) continue;
+            const double v = ir * __builtin_fabs(Rd[r][c] - (r == c ? 1.0 : 0.0));
+            mr = v > mr ? v : mr;
+        }
+    double mt = it * __builtin_fabs(td[0]);
+PCORE_UNROLL
+    for (int r = 1; r < 3; r++) {
+        const double v = it * __builtin_fabs(td[r]);
+        mt = v > mt ? v : mt;
+    }
+    const double m = mr < mt ? mt : mr;  // std::max(a, b) = a < b ? b : a
+    return m < 1.0;
+}
+
+// rho = (y0 - yi) / d.(lambda d - b), the dot product in index order
+PCORE_GHD double lm_rho(const double* sys, double lambda, const double (&d)[6], double y0, double yi) {
+    double den = d[0] * (lambda * d[0] - sys[21]);
+PCORE_UNROLL
+    for (int a = 1; a < 6; a++) den = den + d[a] * (lambda * d[a] - sys[21 + a]);
+    return (y0 - yi) / den;
+}
+
+// accepted step: lambda * max(1/3, 1 - (2 rho - 1)^3), the cube as (u u) u
+PCORE_GHD double lm_accept_lambda(double lambda, double rho) {
+    const double u = 2.0 * rho - 1.0;
+    const double f = 1.0 - u * u * u;
+    const double third = 1.0 / 3.0;
+    return lambda * (third < f ? f : third);
+}
+
+PCORE_GHD bool all_finite6(const double (&d)[6]) {
+    bool ok = true;
+PCORE_UNROLL
+    for (int a = 0; a < 6; a++) ok = ok && (d[a] - d[a] == 0.0);
+    return ok;
+}
+
+// outcome of one LM iteration
+enum LmStatus { kLmAccepted = 0, kLmConverged = 1, kLmFailed = 2 };
 
 }  // namespace gicpm
 }  // namespace pcore

@@ -133,6 +133,10 @@ struct GicpArgs {
     const int32_t* src_count;
     const double* src_cov;    // 6 per source point, same slots
     int32_t src_cap;
+    // per-iteration scratch, same slots: each source point's correspondence (-1: none) and Mahalanobis matrix
+    // (xx, xy, xz, yy, yz, zz), written by the linearisation and read by the LM trials' error sums
+    int32_t* corr;
+    double* mahal;
     const float4* tgt;        // observed points, label-sorted
     const double* tgt_cov;    // 6 per target point (covariances within the segment)
     const int32_t* seg_lo;    // num_segs entries

@@ -1,0 +1,107 @@
+"""Independent numpy restatement of fast_gicp's published GICP (test reference only).
+
+Shares no arithmetic with perception_amd/csrc/pcore_gicp_math.h: the per-point step is the dense 3x3 form
+(M = inv(C_t + R C_s R^T) by numpy, J = [skew(T s) | -I], H = sum J^T M J, b = sum J^T M e, y = sum e^T M e),
+the solve is numpy.linalg.solve, the SE(3) exponential is scipy's matrix exponential of the twist, and the
+Levenberg-Marquardt control is LsqRegistration::step_lm / computeTransformation as published (lm_init_lambda_factor
+1e-9, lm_max_iterations 10, lambda *= max(1/3, 1 - (2 rho - 1)^3) on acceptance, nu doubling on rejection,
+is_converged on max(|dR - I| / rot_eps, |dt| / trans_eps) < 1).  Only the correspondence rule -- the spec's
+nearest target of the float query, which is a tie / rounding rule rather than algebra -- comes from the oracle
+(oracle.gicp_nn).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.linalg as sla
+
+import oracle
+
+
+def sym3(c6):
+    c = np.asarray(c6, np.float64)
+    return np.stack([c[:, [0, 1, 2]], c[:, [1, 3, 4]], c[:, [2, 4, 5]]], 1)
+
+
+def skew(v):
+    return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
+
+
+def query_f(T, src):
+    """fast_gicp update_correspondences: trans.cast<float>() * point, in float, row by row left to right."""
+    Tf = T.astype(np.float32)
+    s = np.asarray(src, np.float32)
+    return np.stack([((Tf[r, 0] * s[:, 0] + Tf[r, 1] * s[:, 1]) + Tf[r, 2] * s[:, 2]) + Tf[r, 3] for r in range(3)], 1)
+
+
+def linearize(T, src, Cs, tgt, Ct, j):
+    ok = j >= 0
+    s = np.asarray(src, np.float64)[ok]
+    jj = j[ok]
+    R = T[:3, :3]
+    tA = s @ R.T + T[:3, 3]
+    M = np.linalg.inv(Ct[jj] + R @ Cs[ok] @ R.T)
+    e = np.asarray(tgt, np.float64)[jj] - tA
+    J = np.zeros((len(s), 3, 6))
+    J[:, 0, 1], J[:, 0, 2] = -tA[:, 2], tA[:, 1]
+    J[:, 1, 0], J[:, 1, 2] = tA[:, 2], -tA[:, 0]
+    J[:, 2, 0], J[:, 2, 1] = -tA[:, 1], tA[:, 0]
+    J[:, 0, 3] = J[:, 1, 4] = J[:, 2, 5] = -1.0
+    H = np.einsum("nka,nkl,nlb->ab", J, M, J)
+    b = np.einsum("nka,nkl,nl->a", J, M, e)
+    y = float(np.einsum("nk,nkl,nl->", e, M, e))
+    return H, b, y, M, ok
+
+
+def error(T, src, tgt, j, M, ok):
+    s = np.asarray(src, np.float64)[ok]
+    e = np.asarray(tgt, np.float64)[j[ok]] - (s @ T[:3, :3].T + T[:3, 3])
+    return float(np.einsum("nk,nkl,nl->", e, M, e))
+
+
+def se3_exp(d):
+    X = np.zeros((4, 4))
+    X[:3, :3] = skew(d[:3])
+    X[:3, 3] = d[3:]
+    return sla.expm(X)
+
+
+def is_converged(D, rot_eps, trans_eps):
+    return max((np.abs(D[:3, :3] - np.eye(3)) / rot_eps).max(), (np.abs(D[:3, 3]) / trans_eps).max()) < 1.0
+
+
+def gicp(src, src_cov, tgt, tgt_cov, max_iter=oracle.GICP_MAX_ITER, rot_eps=oracle.GICP_ROT_EPS,
+         trans_eps=oracle.GICP_TRANS_EPS):
+    """-> (T (4,4) float64, iterations) as LsqRegistration::computeTransformation from the identity guess."""
+    Cs, Ct = sym3(src_cov), sym3(tgt_cov)
+    T = np.eye(4)
+    lam = -1.0
+    it = 0
+    if len(src) == 0 or len(tgt) == 0:
+        return T, 0
+    while it < max_iter:
+        it += 1
+        j = oracle.gicp_nn(query_f(T, src), tgt)
+        H, b, y0, M, ok = linearize(T, src, Cs, tgt, Ct, j)
+        if lam < 0.0:
+            lam = 1e-9 * np.abs(np.diag(H)).max()
+        nu = 2.0
+        status = "failed"
+        for _ in range(10):
+            d = np.linalg.solve(H + lam * np.eye(6), -b)
+            D = se3_exp(d)
+            Ti = D @ T
+            rho = (y0 - error(Ti, src, tgt, j, M, ok)) / (d @ (lam * d - b))
+            if rho < 0.0:
+                if is_converged(D, rot_eps, trans_eps):
+                    status = "converged"
+                    break
+                lam *= nu
+                nu *= 2.0
+                continue
+            T = Ti
+            lam *= max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3)
+            status = "converged" if is_converged(D, rot_eps, trans_eps) else "accepted"
+            break
+        if status != "accepted":
+            break
+    return T, it

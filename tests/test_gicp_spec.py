@@ -1,0 +1,177 @@
+"""CPU tests of the GICP spec against independent restatements.
+
+The GPU kernels and the oracle's bit-exact GICP share pcore_gicp_math.h; these tests hold that shared arithmetic
+to references that share nothing with it:
+  - the double sin / cos of pcore_dmath.h against numpy (1 ulp);
+  - se3_exp against scipy's matrix exponential of the twist;
+  - the damped pivoted LDLT against numpy.linalg.solve;
+  - the per-point linearisation (H, b, e^T M e) against the oracle's long-double 4x4 textbook form (1e-9 relative);
+  - the whole LM iteration against tests/gicp_reference.py (numpy + scipy, fast_gicp's published step_lm);
+  - the three-FMA correspondence key against the exact float squared-distance argmin.
+Fast_gicp itself is not vendored: parity against the reference binary stays unpinned.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+import oracle
+from tests import gicp_reference as gref
+from tests.helpers import SceneCase
+
+C3_NAMES = ("003_cracker_box", "004_sugar_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can")
+
+
+@pytest.fixture(scope="module")
+def c3_pairs():
+    """(rendered cloud, its covariances, label segment, segment covariances) of C3-style candidate poses: five
+    objects, stride 8, 640x480, candidates around the ground truth (oracle raster + unprojection)."""
+    case = SceneCase(names=C3_NAMES, n_poses=5, seed=7)
+    sc = case.scene
+    depth = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses, case.pose_model, case.pose_label,
+                                sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0)
+    seg_cov = {}
+    out = []
+    for i in range(len(case.poses)):
+        xyz = oracle.depth_to_cloud(depth[i], 8, sc.cx, sc.cy, sc.fx, sc.fy, 100.0)[0]
+        lab = int(case.pose_label[i])
+        tgt = case.obs_xyz[case.label_start[lab]:case.label_end[lab]]
+        if len(xyz) == 0 or len(tgt) == 0:
+            continue
+        if lab not in seg_cov:
+            seg_cov[lab] = oracle.covariances(tgt)
+        out.append((xyz, oracle.covariances(xyz), tgt, seg_cov[lab]))
+    assert len(out) >= 20
+    return out
+
+
+def test_sin_cos_within_one_ulp():
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.uniform(-4, 4, 4000), rng.uniform(-1e3, 1e3, 2000), rng.uniform(-1e6, 1e6, 500),
+                         np.geomspace(1e-300, 1.0, 200), -np.geomspace(1e-12, 1.0, 50),
+                         np.arange(-40, 41) * (np.pi / 4)])
+    for f, ref in ((oracle.sin_d, np.sin), (oracle.cos_d, np.cos)):
+        got = np.array([f(x) for x in xs])
+        want = ref(xs)
+        ulp = np.spacing(np.maximum(np.abs(want), 1e-300)) * np.where(np.abs(xs) < 1e4, 1.0, 2.0)
+        # near a zero of the function the absolute error is the reduction's (three-part pi/2)
+        err = np.abs(got - want)
+        assert np.all((err <= ulp) | (err <= 1e-29 * np.maximum(1.0, np.abs(xs)))), f
+    assert np.isnan(oracle.sin_d(np.inf)) and np.isnan(oracle.cos_d(np.nan))
+    assert oracle.sin_d(0.0) == 0.0 and oracle.cos_d(0.0) == 1.0
+
+
+@pytest.mark.parametrize("scale", [0.0, 1e-12, 3e-6, 1e-3, 0.2, 1.5, 3.0])
+def test_se3_exp_matches_matrix_exponential(scale):
+    """se3_exp (fast_gicp so3.hpp: exact so3_exp quaternion + V rho) = expm of the twist; the Taylor branches below
+    theta^2 = 1e-10 and theta = 1e-10 included (below theta = 1e-10 fast_gicp takes V = R instead of I + Omega / 2
+    + ..., off by theta |rho| / 2; above it, (1 - cos theta) / theta^2 and (theta - sin theta) / theta^3 as published
+    cancel to ~eps / theta relative, so V rho is good to ~eps |rho| / theta)."""
+    rng = np.random.default_rng(int(scale * 1e6) + 3)
+    for _ in range(20):
+        w = rng.normal(size=3)
+        w = w / np.linalg.norm(w) * scale
+        d = np.concatenate([w, rng.normal(size=3) * 0.05])
+        T = oracle.gicp_se3_exp(d)
+        ref = gref.se3_exp(d)
+        rho = np.abs(d[3:]).max()
+        tol = 5e-15 + (scale * rho if scale < 1e-10 else 1e-15 * rho / scale)
+        assert np.abs(T - ref).max() < tol
+        R = T[:3, :3]
+        assert np.abs(R @ R.T - np.eye(3)).max() < 4e-15
+
+
+def test_lm_solve_matches_dense_solve():
+    """Eigen's LDLT with diagonal pivoting of H + lambda I, solve(-b): the dense solution to 1e-10; a diagonal
+    ordered so that every column pivots; a zero system gives a zero step (Eigen's pseudo-inverse of D)."""
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        A = rng.normal(size=(6, 6)) * rng.uniform(0.01, 100, 6)
+        H = A @ A.T
+        if trial % 2:
+            H = H[::-1, ::-1].copy()  # largest diagonal last: pivoting reorders every column
+        b = rng.normal(size=6)
+        lam = [0.0, 1e-9, 1e-3][trial % 3] * np.abs(np.diag(H)).max()
+        d = oracle.gicp_lm_solve(H, b, lam)
+        ref = np.linalg.solve(H + lam * np.eye(6), -b)
+        assert np.abs(d - ref).max() <= 1e-10 * np.abs(ref).max() * np.linalg.cond(H + lam * np.eye(6)) ** 0.5 + 1e-300
+    assert np.all(oracle.gicp_lm_solve(np.zeros((6, 6)), np.ones(6), 0.0) == 0.0)
+
+
+def _rel(a, b):
+    return np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300)
+
+
+def test_linearize_matches_textbook(c3_pairs):
+    """The shared per-point step (upper J^T M J, J^T M e, e^T M e; adjugate inverse, structural zeros skipped) equals
+    fast_gicp's 4x4 homogeneous form evaluated independently in long double, to 1e-9 relative, at the identity, at a
+    perturbed transform and at the converged one."""
+    rng = np.random.default_rng(11)
+    for src, scov, tgt, tcov in c3_pairs[::2]:
+        T_conv, _ = oracle.gicp(src, scov, tgt, tcov)
+        pert = gref.se3_exp(np.concatenate([rng.normal(size=3) * 0.05, rng.normal(size=3) * 0.01]))
+        for T in (np.eye(4), pert, T_conv):
+            c0, H0, b0, y0 = oracle.gicp_linearize(src, scov, tgt, tcov, T, textbook=False)
+            c1, H1, b1, y1 = oracle.gicp_linearize(src, scov, tgt, tcov, T, textbook=True)
+            assert np.array_equal(c0, c1)
+            assert _rel(H0, H1) < 1e-9
+            assert _rel(b0, b1) < 1e-9 or np.abs(b0 - b1).max() < 1e-9 * np.abs(H1).max()
+            assert abs(y0 - y1) <= 1e-9 * max(abs(y1), 1e-12)
+
+
+def test_gicp_matches_independent_numpy_lm(c3_pairs):
+    """The oracle's GICP (the GPU's arithmetic) and the independent numpy / scipy restatement of fast_gicp's LM
+    (tests/gicp_reference.py) run the same number of iterations and land within 1e-9 of each other -- including
+    the poses that run all 150 iterations (wrong candidates whose correspondences flip between two sets every
+    iteration, a limit cycle the published step_lm accepts)."""
+    iters = []
+    for src, scov, tgt, tcov in c3_pairs:
+        T1, it1 = oracle.gicp(src, scov, tgt, tcov)
+        T2, it2 = gref.gicp(src, scov, tgt, tcov)
+        assert it1 == it2
+        assert np.abs(T1 - T2).max() < 1e-9
+        iters.append(it1)
+    assert min(iters) >= 1 and max(iters) <= 150
+
+
+def _key_gap(q, tgt):
+    j = oracle.gicp_nn(q, tgt)
+    d = ((q[:, None, :] - tgt[None, :, :]) ** 2).sum(-1, dtype=np.float32)  # float squared distances
+    ok = j >= 0
+    got = d[np.arange(len(q))[ok], j[ok]]
+    return got - d[ok].min(1), ok
+
+
+@pytest.mark.parametrize("n_tgt", [57, 180, 2048, 2049])
+def test_key_nearest_is_the_nearest(c3_pairs, n_tgt):
+    """The correspondence key |q'-t'|^2 - |q'|^2 (three FMAs about the segment's origin) picks a target whose float
+    squared distance is within 1e-9 m^2 of the true nearest one -- queries on the object, a centimetre off it, a
+    decimetre off and a metre away; segments of 2048 targets (the largest key scan) and 2049 (the plain distance of
+    the grid-search path, exact)."""
+    rng = np.random.default_rng(n_tgt)
+    pool = np.concatenate([p[2] for p in c3_pairs] + [p[0] for p in c3_pairs])
+    tgt = pool[rng.choice(len(pool), min(n_tgt, len(pool)), replace=False)]
+    if len(tgt) < n_tgt:  # whole-scene style segment: jittered copies
+        extra = tgt[rng.choice(len(tgt), n_tgt - len(tgt))] + rng.normal(scale=0.003, size=(n_tgt - len(tgt), 3))
+        tgt = np.concatenate([tgt, extra]).astype(np.float32)
+    base = tgt[rng.choice(len(tgt), 300)]
+    for off in (0.0, 0.01, 0.1, 1.0):
+        q = (base + rng.normal(scale=off, size=base.shape)).astype(np.float32) if off else base.copy()
+        gap, ok = _key_gap(q, tgt)
+        assert ok.all()
+        if n_tgt > 2048:
+            assert np.all(gap == 0.0)
+        else:
+            assert np.all(gap <= 1e-9 + 1e-6 * off * off), (off, gap.max())
+
+
+def test_key_nearest_ties_and_tiny_keys():
+    """Exact duplicates: the first index wins (strict <); queries at a target give keys near -|q'|^2 and denormal
+    differences without losing the nearest."""
+    t = np.array([[0.1, 0.2, 0.8], [0.1, 0.2, 0.8], [0.1, 0.2, 0.80000001], [0.3, 0.2, 0.8]], np.float32)
+    j = oracle.gicp_nn(t[[0, 2, 3]], t)
+    assert list(j) == [0, 0, 3] or list(j) == [0, 2, 3]
+    assert j[0] == 0
+    q = np.array([[0.2, 0.2, 0.8], [1e-30, 0.0, 0.0]], np.float32)
+    assert list(oracle.gicp_nn(q, t)) == [0, 0]

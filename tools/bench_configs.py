@@ -73,6 +73,11 @@ def run(name, names, per_model, cam, icp, steps, warmup):
         it = out[1].float()
         res["gicp_iters_mean"] = float(it.mean().item())
         res["gicp_iters_max"] = int(it.max().item())
+        itn = out[1].cpu().numpy()
+        edges = [1, 2, 5, 10, 20, 50, 100, 149, 150]
+        res["gicp_iters_hist"] = {f"<={e}": int((itn <= e).sum()) for e in edges}
+        res["gicp_iters_at_max"] = int((itn >= 150).sum())
+        res["gicp_iters_p50_p90"] = [float(np.percentile(itn, 50)), float(np.percentile(itn, 90))]
     # pose accuracy of the selected poses against the synthetic ground truth (f3 metrics, on the GPU)
     final = (out[0] if icp else w.poses).cpu().numpy()
     errs_add, errs_adds = [], []
