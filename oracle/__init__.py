@@ -200,6 +200,9 @@ def _gicp_lib():
                                        c_float, _f32p, _f64p, c_int, _opt(_i32p), _opt(_i32p), c_int, _opt(_f32p),
                                        c_int, c_int, c_float, c_int, c_int, c_double, c_double, _f32p, _opt(_i32p),
                                        _f32p, _f32p, _f32p, c_int]
+        L.orc_gicp_trace.restype = c_int
+        L.orc_gicp_trace.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, _f64p,
+                                     _opt(_f64p)]
         L.orc_gicp_linearize.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, _f64p, c_int, _i32p, _f64p]
         L.orc_gicp_se3_exp.argtypes = [_f64p, _f64p]
         L.orc_gicp_lm_solve.argtypes = [_f64p, c_double, _f64p]
@@ -236,6 +239,19 @@ def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EP
                               _c(tgt_cov, np.float64).reshape(-1) if len(tgt) else z6, len(tgt), max_iter, rot_eps,
                               trans_eps, T)
     return T.reshape(4, 4), it
+
+
+def gicp_trace(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS):
+    """orc_gicp with its per-iteration trace: (T, iterations, trace (iterations, 16): R (9), t (3) after each
+    iteration, the lambda of its first trial, 0, 0, the LM status)."""
+    src = _c(src, np.float32).reshape(-1, 3)
+    tgt = _c(tgt, np.float32).reshape(-1, 3)
+    T = np.zeros(16, np.float64)
+    tr = np.zeros((max_iter, 16), np.float64)
+    it = _gicp_lib().orc_gicp_trace(src.reshape(-1), _c(src_cov, np.float64).reshape(-1), len(src), tgt.reshape(-1),
+                                    _c(tgt_cov, np.float64).reshape(-1), len(tgt), max_iter, rot_eps, trans_eps, T,
+                                    tr.reshape(-1))
+    return T.reshape(4, 4), it, tr[:it]
 
 
 def gicp_linearize(src, src_cov, tgt, tgt_cov, T, textbook=False):

@@ -598,12 +598,14 @@ void gicp_linearize_spec(const OXform& x, const float* src_xyz, const double* sr
 
 // One LM iteration (LsqRegistration::step_lm) on the reduced system, as the GPU's lm_iteration
 int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double& lambda, const float* src_xyz, int ns,
-                      const float* tgt_xyz, const int32_t* corr, const double* mah, double rot_eps, double trans_eps) {
+                      const float* tgt_xyz, const int32_t* corr, const double* mah, double rot_eps, double trans_eps,
+                      double* lambda_used) {
     namespace gm = pcore::gicpm;
     const double y0 = sys[gm::kErr];
     if (lambda < 0.0) lambda = gm::lm_init_lambda(sys);
     double nu = 2.0;
     std::vector<double> part(64);
+    *lambda_used = lambda;
     for (int trial = 0; trial < gm::kLmMaxTrials; trial++) {
         double d[6];
         gm::lm_solve(sys, lambda, d);
@@ -743,8 +745,11 @@ void orc_covariances(const float* xyz, int n, int k, double* out_cov6) {
     for (int i = 0; i < n; i++) covariance_one(xyz, n, i, k, out_cov6 + (size_t)6 * i);
 }
 
-int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov, int nt,
-             int max_iter, double rot_eps, double trans_eps, double* out_T) {
+// The spec's GICP with an optional per-iteration trace (max_iter x 16: R, t after the iteration, the lambda of its
+// first trial, 0, 0, the LM status).
+int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
+                   int nt, int max_iter, double rot_eps, double trans_eps, double* out_T, double* trace) {
+    namespace gm = pcore::gicpm;
     OXform x;
     for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) x.R[r][c] = r == c ? 1.0 : 0.0;
@@ -752,20 +757,30 @@ int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* t
     }
     int it = 0;
     if (ns > 0 && nt > 0) {
-        std::vector<pcore::gicpm::NNTarget> keys;
+        std::vector<gm::NNTarget> keys;
         float org[3];
         gicp_keys(tgt_xyz, nt, keys, org);
         std::vector<int32_t> corr(ns);
         std::vector<double> mah((size_t)6 * ns);
         double lambda = -1.0;
         for (it = 0; it < max_iter;) {
+            const int k = it;
             it++;
-            double sys[pcore::gicpm::kTerms];
+            double sys[gm::kTerms];
             gicp_linearize_spec(x, src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, keys.empty() ? nullptr : keys.data(),
                                 org, corr.data(), mah.data(), sys);
+            double lam_used;
             const int st = gicp_lm_iteration(sys, x, lambda, src_xyz, ns, tgt_xyz, corr.data(), mah.data(), rot_eps,
-                                             trans_eps);
-            if (st != pcore::gicpm::kLmAccepted) break;
+                                             trans_eps, &lam_used);
+            if (trace) {
+                double* tr = trace + (size_t)16 * k;
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++) tr[3 * r + c] = x.R[r][c];
+                    tr[9 + r] = x.t[r];
+                }
+                tr[12] = lam_used; tr[13] = 0.0; tr[14] = 0.0; tr[15] = st;
+            }
+            if (st != gm::kLmAccepted) break;
         }
     }
     for (int r = 0; r < 3; r++) {
@@ -774,6 +789,11 @@ int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* t
     }
     out_T[12] = 0.0; out_T[13] = 0.0; out_T[14] = 0.0; out_T[15] = 1.0;
     return it;
+}
+
+int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov, int nt,
+             int max_iter, double rot_eps, double trans_eps, double* out_T) {
+    return orc_gicp_trace(src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, max_iter, rot_eps, trans_eps, out_T, nullptr);
 }
 
 // The linearisation at T (double 4x4 row-major) two ways, on the spec's correspondences (out_corr, ns):

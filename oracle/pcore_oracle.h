@@ -110,6 +110,11 @@ void orc_covariances(const float* xyz, int n, int k, double* out_cov6);
 int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
              int nt, int max_iter, double rot_eps, double trans_eps, double* out_T);
 
+/* orc_gicp with a per-iteration trace (nullable; max_iter x 16 doubles: R (9) and t (3) after the iteration, the
+ * lambda of its first trial, 0, 0, the LM status 0 accepted / 1 converged / 2 failed). */
+int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
+                   int nt, int max_iter, double rot_eps, double trans_eps, double* out_T, double* trace);
+
 /* The linearisation at T (4x4 row-major double) on the spec's correspondences (out_corr: ns, -1 = none):
  * textbook = 0 the spec's arithmetic and reduction order, textbook = 1 an independent long-double restatement of
  * fast_gicp's 4x4 homogeneous form (RCR = C_B + T C_A T^T, RCR(3,3) = 1, M = RCR^-1 by Gauss-Jordan, M(3,3) = 0,

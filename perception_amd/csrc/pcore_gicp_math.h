@@ -407,13 +407,14 @@ PCORE_UNROLL
     return (y0 - yi) / den;
 }
 
-// accepted step: lambda * max(1/3, 1 - (2 rho - 1)^3), the cube as (u u) u
-PCORE_GHD double lm_accept_lambda(double lambda, double rho) {
+// accepted step: lambda <- lambda * max(1/3, 1 - (2 rho - 1)^3), the cube as (u u) u; lm_gain is the factor
+PCORE_GHD double lm_gain(double rho) {
     const double u = 2.0 * rho - 1.0;
     const double f = 1.0 - u * u * u;
     const double third = 1.0 / 3.0;
-    return lambda * (third < f ? f : third);
+    return third < f ? f : third;  // std::max(1/3, f)
 }
+PCORE_GHD double lm_accept_lambda(double lambda, double rho) { return lambda * lm_gain(rho); }
 
 PCORE_GHD bool all_finite6(const double (&d)[6]) {
     bool ok = true;
