@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PCORE_ABI_VERSION 3
+#define PCORE_ABI_VERSION 4
 
 enum pcore_status {
     PCORE_OK = 0,
@@ -168,10 +168,28 @@ int pcore_evaluate_icp(pcore_ctx* ctx, const float* d_poses, const int32_t* d_po
                        int32_t* d_out_iters, float* d_out_rc, float* d_out_oc, float* d_out_diff,
                        pcore_stream stream);
 
-/* Stage "RENDER": full-resolution int32 z-buffers (cm) with source occlusion and INT_MAX -> 0
- * (image_render, image_renderer.cuh:336-496).  d_out_depth: N x H x W.  Parity mode. */
+/* Stage "RENDER" / "DEBUG" images (renderer.cu:1594-1615): full-resolution int32 z-buffers (cm) with source
+ * occlusion and INT_MAX -> 0 (image_render, image_renderer.cuh:336-496).  d_out_depth: N x H x W.
+ * d_out_color (nullable): the reference's result_color -- three planes red, green, blue of N x H x W uint8 each,
+ * concatenated -- holding each pixel's nearest triangle colour (the first triangle reaching the minimum depth,
+ * as the serial z-test of image_renderer.cuh:146-159 keeps it; the tri_rgb of pcore_upload_meshes), black where
+ * nothing is rendered or the source occludes the render (image_renderer.cuh:160-196). */
 int pcore_render(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
-                 int32_t num_poses, float occlusion_threshold, int32_t* d_out_depth, pcore_stream stream);
+                 int32_t num_poses, float occlusion_threshold, int32_t* d_out_depth, uint8_t* d_out_color,
+                 pcore_stream stream);
+
+/* gpu_stats of render_cuda_multi_unified (model.h:24-27, filled at renderer.cu:1707 and 1739) for the last
+ * pcore_evaluate_icp: icp_runtime = seconds of its GICP stage (source covariances + GICP launches, HIP events on
+ * the call's stream -- this call waits for them); peak_memory_usage = the most device memory in use (MB,
+ * hipMemGetInfo like print_cuda_memory_usage, cuda/utils.cuh:6-24) at a GICP stage since the last reset;
+ * gicp_ms = the GICP launches alone; icp_chunks = chunks the batch ran in.  reset != 0 restarts the peak. */
+typedef struct pcore_gpu_stats {
+    float icp_runtime;
+    double peak_memory_usage;
+    float gicp_ms;
+    int32_t icp_chunks;
+} pcore_gpu_stats;
+int pcore_get_stats(pcore_ctx* ctx, pcore_gpu_stats* out, int32_t reset);
 
 /* Stage "CLOUD": compute_point_clouds (compute_point_clouds.cuh:188-367) over N z-buffers: stride mask,
  * pose-major / row / column compaction, unprojection.  xyz AoS (cap x 3).  d_label_mask (H x W) only

@@ -94,6 +94,30 @@ def render_depth(tris, tris_model_count, poses, pose_model, pose_label, width, h
     return out
 
 
+def render_depth_color(tris, tri_rgb, tris_model_count, poses, pose_model, pose_label, width, height, proj,
+                       src_depth, src_mask, occlusion_threshold=1.0, nthreads=0):
+    """Stage RENDER with colours: (depth (N, H, W) int32, colour (3, N, H, W) uint8 red / green / blue planes, the
+    layout of the reference's result_color)."""
+    L = lib()
+    if not getattr(L, "_rgb_typed", False):
+        L.orc_render_depth_color.argtypes = [_f32p, ctypes.c_int, _opt(_u8p), _i32p, ctypes.c_int, _f32p, _i32p,
+                                             _opt(_i32p), ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _i32p,
+                                             _opt(_u8p), ctypes.c_float, _i32p, _u8p, ctypes.c_int]
+        L._rgb_typed = True
+    tris = _c(tris, np.float32).reshape(-1)
+    poses = _c(poses, np.float32).reshape(-1)
+    n = poses.size // 16
+    out = np.empty((n, height, width), np.int32)
+    col = np.empty((n, 3, height, width), np.uint8)
+    L.orc_render_depth_color(tris, tris.size // 9, None if tri_rgb is None else _c(tri_rgb, np.uint8).reshape(-1),
+                             _c(tris_model_count, np.int32), len(tris_model_count), poses, _c(pose_model, np.int32),
+                             _c(pose_label, np.int32), n, width, height, _c(proj, np.float32),
+                             _c(src_depth, np.int32).reshape(-1),
+                             None if src_mask is None else _c(src_mask, np.uint8).reshape(-1),
+                             float(occlusion_threshold), out.reshape(-1), col.reshape(-1), nthreads)
+    return out, np.ascontiguousarray(col.transpose(1, 0, 2, 3))
+
+
 def depth_to_cloud(depth, stride, cx, cy, fx, fy, depth_factor, label_mask=None, pose_label=None):
     """Returns (xyz (P,3) f32, pose (P,) i32, label (P,) i32) in the reference's compaction order."""
     depth = _c(depth, np.int32)

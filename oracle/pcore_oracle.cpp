@@ -77,7 +77,9 @@ inline F3 barycentric(const float* A, const float* B, const float* C, const uint
 void rasterize_with_source(const F3 tri[3], F3 last_row, int32_t* depth, int width, int height,
                            const int32_t* src_depth, const uint8_t* src_mask, bool use_seg,
                            int32_t pose_label, float occlusion_threshold, int32_t* dmin = nullptr,
-                           int32_t* tri_id = nullptr, int32_t t = 0) {
+                           int32_t* tri_id = nullptr, int32_t t = 0, const uint8_t* rgb = nullptr,
+                           uint8_t* col = nullptr) {
+    const size_t npx = (size_t)width * height;
     const float W = (float)width, H = (float)height;
     float pts2[3][2];
     const float lr[3] = {last_row.x, last_row.y, last_row.z};
@@ -111,15 +113,25 @@ void rasterize_with_source(const F3 tri[3], F3 last_row, int32_t* depth, int wid
                 dmin[idx] = curr;
                 tri_id[idx] = t;
             }
-            // z-test (image_renderer.cuh:146-159), serial order
-            if (curr < depth[idx]) depth[idx] = curr;
+            // z-test (image_renderer.cuh:146-159), serial order; the colour planes with the depth
+            if (curr < depth[idx]) {
+                depth[idx] = curr;
+                if (col) {
+                    col[idx] = rgb[0];
+                    col[npx + idx] = rgb[1];
+                    col[2 * npx + idx] = rgb[2];
+                }
+            }
             const int32_t nd = depth[idx];
             const int32_t src = src_depth[idx];
             const int lab = use_seg ? (int)src_mask[idx] : 0;
             // source occlusion black-out (image_renderer.cuh:160-196)
             if ((!use_seg && (float)iabs_wrap(nd, src) > occlusion_threshold) ||
                 (use_seg && pose_label != lab - 1 && (float)iabs_wrap(nd, src) > 0.5f)) {
-                if (nd > src && src > 0) depth[idx] = INT_MAX;
+                if (nd > src && src > 0) {
+                    if (col) col[idx] = col[npx + idx] = col[2 * npx + idx] = 0;
+                    depth[idx] = INT_MAX;
+                }
             }
         }
     }
@@ -128,9 +140,10 @@ void rasterize_with_source(const F3 tri[3], F3 last_row, int32_t* depth, int wid
 void render_one_pose(const float* tris, int lo, int hi, const float* pose, int width, int height,
                      const float* proj, const int32_t* src_depth, const uint8_t* src_mask, bool use_seg,
                      int32_t pose_label, float occlusion_threshold, int32_t* depth, int32_t* dmin = nullptr,
-                     int32_t* tri_id = nullptr) {
+                     int32_t* tri_id = nullptr, const uint8_t* tri_rgb = nullptr, uint8_t* col = nullptr) {
     const size_t npx = (size_t)width * height;
     for (size_t i = 0; i < npx; i++) depth[i] = INT_MAX;
+    if (col != nullptr) std::memset(col, 0, 3 * npx);
     if (dmin != nullptr)
         for (size_t i = 0; i < npx; i++) {
             dmin[i] = INT_MAX;
@@ -144,8 +157,10 @@ void render_one_pose(const float* tris, int lo, int hi, const float* pose, int w
         for (int k = 0; k < 3; k++) local[k] = mat_mul_v(pose, v[k]);
         F3 last_row = {local[0].z, local[1].z, local[2].z};
         for (int k = 0; k < 3; k++) projd[k] = mat_mul_v(proj, local[k]);
+        static const uint8_t grey[3] = {128, 128, 128};  // model.cpp:97-101
         rasterize_with_source(projd, last_row, depth, width, height, src_depth, src_mask, use_seg, pose_label,
-                              occlusion_threshold, dmin, tri_id, t);
+                              occlusion_threshold, dmin, tri_id, t,
+                              col ? (tri_rgb ? tri_rgb + (size_t)3 * t : grey) : nullptr, col);
     }
     // max2zero (image_renderer.cuh:324-333, 465-466)
     for (size_t i = 0; i < npx; i++)
@@ -223,6 +238,28 @@ void orc_render_depth(const float* tris, int num_tris, const int32_t* tris_model
         const int m = pose_model[n];
         render_one_pose(tris, lo[m], hi[m], poses + (size_t)16 * n, width, height, proj, src_depth, src_mask,
                         use_seg, use_seg ? pose_label[n] : 0, occlusion_threshold, out + npx * n);
+    }
+}
+
+// Stage RENDER with the colour planes: out_col = 3 planes (red, green, blue) per pose, pose-major (3 x H x W each);
+// tri_rgb nullable (grey 128).
+void orc_render_depth_color(const float* tris, int num_tris, const uint8_t* tri_rgb, const int32_t* tris_model_count,
+                            int num_models, const float* poses, const int32_t* pose_model, const int32_t* pose_label,
+                            int num_poses, int width, int height, const float* proj, const int32_t* src_depth,
+                            const uint8_t* src_mask, float occlusion_threshold, int32_t* out, uint8_t* out_col,
+                            int nthreads) {
+    (void)num_tris;
+    std::vector<int> lo, hi;
+    model_ranges(tris_model_count, num_models, lo, hi);
+    const bool use_seg = pose_label != nullptr;
+    const size_t npx = (size_t)width * height;
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int n = 0; n < num_poses; n++) {
+        const int m = pose_model[n];
+        render_one_pose(tris, lo[m], hi[m], poses + (size_t)16 * n, width, height, proj, src_depth, src_mask,
+                        use_seg, use_seg ? pose_label[n] : 0, occlusion_threshold, out + npx * n, nullptr, nullptr,
+                        tri_rgb, out_col + 3 * npx * n);
     }
 }
 

@@ -40,6 +40,15 @@ void orc_render_depth(const float* tris, int num_tris, const int32_t* tris_model
                       const int32_t* src_depth, const uint8_t* src_mask, float occlusion_threshold,
                       int32_t* out, int nthreads);
 
+/* orc_render_depth plus the colour planes the serial z-test writes (image_renderer.cuh:146-196: a strictly nearer
+ * fragment writes its triangle's colour, the black-out writes 0): out_col = per pose 3 planes (red, green, blue) of
+ * H x W uint8, pose-major.  tri_rgb: T x 3 (nullable: grey 128). */
+void orc_render_depth_color(const float* tris, int num_tris, const uint8_t* tri_rgb, const int32_t* tris_model_count,
+                            int num_models, const float* poses, const int32_t* pose_model, const int32_t* pose_label,
+                            int num_poses, int width, int height, const float* proj, const int32_t* src_depth,
+                            const uint8_t* src_mask, float occlusion_threshold, int32_t* out, uint8_t* out_col,
+                            int nthreads);
+
 /* compute_point_clouds.cuh:37-184 + 265-346: stride mask, exclusive scan (pose-major, row, col),
  * unprojection.  label_mask (H x W, only valid for num_poses == 1) -> observed cloud, label = mask-1;
  * else pose_label (nullable) -> rendered cloud label.  Writes at most `cap` points; returns the

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "pcore_set_camera", "pcore_observed_cloud", "pcore_set_observation", "pcore_evaluate", "pcore_evaluate_icp",
     "pcore_render",
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
-    "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation",
+    "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation", "pcore_get_stats",
 )
 
 
@@ -49,6 +49,12 @@ class EvalParams(ctypes.Structure):
     _fields_ = [("cost_type", ctypes.c_int32), ("calc_obs_cost", ctypes.c_int32), ("stride", ctypes.c_int32),
                 ("depth_factor", ctypes.c_float), ("sensor_resolution", ctypes.c_float),
                 ("occlusion_threshold", ctypes.c_float), ("color_distance_threshold", ctypes.c_float)]
+
+
+class GpuStats(ctypes.Structure):
+    """pcore_gpu_stats (include/pcore.h; the reference's gpu_stats, model.h:24-27)."""
+    _fields_ = [("icp_runtime", ctypes.c_float), ("peak_memory_usage", ctypes.c_double), ("gicp_ms", ctypes.c_float),
+                ("icp_chunks", ctypes.c_int32)]
 
 
 class IcpParams(ctypes.Structure):
@@ -103,7 +109,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     L.pcore_evaluate.argtypes = [vp, vp, vp, vp, vp, i32, ctypes.POINTER(EvalParams), vp, vp, vp, vp, vp]
     L.pcore_evaluate_icp.argtypes = [vp, vp, vp, vp, vp, i32, ctypes.POINTER(EvalParams), ctypes.POINTER(IcpParams),
                                      vp, vp, vp, vp, vp, vp]
-    L.pcore_render.argtypes = [vp, vp, vp, vp, i32, f32, vp, vp]
+    L.pcore_render.argtypes = [vp, vp, vp, vp, i32, f32, vp, vp, vp]
+    L.pcore_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats), i32]
     L.pcore_depth_to_cloud.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, i32,
                                        ctypes.POINTER(i32), vp]
     L.pcore_select.argtypes = [vp, vp, vp, vp, i32, i64, i32, vp, vp]

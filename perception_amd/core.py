@@ -226,16 +226,28 @@ class PoseCore:
         return adj, iters, rc, oc, df
 
     def render(self, poses: torch.Tensor, pose_model: torch.Tensor, pose_label: Optional[torch.Tensor],
-               occlusion_threshold: float = 1.0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
-        """Stage RENDER: (N, H, W) int32 z-buffers in cm."""
+               occlusion_threshold: float = 1.0, out: Optional[torch.Tensor] = None, color: bool = False,
+               out_color: Optional[torch.Tensor] = None, stream=None):
+        """Stage RENDER: (N, H, W) int32 z-buffers in cm; with color=True also the reference's result_color planes,
+        returned as (depth, color (3, N, H, W) uint8 red / green / blue)."""
         n = int(poses.shape[0])
         if out is None:
             out = torch.empty((n, self.height, self.width), dtype=torch.int32, device=poses.device)
+        if color and out_color is None:
+            out_color = torch.empty((3, n, self.height, self.width), dtype=torch.uint8, device=poses.device)
         self._check(self.lib.pcore_render(
             self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
             _ptr(pose_label, torch.int32, "pose_label"), n, float(occlusion_threshold),
-            _ptr(out, torch.int32, "out"), _stream(stream)))
-        return out
+            _ptr(out, torch.int32, "out"), _ptr(out_color, torch.uint8, "out_color") if color else None,
+            _stream(stream)))
+        return (out, out_color) if color else out
+
+    def stats(self, reset: bool = False) -> dict:
+        """pcore_get_stats: the reference's gpu_stats of the last evaluate_icp (waits for its GICP stage)."""
+        st = _native.GpuStats()
+        self._check(self.lib.pcore_get_stats(self._h, ctypes.byref(st), int(bool(reset))))
+        return {"icp_runtime": st.icp_runtime, "peak_memory_usage": st.peak_memory_usage, "gicp_ms": st.gicp_ms,
+                "icp_chunks": st.icp_chunks}
 
     def depth_to_cloud(self, depth: torch.Tensor, stride: int, depth_factor: float,
                        label_mask: Optional[torch.Tensor] = None, pose_label: Optional[torch.Tensor] = None,
@@ -316,6 +328,8 @@ class PoseLanes:
     @classmethod
     def replicate(cls, core: "PoseCore", scene_setup, lanes: int = 2) -> "PoseLanes":
         """Lanes whose lane 0 is an existing, set-up context; scene_setup(c) repeats its setup on a new one."""
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
         self = cls.__new__(cls)
         self.cores = [core] + [PoseCore(core.device) for _ in range(lanes - 1)]
         dev = torch.device("cuda", core.device)

@@ -45,6 +45,7 @@ struct pcore_ctx {
     DevBuf<int4> streams;
     DevBuf<int32_t> model_st_lo, model_st_hi;
     DevBuf<float4> model_box;  // FusedArgs::model_box
+    DevBuf<uint32_t> tri_rgb;  // per original triangle: r | g << 8 | b << 16 (stage RENDER colour planes)
     bool have_mesh = false;
     // camera
     pcore_camera cam{};
@@ -103,6 +104,12 @@ struct pcore_ctx {
     DevBuf<double> metric_part;  // ADD / ADD-S per-block partial sums
     // scratch (parity stages)
     DevBuf<int32_t> scratch_counts, scratch_offsets, scratch_total;
+    DevBuf<int32_t> render_tri;  // stage RENDER colour: nearest triangle per pixel
+    // gpu_stats of the last pcore_evaluate_icp (pcore_get_stats): per chunk, events at the source covariances,
+    // the GICP launch and its end on the call's stream; the peak device memory in use at a GICP stage
+    std::vector<hipEvent_t> icp_ev;
+    int icp_ev_used = 0;
+    double peak_mem_mb = 0.0;
 };
 
 namespace {
@@ -306,7 +313,8 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
     (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
-    (void)dev_free(c->metric_part);
+    (void)dev_free(c->metric_part); (void)dev_free(c->tri_rgb); (void)dev_free(c->render_tri);
+    for (hipEvent_t e : c->icp_ev) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -402,6 +410,15 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
         tl[t] = lab_of(col);
     }
     HIPC(c, dev_upload(c->tri_lab, tl));
+    std::vector<uint32_t> packed((size_t)num_tris);
+    for (int t = 0; t < num_tris; t++) {
+        uint32_t v = 128u | 128u << 8 | 128u << 16;  // model.cpp:97-101: grey without vertex colours
+        if (tri_rgb)
+            v = (uint32_t)tri_rgb[3 * (size_t)t] | (uint32_t)tri_rgb[3 * (size_t)t + 1] << 8 |
+                (uint32_t)tri_rgb[3 * (size_t)t + 2] << 16;
+        packed[t] = v;
+    }
+    HIPC(c, dev_upload(c->tri_rgb, packed));
     HIPC(c, dev_upload(c->model_st_lo, slo));
     HIPC(c, dev_upload(c->model_st_hi, shi));
     HIPC(c, dev_upload(c->model_box, box));
@@ -911,6 +928,21 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, dev_reserve(c->icp_order_temp, order_temp));
     FusedArgs a{};
     fill_fused_args(c, p, a);
+    // gpu_stats (renderer.cu:1707, 1739): device memory in use at the GICP stage, events around it per chunk
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            c->peak_mem_mb = std::max(c->peak_mem_mb, (double)(total_b - free_b) / 1024.0 / 1024.0);
+    }
+    hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
+    HIPC(c, hipStreamIsCapturing(s, &cap_status));
+    const bool timed = cap_status == hipStreamCaptureStatusNone;
+    c->icp_ev_used = 0;
+    while (timed && c->icp_ev.size() < (size_t)3 * nchunks) {
+        hipEvent_t e;
+        HIPC(c, hipEventCreate(&e));
+        c->icp_ev.push_back(e);
+    }
     GicpArgs g{};
     g.src = c->icp_cloud.p;
     g.src_count = c->icp_count.p;
@@ -947,6 +979,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         a.cloud_count = c->icp_count.p;
         a.cloud_cap = nsamp;
         HIPC(c, launch_render_cloud(a, s));
+        hipEvent_t* ev = timed ? c->icp_ev.data() + 3 * c->icp_ev_used : nullptr;
+        if (ev) HIPC(c, hipEventRecord(ev[0], s));
         HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
         g.pose_base = base;
         g.pose_order = nullptr;
@@ -955,7 +989,12 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
                                       c->icp_order_idx.p + chunk, c->icp_order_temp.p, order_temp, s));
             g.pose_order = c->icp_order_idx.p + chunk;
         }
+        if (ev) HIPC(c, hipEventRecord(ev[1], s));
         HIPC(c, launch_gicp(g, n, c->dinfo, s));
+        if (ev) {
+            HIPC(c, hipEventRecord(ev[2], s));
+            c->icp_ev_used++;
+        }
     }
     // re-render and re-score the adjusted poses (renderer.cu:1757-1907)
     return pcore_evaluate(c, d_out_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p, d_out_rc,
@@ -963,7 +1002,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
 }
 
 int pcore_render(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
-                 int32_t num_poses, float occlusion_threshold, int32_t* d_out_depth, pcore_stream stream) {
+                 int32_t num_poses, float occlusion_threshold, int32_t* d_out_depth, uint8_t* d_out_color,
+                 pcore_stream stream) {
     if (!c) return PCORE_E_INVALID_ARG;
     if (!c->have_mesh || !c->have_cam || !c->have_obs)
         return fail(c, PCORE_E_STATE, "render: meshes, camera and observation must be set first");
@@ -978,8 +1018,38 @@ int pcore_render(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model
     HIPC(c, launch_fill_i32(d_out_depth, INT_MAX, (size_t)num_poses * W * H, s));
     HIPC(c, launch_render_full(c->tris.p, c->num_tris, c->tri_lo.p, c->tri_hi.p, d_poses, d_pose_model, num_poses, W,
                                H, c->proj.p, d_out_depth, s));
+    int32_t* tri_min = nullptr;
+    if (d_out_color) {  // stage RENDER / DEBUG colour planes: the nearest triangle per pixel, second pass
+        const size_t npx = (size_t)num_poses * W * H;
+        HIPC(c, dev_reserve(c->render_tri, npx));
+        tri_min = c->render_tri.p;
+        HIPC(c, launch_fill_i32(tri_min, INT_MAX, npx, s));
+        HIPC(c, launch_render_full_tri(c->tris.p, c->num_tris, c->tri_lo.p, c->tri_hi.p, d_poses, d_pose_model,
+                                       num_poses, W, H, c->proj.p, d_out_depth, tri_min, s));
+    }
     HIPC(c, launch_render_finalize(d_out_depth, c->src_depth.p, c->src_mask.p, d_pose_label, num_poses, W, H,
-                                   occlusion_threshold, s));
+                                   occlusion_threshold, s, tri_min, d_out_color ? c->tri_rgb.p : nullptr, d_out_color));
+    return PCORE_OK;
+}
+
+int pcore_get_stats(pcore_ctx* c, pcore_gpu_stats* out, int32_t reset) {
+    if (!c || !out) return PCORE_E_INVALID_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    double icp_ms = 0.0, gicp_ms = 0.0;
+    for (int i = 0; i < c->icp_ev_used; i++) {
+        hipEvent_t* ev = c->icp_ev.data() + 3 * i;
+        HIPC(c, hipEventSynchronize(ev[2]));
+        float a = 0.0f, b = 0.0f;
+        HIPC(c, hipEventElapsedTime(&a, ev[0], ev[2]));
+        HIPC(c, hipEventElapsedTime(&b, ev[1], ev[2]));
+        icp_ms += a;
+        gicp_ms += b;
+    }
+    out->icp_runtime = (float)(icp_ms * 1e-3);
+    out->peak_memory_usage = c->peak_mem_mb;
+    out->gicp_ms = (float)gicp_ms;
+    out->icp_chunks = c->icp_ev_used;
+    if (reset) c->peak_mem_mb = 0.0;
     return PCORE_OK;
 }
 

@@ -218,9 +218,16 @@ constexpr int kOvfGrid = 1024;  // most workgroups of the overflow launch (grid-
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
                               const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
                               const float* proj, int32_t* depth, hipStream_t s);
+// colour of stage RENDER: tri_min (N x H x W, filled with INT_MAX) receives the lowest triangle whose fragment
+// depth equals the z-buffer's minimum (depth before launch_render_finalize)
+hipError_t launch_render_full_tri(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
+                                  const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
+                                  const float* proj, const int32_t* depth, int32_t* tri_min, hipStream_t s);
+// tri_min / rgb / color nullable (no colour): rgb packed r | g << 8 | b << 16 per triangle, color 3 planes N x H x W
 hipError_t launch_render_finalize(int32_t* depth, const int32_t* src_depth, const uint8_t* src_mask,
                                   const int32_t* pose_label, int num_poses, int width, int height,
-                                  float occlusion_threshold, hipStream_t s);
+                                  float occlusion_threshold, hipStream_t s, const int32_t* tri_min = nullptr,
+                                  const uint32_t* rgb = nullptr, uint8_t* color = nullptr);
 hipError_t launch_fill_i32(int32_t* p, int32_t v, size_t n, hipStream_t s);
 // 3-DoF world-frame bounds of depth2cloud_global (compute_point_clouds.cuh:79-91, 125-133): a pixel is
 // kept when its camera-frame point, moved to the world by m (3 x 4 row-major, camera_transform), lies

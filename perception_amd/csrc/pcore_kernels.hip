@@ -12,7 +12,8 @@
 //                          the three per-pose costs.  No per-pose HBM traffic except 64 B of pose in and
 //                          12 B of costs out.
 //   render_full_kernel     stage RENDER (parity): full-resolution z-buffer in HBM via atomicMin.
-//   render_finalize_kernel source occlusion + INT_MAX -> 0 on the full z-buffer.
+//   render_full_tri_kernel stage RENDER colour: the lowest triangle reaching each pixel's minimum depth.
+//   render_finalize_kernel source occlusion + INT_MAX -> 0 on the full z-buffer (+ the colour planes).
 //   cloud_count / cloud_write  stage CLOUD and depth2cloud_global: stride mask, ordered compaction, unprojection.
 //   select_kernel          host selection of the reference (int cost, filter, per-model argmin key).
 #include "pcore_internal.h"
@@ -1247,15 +1248,77 @@ __global__ void __launch_bounds__(256) render_full_kernel(const float* tris, int
         }
 }
 
+// The colour of stage RENDER (render_triangle_multi's red / green / blue planes, image_renderer.cuh:146-196): the
+// serial z-test writes a triangle's colour whenever its fragment is strictly nearer, so the pixel keeps the colour
+// of the first triangle (lowest index) whose fragment reaches the minimum depth.  A second pass over the same
+// fragments keeps, per pixel, the lowest triangle index whose depth equals the z-buffer's minimum.
+__global__ void __launch_bounds__(256) render_full_tri_kernel(const float* tris, int num_tris, const int32_t* tri_lo,
+                                                              const int32_t* tri_hi, const float* poses,
+                                                              const int32_t* pose_model, int width, int height,
+                                                              const float* proj, const int32_t* depth,
+                                                              int32_t* tri_min) {
+    const int pose = blockIdx.y;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tris) return;
+    const int m = pose_model[pose];
+    if (!(t >= tri_lo[m] && t < tri_hi[m])) return;
+    const float* M = poses + (size_t)16 * pose;
+    const float* tp = tris + (size_t)9 * t;
+    const float Wf = (float)width, Hf = (float)height;
+    float p[3][2], z[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const float x = tp[3 * k], y = tp[3 * k + 1], zz = tp[3 * k + 2];
+        const float lx = row4(M[0], M[1], M[2], M[3], x, y, zz);
+        const float ly = row4(M[4], M[5], M[6], M[7], x, y, zz);
+        const float lz = row4(M[8], M[9], M[10], M[11], x, y, zz);
+        const float px = row4(proj[0], proj[1], proj[2], proj[3], lx, ly, lz);
+        const float py = row4(proj[4], proj[5], proj[6], proj[7], lx, ly, lz);
+        p[k][0] = px / lz * Wf / 2.0f + Wf / 2.0f;
+        p[k][1] = py / lz * Hf / 2.0f + Hf / 2.0f;
+        z[k] = lz;
+    }
+    float bmin[2], bmax[2];
+    bbox_ref(p, (float)(width - 1), (float)(height - 1), bmin, bmax);
+    int lo0, hi0, lo1, hi1;
+    if (!loop_bounds(bmin[0], bmax[0], lo0, hi0) || !loop_bounds(bmin[1], bmax[1], lo1, hi1)) return;
+    const size_t base = (size_t)pose * width * height;
+    for (int P1 = lo1; P1 <= hi1; P1++)
+        for (int P0 = lo0; P0 <= hi0; P0++) {
+            int32_t d;
+            if (fragment(p[0][0], p[0][1], p[1][0], p[1][1], p[2][0], p[2][1], z[0], z[1], z[2], (float)P0, (float)P1, d)) {
+                const size_t i = base + P0 + (size_t)(height - 1 - P1) * width;
+                if (d == depth[i]) atomicMin(&tri_min[i], t);
+            }
+        }
+}
+
+// Source occlusion + max2zero on the full z-buffer (the a6' rule); with `rgb` (packed r | g << 8
+// | b << 16 per triangle) also the colour planes (red, green, blue planes of N x H x W each, the reference's
+// result_color): the nearest triangle's colour, black where no fragment landed or the source occludes the render.
 __global__ void render_finalize_kernel(int32_t* depth, const int32_t* src_depth, const uint8_t* src_mask,
-                                       const int32_t* pose_label, int width, int height, float occlusion_threshold) {
+                                       const int32_t* pose_label, int width, int height, float occlusion_threshold,
+                                       const int32_t* tri_min, const uint32_t* rgb, uint8_t* color, int num_poses) {
     const int pose = blockIdx.y;
     const size_t npx = (size_t)width * height;
     const bool use_seg = pose_label != nullptr;
     const int32_t pl = use_seg ? pose_label[pose] : 0;
     int32_t* img = depth + npx * pose;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x)
-        img[i] = occlusion_rule(img[i], src_depth[i], use_seg ? (int)src_mask[i] : 0, use_seg, pl, occlusion_threshold);
+    const size_t plane = npx * (size_t)num_poses;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x) {
+        const int32_t dmin = img[i];
+        const int32_t z = occlusion_rule(dmin, src_depth[i], use_seg ? (int)src_mask[i] : 0, use_seg, pl, occlusion_threshold);
+        img[i] = z;
+        if (color) {
+            // blocked fragments end at INT_MAX (0 after max2zero) and a blocked dmin is > src > 0, so z != dmin
+            const bool shown = dmin != INT_MAX && z == dmin;
+            const uint32_t c = shown ? rgb[tri_min[npx * pose + i]] : 0u;
+            uint8_t* px = color + npx * pose + i;
+            px[0] = (uint8_t)(c & 0xff);
+            px[plane] = (uint8_t)((c >> 8) & 0xff);
+            px[2 * plane] = (uint8_t)((c >> 16) & 0xff);
+        }
+    }
 }
 
 __global__ void fill_i32_kernel(int32_t* p, int32_t v, size_t n) {
@@ -1280,15 +1343,26 @@ hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tr
     return hipGetLastError();
 }
 
+hipError_t launch_render_full_tri(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
+                                  const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
+                                  const float* proj, const int32_t* depth, int32_t* tri_min, hipStream_t s) {
+    if (num_poses <= 0 || num_tris <= 0) return hipSuccess;
+    dim3 grid((num_tris + 255) / 256, num_poses);
+    hipLaunchKernelGGL(render_full_tri_kernel, grid, dim3(256), 0, s, tris, num_tris, tri_lo, tri_hi, poses,
+                       pose_model, width, height, proj, depth, tri_min);
+    return hipGetLastError();
+}
+
 hipError_t launch_render_finalize(int32_t* depth, const int32_t* src_depth, const uint8_t* src_mask,
                                   const int32_t* pose_label, int num_poses, int width, int height,
-                                  float occlusion_threshold, hipStream_t s) {
+                                  float occlusion_threshold, hipStream_t s, const int32_t* tri_min,
+                                  const uint32_t* rgb, uint8_t* color) {
     if (num_poses <= 0) return hipSuccess;
     const size_t npx = (size_t)width * height;
     unsigned bx = (unsigned)((npx + 255) / 256);
     if (bx > 256) bx = 256;
     hipLaunchKernelGGL(render_finalize_kernel, dim3(bx, num_poses), dim3(256), 0, s, depth, src_depth, src_mask,
-                       pose_label, width, height, occlusion_threshold);
+                       pose_label, width, height, occlusion_threshold, tri_min, rgb, color, num_poses);
     return hipGetLastError();
 }
 

@@ -50,6 +50,10 @@ class PerchParams:
     use_color_cost: bool = False
     color_distance_threshold: float = 15.0
     use_cylinder_observed: bool = False      # 3-DoF observed totals from the pose's cylinder
+    # IsValidPose's grid-cell radius (search_env.cpp:336-349): env_params_.res = /search_resolution_translation
+    # (object_recognizer.cpp:59-60, default 0.04 m), or the model's own with use_model_specific_search_resolution
+    search_resolution: float = 0.04
+    use_model_specific_search_resolution: bool = False
     # fast_gicp settings hard-coded at renderer.cu:1696-1699
     icp_k: int = ICP_K
     icp_max_iterations: int = ICP_MAX_ITER
@@ -78,6 +82,7 @@ class ModelMetaData:
     symmetry_mode: int = 0                   # 1 = semi-symmetric (yaw grid stops past pi)
     mesh_in_mm: bool = False
     mesh_scaling_factor: float = 1.0
+    search_resolution: float = 0.04          # used with use_model_specific_search_resolution
 
 
 @dataclass
@@ -131,6 +136,48 @@ def preprocessing_transform(model: Model, flipped: bool = False, mesh_in_mm: boo
     T[:3, :3] *= s
     T[:3, 3] = -np.array([c[0] * s, c[1] * s, z * s])
     return (T @ flip).astype(np.float32).astype(np.float64)
+
+
+def radius_counts(queries: np.ndarray, points: np.ndarray, radius: float, device, cap: Optional[int] = None
+                  ) -> np.ndarray:
+    """Neighbour counts of PCL's KdTreeFLANN radiusSearch (pcl::search::KdTree over FLANN's exact single-index
+    tree), as IsValidPose (search_env.cpp:359-396) and the cylinder totals (search_env.cpp:1593-1612) call it: query
+    and points are float PointXYZ, the radius is passed squared as float(r * r), FLANN's L2_Simple sums (q - p)^2 over
+    x, y, z in float from zero, and RadiusResultSet keeps a point when dist < r^2 (strict); max_nn (`cap`) caps the
+    count.  Elementwise float32 tensor ops on `device`, chunked: each is one IEEE operation, so the counts do not
+    depend on the device."""
+    q = np.ascontiguousarray(np.asarray(queries, np.float64).astype(np.float32)).reshape(-1, 3)
+    pts = np.ascontiguousarray(np.asarray(points, np.float32)).reshape(-1, 3)
+    out = np.zeros(len(q), np.int64)
+    if len(pts) == 0 or len(q) == 0:
+        return out
+    r2 = torch.tensor(np.float32(radius * radius), device=device)
+    sg = torch.from_numpy(pts).to(device)
+    tt = torch.from_numpy(q).to(device)
+    step = max(1, (1 << 24) // max(len(pts), 1))
+    for a in range(0, len(q), step):
+        t = tt[a:a + step]
+        dx = t[:, 0:1] - sg[None, :, 0]
+        d2 = dx * dx
+        dy = t[:, 1:2] - sg[None, :, 1]
+        d2 = d2 + dy * dy
+        dz = t[:, 2:3] - sg[None, :, 2]
+        d2 = d2 + dz * dz
+        out[a:a + step] = (d2 < r2).sum(1).cpu().numpy()
+    if cap is not None:
+        out = np.minimum(out, cap)
+    return out
+
+
+def valid_pose_mask(translations: np.ndarray, seg_points: np.ndarray, search_rad: float, need: int,
+                    device) -> np.ndarray:
+    """IsValidPose's neighbour test (search_env.cpp:359-396): the pose translation as a float PointXYZ
+    (search_env.cpp:317-325) has at least `need` points within search_rad (radius_counts; max_nn = need only caps
+    the count)."""
+    seg = np.asarray(seg_points, np.float32).reshape(-1, 3)
+    if len(seg) < need:
+        return np.zeros(len(np.asarray(translations).reshape(-1, 3)), bool)
+    return radius_counts(translations, seg, search_rad, device) >= need
 
 
 def _dims(model: Model):
@@ -200,35 +247,28 @@ class ObjectRecognizer:
         self.segmented_object_names = list(inp.model_names)
 
     # -- GenerateSuccessorStates (search_env.cpp:7056-7254) ----------------------------------------
-    def _valid_pose_mask(self, model_id: int, translations: np.ndarray, required_object_id: int) -> np.ndarray:
-        """IsValidPose (search_env.cpp:309-410), 6-DoF branch: at least min_neighbor_points_for_valid_pose
-        points of the object's segmented observed cloud within inflation * circumscribed_radius_3d."""
+    def _search_radius(self, model_id: int) -> float:
+        """IsValidPose's search radius, 6-DoF branch (search_env.cpp:336-390): max(inflation * circumscribed
+        radius 3D, grid-cell circumscribing radius hypot(res / 2, res / 2)); after_refinement is false on the
+        greedy path (search_env.cpp:7140), so the cell term stays."""
         dims = _dims(self.models[model_id])
         circ3d = float(max(dims)) / 2.0  # GetCircumscribedRadius3D, object_model.cpp:464-466
         inscribed = float(min(dims[0], dims[1])) / 2.0
         infl = 1.0 + K_MESH_ADDITIVE_INFLATION / inscribed if inscribed > 0 else 1.0  # object_model.cpp:381-383
-        rad = infl * circ3d
-        seg = self.obs_xyz_host[self.obs_label_host == required_object_id].astype(np.float64)
-        need = self.params.min_neighbor_points_for_valid_pose
-        if len(seg) < need:
-            return np.zeros(len(translations), bool)
-        # float64 squared distances (dx^2 + dy^2) + dz^2 on the device, chunked -- elementwise eager ops,
-        # the same IEEE operations in the same order as a host evaluation
-        out = np.zeros(len(translations), bool)
-        sg = torch.from_numpy(np.ascontiguousarray(seg)).to(self.device)
-        tt = torch.from_numpy(np.ascontiguousarray(translations, dtype=np.float64)).to(self.device)
-        r2 = rad * rad
-        step = max(1, (1 << 24) // max(len(seg), 1))
-        for a in range(0, len(translations), step):
-            t = tt[a:a + step]
-            dx = t[:, 0:1] - sg[None, :, 0]
-            d2 = dx * dx
-            dy = t[:, 1:2] - sg[None, :, 1]
-            d2 = d2 + dy * dy
-            dz = t[:, 2:3] - sg[None, :, 2]
-            d2 = d2 + dz * dz
-            out[a:a + step] = ((d2 <= r2).sum(1) >= need).cpu().numpy()
-        return out
+        p = self.params
+        res = p.search_resolution
+        if p.use_model_specific_search_resolution:
+            res = self.bank[self.model_names[model_id]].search_resolution
+        cell = float(np.hypot(res / 2.0, res / 2.0))
+        return max(infl * circ3d, cell)
+
+    def _valid_pose_mask(self, model_id: int, translations: np.ndarray, required_object_id: int) -> np.ndarray:
+        """IsValidPose (search_env.cpp:309-410), 6-DoF branch: at least min_neighbor_points_for_valid_pose points
+        of the object's segmented observed cloud within the search radius, counted as PCL's KdTreeFLANN
+        radiusSearch does (valid_pose_mask)."""
+        seg = self.obs_xyz_host[self.obs_label_host == required_object_id]
+        return valid_pose_mask(translations, seg, self._search_radius(model_id),
+                               self.params.min_neighbor_points_for_valid_pose, self.device)
 
     def generate_successor_states(self, inp: RecognitionInput):
         states = []  # (model_id, required_object_id, (7,) pose)
@@ -288,6 +328,7 @@ class ObjectRecognizer:
         keys = torch.full((K,), PCORE_KEY_NONE, dtype=torch.int64, device=self.device)
         adj_all = None
         icp_time = 0.0
+        peak_mb = float(torch.cuda.max_memory_allocated(self.device)) / 1024.0 / 1024.0
         if mine:
             poses = torch.from_numpy(self._pose_in_cam(mine)).to(self.device)
             pm = torch.tensor([s[0] for s in mine], dtype=torch.int32, device=self.device)
@@ -324,6 +365,8 @@ class ObjectRecognizer:
                 self.core.select(rc[sl], oc[sl], pm[sl], K, index_base=lo + b0, keys=keys)
             torch.cuda.synchronize(self.device)
             icp_time = time.perf_counter() - ti if (p.icp_type == 3 and inp.use_icp) else 0.0
+            if p.icp_type == 3 and inp.use_icp:
+                peak_mb = self.core.stats(reset=True)["peak_memory_usage"]  # gpu_stats.peak_memory_usage (MB)
             self._last_costs = (rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy())
         allreduce_min_keys(keys)
         cost, idx = decode_keys(keys)
@@ -347,7 +390,7 @@ class ObjectRecognizer:
             cont = np.concatenate([Tm[:3, 3], q])
             results.append((m, int(cost[m]), int(idx[m]), cont))
         self.last_stats = EnvStats(scenes_rendered=n_total, scenes_valid=0, time=time.perf_counter() - t0,
-                                   icp_time=icp_time, peak_gpu_mem=float(torch.cuda.max_memory_allocated(self.device)))
+                                   icp_time=icp_time, peak_gpu_mem=peak_mb)
         return results
 
     # -- ObjectRecognizer::LocalizeObjectsGreedyRender (object_recognizer.cpp:290-342) -------------

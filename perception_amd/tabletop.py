@@ -36,7 +36,7 @@ import torch
 from ._native import COST_DEPTH_3DOF, COST_RGBD_3DOF
 from .model import pose_matrix
 from .recognizer import (CAM_TO_BODY, K_MESH_ADDITIVE_INFLATION, CameraIntrinsics, ModelMetaData,
-                         ObjectRecognizer, PerchParams, RecognitionInput, _dims)
+                         ObjectRecognizer, PerchParams, RecognitionInput, _dims, radius_counts)
 
 
 @dataclass
@@ -86,19 +86,19 @@ def inflation_factor(dims) -> float:
     return 1.0 + K_MESH_ADDITIVE_INFLATION / inscribed if inscribed > 0 else 1.0
 
 
-def count_within(centres_xy: np.ndarray, pts_xy: np.ndarray, radius: float) -> np.ndarray:
-    """Projected-cloud radius search counts (all points at the table height, so 3-D = 2-D distance)."""
-    out = np.zeros(len(centres_xy), np.int64)
-    r2 = radius * radius
-    for a in range(0, len(centres_xy), 1024):
-        c = centres_xy[a:a + 1024]
-        d2 = ((c[:, None, :] - pts_xy[None, :, :]) ** 2).sum(-1)
-        out[a:a + 1024] = (d2 <= r2).sum(1)
-    return out
+def count_within(centres_xy: np.ndarray, pts_xy: np.ndarray, radius: float, table_height: float = 0.0,
+                 device="cpu", cap: Optional[int] = None) -> np.ndarray:
+    """Projected-cloud radius search counts: every projected point and every query sits at z = table_height
+    (search_env.cpp:5643-5649, 317-325), so the PCL float distance is the (x, y) one (radius_counts)."""
+    c = np.asarray(centres_xy, np.float64).reshape(-1, 2)
+    p = np.asarray(pts_xy, np.float32).reshape(-1, 2)
+    zq = np.full((len(c), 1), table_height, np.float64)
+    zp = np.full((len(p), 1), np.float32(table_height), np.float32)
+    return radius_counts(np.hstack([c, zq]), np.hstack([p, zp]), radius, device, cap)
 
 
 def grid_states(table: TableParams, model_id: int, dims, projected_xy: np.ndarray, min_neighbors: int,
-                symmetry_mode: int = 0) -> List[tuple]:
+                symmetry_mode: int = 0, device="cpu") -> List[tuple]:
     """GenerateSuccessorStates' 3-DoF grid (search_env.cpp:7268-7320) for one model: x and y advance by
     repeated addition of res (double), yaw from 0 below 2 pi by theta_res; a pose needs IsValidPose; for a
     semi-symmetric model (symmetry_mode 1) the yaw loop stops at the first valid yaw above pi + theta_res."""
@@ -119,7 +119,7 @@ def grid_states(table: TableParams, model_id: int, dims, projected_xy: np.ndarra
     states = []
     for x in xs:
         for y in ys:
-            ok = count_within(np.array([[x, y]]), projected_xy, rad)[0] >= min_neighbors
+            ok = count_within(np.array([[x, y]]), projected_xy, rad, table.table_height, device)[0] >= min_neighbors
             for th in thetas:
                 if not ok:
                     continue  # IsValidPose does not depend on yaw in the projected branch
@@ -163,9 +163,11 @@ class TabletopRecognizer(ObjectRecognizer):
             self.core.set_observation_colors(self.obs_rgb)
         # projected cloud (search_env.cpp:5636-5662): full-resolution bounded points at the table height
         full, _ = self.core.observed_cloud_bounded(d_depth, 1, depth_factor, self.transform, self.bounds)
-        f = full.cpu().numpy().astype(np.float64)
-        M = self.transform.astype(np.float64)
-        self.projected_xy = f @ M[:2, :3].T + M[:2, 3]
+        # the world frame in float, row by row left to right (pcl::transformPointCloud with an Affine3f)
+        f = full.cpu().numpy().astype(np.float32)
+        M = self.transform.astype(np.float32)
+        self.projected_xy = np.stack([((M[r, 0] * f[:, 0] + M[r, 1] * f[:, 1]) + M[r, 2] * f[:, 2]) + M[r, 3]
+                                      for r in range(2)], 1)
         self.segmented_object_names = []
 
     def generate_successor_states(self, inp: RecognitionInput = None):
@@ -174,7 +176,7 @@ class TabletopRecognizer(ObjectRecognizer):
             dims = _dims(self.models[ii])
             sym = self.bank[name].symmetry_mode
             states += grid_states(self.table, ii, dims, self.projected_xy,
-                                  self.params.min_neighbor_points_for_valid_pose, sym)
+                                  self.params.min_neighbor_points_for_valid_pose, sym, self.device)
         return states
 
     def _cost_type(self) -> int:
@@ -192,7 +194,8 @@ class TabletopRecognizer(ObjectRecognizer):
         for i, (mid, _, p) in enumerate(states):
             dims = _dims(self.models[mid])
             r = inflation_factor(dims) * circumscribed_radius(dims)
-            out[i] = count_within(np.asarray(p[None, :2]), self.projected_xy, r)[0]
+            out[i] = count_within(np.asarray(p[None, :2]), self.projected_xy, r, self.table.table_height,
+                                  self.device, cap=self.cam.width * self.cam.height)[0]  # max_nn = kNumPixels
         return out
 
     def _pose_in_cam(self, states) -> np.ndarray:

@@ -605,3 +605,36 @@ def test_general_projection_matrix(one_object):
                               case.pose_label[:n], sc.width, sc.height, proj, sc.src_depth_cm, sc.mask, 1.0)
     assert (ref > 0).sum() > 0
     assert np.array_equal(dbg.cpu().numpy(), ref[:, ::s, ::s])
+
+
+@pytest.mark.parametrize("labels", [True, False])
+def test_render_color_planes_bit_exact(labels):
+    """Stage RENDER / DEBUG colour planes (renderer.cu:1594-1615): the reference's result_color -- red, green and
+    blue planes of N x H x W -- against the oracle's serial z-test with colour writes and black-out
+    (image_renderer.cuh:146-196), per-triangle colours random so every tie and occlusion shows."""
+    case = SceneCase(("003_cracker_box", "005_tomato_soup_can", "061_foam_brick"), n_poses=8, seed=5)
+    sc = case.scene
+    rng = np.random.default_rng(9)
+    rgb = rng.integers(0, 256, size=(len(sc.bank.tris), 3), dtype=np.uint8)
+    core = PoseCore(0)
+    core.upload_meshes(sc.bank.tris, sc.bank.tris_model_count, colors=rgb)
+    core.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+    dev = torch.device("cuda", 0)
+    raw, mask = torch.from_numpy(sc.depth_raw).to(dev), torch.from_numpy(sc.mask).to(dev)
+    xyz, lab = core.observed_cloud(raw, mask, 8, sc.depth_factor)
+    core.set_observation(torch.from_numpy(sc.src_depth_cm).to(dev), mask, xyz, lab, 0.01)
+    poses = torch.from_numpy(case.poses).to(dev)
+    pm = torch.from_numpy(case.pose_model).to(dev)
+    pl = torch.from_numpy(case.pose_label).to(dev) if labels else None
+    zb, col = core.render(poses, pm, pl, color=True)
+    rz, rc = oracle.render_depth_color(sc.bank.tris, rgb, sc.bank.tris_model_count, case.poses, case.pose_model,
+                                       case.pose_label if labels else None, sc.width, sc.height, sc.proj,
+                                       sc.src_depth_cm, sc.mask if labels else None, 1.0)
+    assert np.array_equal(zb.cpu().numpy(), rz)
+    got = col.cpu().numpy()
+    assert got.shape == rc.shape == (3, len(case.poses), sc.height, sc.width)
+    mism = np.argwhere(got != rc)
+    assert len(mism) == 0, f"{len(mism)} mismatching colour samples, first {mism[:5]}"
+    assert (rc.max(0) > 0).sum() > 1000
+    # the depth-only call is unchanged by the colour pass
+    assert np.array_equal(core.render(poses, pm, pl).cpu().numpy(), rz)

@@ -217,3 +217,38 @@ def test_gicp_recovers_a_small_rigid_motion():
     back = src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]
     assert it < 150
     assert np.abs(back - tgt).max() < 1e-4
+
+
+def test_render_color_nearest_triangle_and_black_out():
+    """Colour planes of the oracle's serial z-test (image_renderer.cuh:146-196): two overlapping fronto-parallel
+    squares of different colours -- the nearer one's colour shows where they overlap, the farther one's elsewhere;
+    a source pixel nearer than the render by more than the threshold (3-DoF) blacks the pixel out (depth 0, colour
+    0); the depth equals orc_render_depth's."""
+    W, H = 64, 48
+    fx = fy = 50.0
+    cx, cy = 32.0, 24.0
+    proj = oracle.compute_proj(fx, fy, cx, cy, W, H)
+
+    def square(z, half, dx):
+        a = [[-half + dx, -half, z], [half + dx, -half, z], [half + dx, half, z]]
+        b = [[-half + dx, -half, z], [half + dx, half, z], [-half + dx, half, z]]
+        return np.array([a, b], np.float32).reshape(2, 9)
+
+    tris = np.concatenate([square(1.0, 0.2, -0.1), square(0.8, 0.1, 0.1)])
+    rgb = np.array([[200, 10, 10], [200, 10, 10], [10, 220, 30], [10, 220, 30]], np.uint8)
+    pose = np.eye(4, dtype=np.float32) * 100.0
+    pose[3, 3] = 1.0
+    src = np.zeros((H, W), np.int32)
+    src[0:10, 0:64] = 50  # a source surface at 50 cm over the top rows
+    z, col = oracle.render_depth_color(tris, rgb, [4], pose.reshape(1, 16), np.zeros(1, np.int32), None, W, H, proj,
+                                       src, None, 1.0)
+    z0 = oracle.render_depth(tris, [4], pose.reshape(1, 16), np.zeros(1, np.int32), None, W, H, proj, src, None, 1.0)
+    assert np.array_equal(z, z0)
+    near = z[0] == 80
+    far = z[0] == 100
+    assert near.sum() > 50 and far.sum() > 50
+    assert np.all(col[:, 0][:, near] == np.array([[10], [220], [30]]))
+    assert np.all(col[:, 0][:, far] == np.array([[200], [10], [10]]))
+    blocked = (src > 0) & (z[0] == 0)
+    assert blocked.sum() > 0 and np.all(col[:, 0][:, blocked] == 0)
+    assert np.all(col[:, 0][:, z[0] == 0] == 0)
