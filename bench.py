@@ -12,7 +12,10 @@ the next step's fill; every step is still one full 10k-pose batch and completes 
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
 Rank 0 prints ONE JSON line (see DESIGN.md "Measurement" for the roofline / cpu_baseline fields;
-cpu_reference_path times the reference's own CPU/OMP path, SURVEY.md row a14, on config C1).
+cpu_reference_path times the reference's own CPU/OMP path, SURVEY.md row a14, on config C1).  The same line
+carries "c3": BASELINE.json configs[2] measured in the same run -- 5 objects x 10k candidate poses per GPU,
+render + stride cloud + covariances + GICP + re-render + re-score + select per step (the north star's
+"rendered + GICP-refined + scored" figure), with its own roofline for the GICP kernel.
 """
 from __future__ import annotations
 
@@ -95,6 +98,107 @@ def cpu_reference_path(seconds: float):
                       f"{iters / max(done, 1):.1f} ICP iterations), one pose per OpenMP thread, {dt:.1f} s"}
 
 
+C3_NAMES = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
+
+
+def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per_model: int = 10000):
+    """BASELINE.json configs[2] (C3) on this rank's GPU: 5 objects, poses_per_model candidates each, GICP on.
+    One step = pcore_evaluate_icp over the whole batch (render, cloud, covariances, GICP, re-render, re-score)
+    + the per-model argmin keys + their all-reduce(MIN).  Timed like the C2 leg (barrier + synchronize on both
+    sides, max over ranks); the GICP launches' own time comes from pcore_get_stats (HIP events on the call's
+    stream), the time base of the GICP kernel's roofline."""
+    import torch
+    from perception_amd import distributed as pdist
+    from perception_amd import workloads
+    from perception_amd._native import PCORE_KEY_NONE
+    from perception_amd.core import decode_keys
+
+    w = workloads.build(names=C3_NAMES, poses_per_model=poses_per_model, device=local, rank=rank)
+    n = int(w.poses.shape[0])
+    dev = w.poses.device
+    out = (torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+           *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)))
+    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev)
+    gicp_ms, icp_s = [], []
+
+    def step(record):
+        keys.fill_(PCORE_KEY_NONE)
+        adj, it, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                  stride=w.stride, out=out)
+        w.core.select(rc, oc, w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
+        if record:
+            st = w.core.stats()  # waits for this step's GICP stage (events), not for the re-score
+            gicp_ms.append(st["gicp_ms"])
+            icp_s.append(st["icp_runtime"])
+        work = pdist.allreduce_min_keys_async(keys)
+        if work is not None:
+            work.wait()
+
+    for _ in range(max(warmup, 1)):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    its = out[1].cpu().numpy()
+    cost, idx = decode_keys(keys)
+    g_ms = float(np.mean(gicp_ms)) if gicp_ms else None
+    iter_total = int(its.sum())
+    valu_peak = VALU_SIMDS * VALU_CLOCK_HZ / 2.0
+    instr_per_iter, sq_note = None, "no profiles/sq_counters_gicp.json"
+    sq_path = os.path.join(ROOT, "profiles", "sq_counters_gicp.json")
+    if os.path.exists(sq_path):
+        try:
+            from perception_amd.build import gicp_source_digest
+            with open(sq_path) as f:
+                sq = json.load(f)
+            if sq.get("gicp_source_digest") != gicp_source_digest():
+                sq_note = "counter profile of other GICP sources (stale): not used"
+            else:
+                instr_per_iter = float(sq["gicp_kernel"]["derived_valu_instr_per_pose_iteration"])
+                sq_note = ("profiles/sq_counters_gicp.json (SQ_INSTS_VALU / pose-iterations, counters-only rocprofv3 "
+                           "pass of the same GICP sources)")
+        except (OSError, ValueError, KeyError) as e:
+            sq_note = f"unreadable counter profile: {e}"
+    achieved = instr_per_iter * iter_total / (g_ms * 1e-3) if (instr_per_iter and g_ms) else None
+    return {
+        "metric": "candidate poses rendered+GICP-refined+scored/sec @640x480 (C3)",
+        "value": n * world * steps / elapsed,
+        "unit": "poses/s",
+        "ms_per_step": elapsed * 1e3 / steps,
+        "steps": steps,
+        "warmup": max(warmup, 1),
+        "config": {"workload": "C3: 5 YCB-proxy objects x 10k 6-DoF candidate poses/GPU, render + GICP (fast_gicp LM, "
+                               "k 10, <= 150 iterations) + re-render + score + select, 640x480, stride 8",
+                   "poses_per_gpu": n, "objects": C3_NAMES, "parallelism": f"pose-shard x{world}"},
+        "gicp": {"iterations_mean": float(its.mean()), "iterations_p50": float(np.percentile(its, 50)),
+                 "iterations_p90": float(np.percentile(its, 90)), "at_max_iterations": int((its >= 150).sum()),
+                 "gicp_ms_per_step": g_ms, "icp_stage_ms_per_step": float(np.mean(icp_s)) * 1e3 if icp_s else None,
+                 "timing": "pcore_get_stats: HIP events on the call's stream around the GICP launches / the "
+                           "covariances + GICP launches of every timed step"},
+        "roofline": {"bound": "valu", "kernel": "gicp_kernel",
+                     "achieved": achieved / 1e9 if achieved else None, "peak": valu_peak / 1e9,
+                     "unit": "Gwave-instr/s", "frac": achieved / valu_peak if achieved else None,
+                     "traffic": None, "valu_instr_per_pose_iteration": instr_per_iter, "valu_source": sq_note,
+                     "note": "a serial chain of <= 150 dependent iterations per pose (one wave each): latency-bound "
+                             "by design, so the VALU issue fraction is the figure of merit; HBM traffic is a few KB "
+                             "per pose-iteration, L2-resident"},
+        "argmin": {"best_cost": [int(c) for c in cost], "best_index": [int(i) for i in idx],
+                   "gt_index": [int(g) for g in w.gt_index]},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +208,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--ref-cpu-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c3-steps", type=int, default=3, help="timed C3 (GICP) steps; 0 skips the C3 leg")
+    ap.add_argument("--c3-warmup", type=int, default=1)
     args = ap.parse_args()
 
     import torch
@@ -202,6 +308,11 @@ def main():
     busy_ms = busy / len(iv)
 
     best_cost, best_idx = decode_keys(keys)
+    c3 = None
+    if args.c3_steps > 0:
+        del lanes, outs, keys_ring, works
+        torch.cuda.empty_cache()
+        c3 = c3_leg(args.c3_steps, args.c3_warmup, local, rank, world)
     if rank != 0:
         return
     total_poses = n * world * args.steps
@@ -293,6 +404,8 @@ def main():
         "roofline": roofline,
         "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},
     }
+    if c3 is not None:
+        line["c3"] = c3
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
         line["cpu_reference_path"] = cpu_reference_path(args.ref_cpu_seconds)

@@ -45,6 +45,18 @@ def kernel_source_digest() -> str:
     return h.hexdigest()[:16]
 
 
+def gicp_source_digest() -> str:
+    """SHA-256 (16 hex) of the sources that define the GICP kernels: ties profiles/sq_counters_gicp.json to the code
+    it measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("pcore_gicp.hip", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_internal.h"):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True

@@ -54,6 +54,7 @@ class PerchParams:
     # (object_recognizer.cpp:59-60, default 0.04 m), or the model's own with use_model_specific_search_resolution
     search_resolution: float = 0.04
     use_model_specific_search_resolution: bool = False
+    depth_median_blur: int = 17              # 3-DoF 8-bit depth: medianBlur aperture (search_env.cpp:187, 5922)
     # fast_gicp settings hard-coded at renderer.cu:1696-1699
     icp_k: int = ICP_K
     icp_max_iterations: int = ICP_MAX_ITER

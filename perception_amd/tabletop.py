@@ -22,7 +22,8 @@ Scoring is the GPU hot path with cost_type 0 (depth) -- or 1 (colour gate) once 
 colours -- and no pose labels.  Differences from the reference: the projected cloud is the stride-1
 bounded GPU cloud moved to the world frame (the reference builds it on the CPU with PCL from the same
 depth image, GetGravityAlignedPointCloud, search_env.cpp:4475-4600, without downsampling by default); the
-depth image is used as given (no medianBlur).
+8-bit depth images (the reference's non-16-bit branch, search_env.cpp:5916-5929) are median-blurred first
+(median_blur_u8, OpenCV medianBlur semantics).
 """
 from __future__ import annotations
 
@@ -60,6 +61,31 @@ def pr2_gpu_params(**kw) -> PerchParams:
     for k, v in kw.items():
         setattr(p, k, v)
     return p
+
+
+def median_blur_u8(img: np.ndarray, ksize: int, device="cpu") -> np.ndarray:
+    """cv::medianBlur of an 8-bit image (search_env.cpp:5922, applied to 8-bit depth before the GPU path): each
+    pixel becomes the median of its ksize x ksize window, the border replicated (OpenCV's BORDER_REPLICATE); ksize
+    odd and > 1 (ksize 1 copies).  Exact: the window holds an odd number of integers.  Torch ops on `device`
+    (unfold + kthvalue), once per scene."""
+    a = np.ascontiguousarray(img, np.uint8)
+    k = int(ksize)
+    if k <= 1:
+        return a.copy()
+    if k % 2 == 0:
+        raise ValueError("medianBlur: ksize must be odd")
+    r = k // 2
+    t = torch.from_numpy(a).to(device).to(torch.int16)[None, None].float()
+    t = torch.nn.functional.pad(t, (r, r, r, r), mode="replicate")
+    H, W = a.shape
+    out = np.empty((H, W), np.uint8)
+    rows = max(1, (1 << 24) // (k * k * W))
+    for y0 in range(0, H, rows):
+        y1 = min(H, y0 + rows)
+        win = torch.nn.functional.unfold(t[:, :, y0:y1 + 2 * r, :], kernel_size=k)  # (1, k*k, rows*W)
+        med = win[0].kthvalue(k * k // 2 + 1, dim=0).values
+        out[y0:y1] = med.reshape(y1 - y0, W).to(torch.uint8).cpu().numpy()
+    return out
 
 
 def normalize_angle_positive(a: float) -> float:
@@ -142,6 +168,8 @@ class TabletopRecognizer(ObjectRecognizer):
     def set_input_3dof(self, depth: np.ndarray, camera_pose: np.ndarray, depth_factor: float,
                        rgb: Optional[np.ndarray] = None):
         p, tb = self.params, self.table
+        if np.asarray(depth).dtype == np.uint8:  # 8-bit depth: medianBlur first (search_env.cpp:5916-5929)
+            depth = median_blur_u8(depth, p.depth_median_blur, self.device)
         depth = np.ascontiguousarray(depth, np.int32)
         if depth.shape != (self.cam.height, self.cam.width):
             raise ValueError("depth size does not match the camera")

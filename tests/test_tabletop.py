@@ -42,3 +42,19 @@ def test_grid_states_loop_semantics_and_validity():
     half = grid_states(tb, 0, [0.06, 0.06, 0.2], pts, 30, symmetry_mode=1)
     per_cell = len(half) // len(centres)
     assert per_cell == sum(1 for k in range(16) if k * 0.3926991 <= math.pi + 0.3926991)
+
+
+def test_median_blur_u8_matches_replicate_border_median():
+    """cv::medianBlur semantics for 8-bit depth (search_env.cpp:5922): the window median with the border
+    replicated -- scipy's median_filter(mode='nearest') is the same definition."""
+    from scipy.ndimage import median_filter
+
+    from perception_amd.tabletop import median_blur_u8
+
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, size=(61, 83), dtype=np.uint8)
+    img[10:30, 20:50] = 0  # depth holes
+    for k in (1, 3, 5, 17):
+        got = median_blur_u8(img, k)
+        want = img if k == 1 else median_filter(img, size=k, mode="nearest")
+        assert np.array_equal(got, want), k

@@ -18,17 +18,24 @@ def main():
     ap.add_argument("--poses", type=int, default=10000)
     ap.add_argument("--icp", action="store_true")
     ap.add_argument("--c3", action="store_true", help="the 5-object C3 scene")
+    ap.add_argument("--iters-json", default=None, help="write the GICP iterations of the last call here (--icp)")
     a = ap.parse_args()
     names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can",
              "024_bowl"] if a.c3 else ["003_cracker_box"]
     w = workloads.build(names=names, poses_per_model=a.poses)
     n = int(w.poses.shape[0])
+    its = None
     for _ in range(a.iters):
         if a.icp:
-            w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+            _, its, _, _, _ = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                  stride=w.stride)
         else:
             w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
         torch.cuda.synchronize()  # steady state: the next call sees this call's window histogram
+    if a.iters_json and its is not None:
+        import json
+        with open(a.iters_json, "w") as f:
+            json.dump({"poses": n, "pose_iterations": int(its.sum().item()), "gicp_launches_per_call": 1}, f)
     print("done", n)
 
 
