@@ -12,6 +12,7 @@
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -202,6 +203,25 @@ def read_poses_txt(path: str) -> np.ndarray:
         return np.array(fields, dtype=np.float64).reshape(-1, 7)
     rows = [[float(v) for v in ln.split(" ")[:7]] for ln in lines]
     return np.asarray(rows, np.float64).reshape(-1, 7)
+
+
+_POSES_CACHE: dict = {}
+
+
+def read_poses_txt_cached(path: str) -> np.ndarray:
+    """read_poses_txt, parsed once per file version: keyed by (path, size, mtime_ns), so an unchanged poses.txt
+    is not parsed again on the next search (the reference re-reads it every GenerateSuccessorStates; the content,
+    and so the result, is the same).  Returns a read-only array."""
+    st = os.stat(path)
+    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns)
+    hit = _POSES_CACHE.get(key)
+    if hit is None:
+        hit = read_poses_txt(path)
+        hit.setflags(write=False)
+        if len(_POSES_CACHE) > 64:
+            _POSES_CACHE.clear()
+        _POSES_CACHE[key] = hit
+    return hit
 
 
 # ------------------------------------------------------------------------------------------------

@@ -110,6 +110,39 @@ class EnvStats:
     peak_gpu_mem: float = 0.0
 
 
+class States:
+    """The candidate states of one search as arrays (the reference's vector<GraphState>): model id, required object
+    id (the pose's segmentation label; -1 in 3-DoF) and the pose row -- (x y z qx qy qz qw) for 6-DoF pose lists,
+    (x y z yaw) for the 3-DoF grid.  Iterating (or indexing with an int) yields (model, required, pose) tuples; a
+    slice is a States."""
+
+    def __init__(self, model=None, req=None, pose=None, width: int = 7):
+        self.model = np.zeros(0, np.int32) if model is None else np.ascontiguousarray(model, np.int32)
+        self.req = np.zeros(0, np.int32) if req is None else np.ascontiguousarray(req, np.int32)
+        self.pose = (np.zeros((0, width), np.float64) if pose is None
+                     else np.ascontiguousarray(pose, np.float64).reshape(len(self.model), -1))
+
+    @staticmethod
+    def concat(parts: Sequence["States"], width: int = 7) -> "States":
+        parts = [p for p in parts if len(p)]
+        if not parts:
+            return States(width=width)
+        return States(np.concatenate([p.model for p in parts]), np.concatenate([p.req for p in parts]),
+                      np.concatenate([p.pose for p in parts]))
+
+    def __len__(self):
+        return len(self.model)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return States(self.model[i], self.req[i], self.pose[i])
+        return int(self.model[i]), int(self.req[i]), self.pose[i]
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
+
+
 @dataclass
 class LocalizationResult:
     object_transforms: List[np.ndarray]
@@ -271,46 +304,45 @@ class ObjectRecognizer:
         return valid_pose_mask(translations, seg, self._search_radius(model_id),
                                self.params.min_neighbor_points_for_valid_pose, self.device)
 
-    def generate_successor_states(self, inp: RecognitionInput):
-        states = []  # (model_id, required_object_id, (7,) pose)
+    def generate_successor_states(self, inp: RecognitionInput) -> States:
+        parts = []
         for ii, name in enumerate(self.model_names):
             if inp.pose_lists is not None and name in inp.pose_lists:
                 P = np.asarray(inp.pose_lists[name], np.float64).reshape(-1, 7)
             elif inp.rendered_root_dir is not None:
                 path = os.path.join(inp.rendered_root_dir, name, "poses.txt")
-                P = pio.read_poses_txt(path) if os.path.exists(path) else np.zeros((0, 7))
+                P = pio.read_poses_txt_cached(path) if os.path.exists(path) else np.zeros((0, 7))
             else:
                 P = np.zeros((0, 7))
             req = self.segmented_object_names.index(name) if name in self.segmented_object_names else \
                 len(self.segmented_object_names)
             ok = self._valid_pose_mask(ii, P[:, :3], req) if len(P) else np.zeros(0, bool)
-            for p in P[ok]:
-                states.append((ii, req, p))
-        return states
+            k = int(ok.sum())
+            parts.append(States(np.full(k, ii, np.int32), np.full(k, req, np.int32), P[ok]))
+        return States.concat(parts)
 
     # -- per-state inputs of the GPU call (GetStateImagesUnifiedGPU, search_env.cpp:1577-1620) -------
     def _cost_type(self) -> int:
         return COST_DEPTH_6DOF
 
-    def _pose_labels(self, states) -> Optional[torch.Tensor]:
+    def _pose_labels(self, states: States) -> Optional[torch.Tensor]:
         """pose_segmentation_label: the state's required object id (6-DoF)."""
-        return torch.tensor([s[1] for s in states], dtype=torch.int32, device=self.device)
+        return torch.from_numpy(states.req.copy()).to(self.device)
 
-    def _obs_totals(self, states) -> np.ndarray:
+    def _obs_totals(self, states: States) -> np.ndarray:
         """pose_observed_points_total: segmented_observed_point_count of the label (6-DoF)."""
-        seg = np.append(self.segmented_count, 0.0)
-        return np.array([seg[min(s[1], len(seg) - 1)] for s in states], np.float32)
+        seg = np.append(self.segmented_count, 0.0).astype(np.float32)
+        return seg[np.minimum(states.req, len(seg) - 1)]
 
     def _pose_in_cam(self, states) -> np.ndarray:
         """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576): inv(cam_z_front) * T(state) *
         preprocess, vectorised over the states (model.chain_matmul_batch: index-order 4x4 products)."""
         cam_z_front = self.camera_pose @ CAM_TO_BODY
         cam_matrix = np.linalg.inv(cam_z_front)
-        if not states:
+        if not len(states):
             return init_from_eigen_batch(np.zeros((0, 4, 4)), 100)
-        P = np.stack([s[2] for s in states]).astype(np.float64)
-        mids = np.fromiter((s[0] for s in states), dtype=np.int64, count=len(states))
-        pre = np.stack(self.preprocess)[mids]
+        P = states.pose
+        pre = np.stack(self.preprocess)[states.model]
         mats = chain_matmul_batch(cam_matrix, pose_matrix_batch(P[:, :3], P[:, 3:7]), pre)
         return init_from_eigen_batch(mats, 100)
 
@@ -330,9 +362,9 @@ class ObjectRecognizer:
         adj_all = None
         icp_time = 0.0
         peak_mb = float(torch.cuda.max_memory_allocated(self.device)) / 1024.0 / 1024.0
-        if mine:
+        if len(mine):
             poses = torch.from_numpy(self._pose_in_cam(mine)).to(self.device)
-            pm = torch.tensor([s[0] for s in mine], dtype=torch.int32, device=self.device)
+            pm = torch.from_numpy(mine.model.copy()).to(self.device)
             pl = self._pose_labels(mine)
             tot = torch.from_numpy(self._obs_totals(mine)).to(self.device)
             cost_type = self._cost_type()
@@ -342,28 +374,23 @@ class ObjectRecognizer:
             df = torch.empty_like(rc)
             adj_all = poses.clone()
             iters = torch.zeros(n, dtype=torch.int32, device=self.device)
-            # the reference's gpu_batch_size loop (search_env.cpp:2504-2525); batches only bound memory here
-            bs = max(1, p.gpu_batch_size)
+            # The reference loops over gpu_batch_size batches (search_env.cpp:2504-2525) only to bound its
+            # per-call device allocations; the results are batch-invariant (the keys fold across batches, tests/
+            # test_gpu_fullsize.py::test_c2_permutation_and_chunking_invariance) and the context chunks GICP by
+            # its own scratch budget, so the whole shard goes down in one call.
             ti = time.perf_counter()
-            for b0 in range(0, n, bs):
-                b1 = min(n, b0 + bs)
-                sl = slice(b0, b1)
-                pls = pl[sl] if pl is not None else None
-                if p.icp_type == 3 and inp.use_icp:
-                    self.core.evaluate_icp(poses[sl], pm[sl], pls, tot[sl], cost_type=cost_type,
-                                           stride=p.gpu_stride, depth_factor=p.gpu_depth_factor,
-                                           sensor_resolution=p.sensor_resolution,
-                                           occlusion_threshold=p.gpu_occlusion_threshold, k=p.icp_k,
-                                           max_iterations=p.icp_max_iterations,
-                                           rotation_epsilon=p.icp_rotation_epsilon,
-                                           transformation_epsilon=p.icp_transformation_epsilon,
-                                           out=(adj_all[sl], iters[sl], rc[sl], oc[sl], df[sl]))
-                else:
-                    self.core.evaluate(poses[sl], pm[sl], pls, tot[sl], cost_type=cost_type,
-                                       stride=p.gpu_stride, depth_factor=p.gpu_depth_factor,
-                                       sensor_resolution=p.sensor_resolution,
-                                       occlusion_threshold=p.gpu_occlusion_threshold, out=(rc[sl], oc[sl], df[sl]))
-                self.core.select(rc[sl], oc[sl], pm[sl], K, index_base=lo + b0, keys=keys)
+            if p.icp_type == 3 and inp.use_icp:
+                self.core.evaluate_icp(poses, pm, pl, tot, cost_type=cost_type, stride=p.gpu_stride,
+                                       depth_factor=p.gpu_depth_factor, sensor_resolution=p.sensor_resolution,
+                                       occlusion_threshold=p.gpu_occlusion_threshold, k=p.icp_k,
+                                       max_iterations=p.icp_max_iterations, rotation_epsilon=p.icp_rotation_epsilon,
+                                       transformation_epsilon=p.icp_transformation_epsilon,
+                                       out=(adj_all, iters, rc, oc, df))
+            else:
+                self.core.evaluate(poses, pm, pl, tot, cost_type=cost_type, stride=p.gpu_stride,
+                                   depth_factor=p.gpu_depth_factor, sensor_resolution=p.sensor_resolution,
+                                   occlusion_threshold=p.gpu_occlusion_threshold, out=(rc, oc, df))
+            self.core.select(rc, oc, pm, K, index_base=lo, keys=keys)
             torch.cuda.synchronize(self.device)
             icp_time = time.perf_counter() - ti if (p.icp_type == 3 and inp.use_icp) else 0.0
             if p.icp_type == 3 and inp.use_icp:

@@ -37,7 +37,7 @@ import torch
 from ._native import COST_DEPTH_3DOF, COST_RGBD_3DOF
 from .model import pose_matrix
 from .recognizer import (CAM_TO_BODY, K_MESH_ADDITIVE_INFLATION, CameraIntrinsics, ModelMetaData,
-                         ObjectRecognizer, PerchParams, RecognitionInput, _dims, radius_counts)
+                         ObjectRecognizer, PerchParams, RecognitionInput, States, _dims, radius_counts)
 
 
 @dataclass
@@ -198,14 +198,17 @@ class TabletopRecognizer(ObjectRecognizer):
                                       for r in range(2)], 1)
         self.segmented_object_names = []
 
-    def generate_successor_states(self, inp: RecognitionInput = None):
-        states = []
+    def generate_successor_states(self, inp: RecognitionInput = None) -> States:
+        parts = []
         for ii, name in enumerate(self.model_names):
             dims = _dims(self.models[ii])
             sym = self.bank[name].symmetry_mode
-            states += grid_states(self.table, ii, dims, self.projected_xy,
-                                  self.params.min_neighbor_points_for_valid_pose, sym, self.device)
-        return states
+            st = grid_states(self.table, ii, dims, self.projected_xy,
+                             self.params.min_neighbor_points_for_valid_pose, sym, self.device)
+            if st:
+                parts.append(States(np.array([s[0] for s in st], np.int32), np.array([s[1] for s in st], np.int32),
+                                    np.stack([s[2] for s in st])))
+        return States.concat(parts, width=4)
 
     def _cost_type(self) -> int:
         return COST_RGBD_3DOF if getattr(self, "use_colour", False) else COST_DEPTH_3DOF
@@ -219,11 +222,12 @@ class TabletopRecognizer(ObjectRecognizer):
         if not self.params.use_cylinder_observed:
             return np.full(len(states), float(len(self.obs_xyz_host)), np.float32)
         out = np.empty(len(states), np.float32)
-        for i, (mid, _, p) in enumerate(states):
+        for mid in np.unique(states.model):
+            sel = states.model == mid
             dims = _dims(self.models[mid])
             r = inflation_factor(dims) * circumscribed_radius(dims)
-            out[i] = count_within(np.asarray(p[None, :2]), self.projected_xy, r, self.table.table_height,
-                                  self.device, cap=self.cam.width * self.cam.height)[0]  # max_nn = kNumPixels
+            out[sel] = count_within(states.pose[sel, :2], self.projected_xy, r, self.table.table_height,
+                                    self.device, cap=self.cam.width * self.cam.height)  # max_nn = kNumPixels
         return out
 
     def _pose_in_cam(self, states) -> np.ndarray:
@@ -231,13 +235,12 @@ class TabletopRecognizer(ObjectRecognizer):
         state, as yaw_pose_matrix; index-order 4x4 products, model.chain_matmul_batch)."""
         from .model import chain_matmul_batch, init_from_eigen_batch, pose_matrix_batch
         cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
-        if not states:
+        if not len(states):
             return init_from_eigen_batch(np.zeros((0, 4, 4)), 100)
-        xyzy = np.array([(p[0], p[1], p[2], p[3]) for _, _, p in states], dtype=np.float64)
+        xyzy = states.pose
         yaws = [normalize_angle_positive(float(y)) for y in xyzy[:, 3]]
         q = np.array([(0.0, 0.0, math.sin(y / 2.0), math.cos(y / 2.0)) for y in yaws])
-        mids = np.fromiter((s[0] for s in states), dtype=np.int64, count=len(states))
-        mats = chain_matmul_batch(cam_matrix, pose_matrix_batch(xyzy[:, :3], q), np.stack(self.preprocess)[mids])
+        mats = chain_matmul_batch(cam_matrix, pose_matrix_batch(xyzy[:, :3], q), np.stack(self.preprocess)[states.model])
         return init_from_eigen_batch(mats, 100)
 
     def localize(self, model_names: Sequence[str], depth: np.ndarray, camera_pose: np.ndarray,

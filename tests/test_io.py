@@ -115,3 +115,17 @@ def test_read_poses_txt_edge_cases(tmp_path):
         p.write_text(text)
         got = io.read_poses_txt(str(p))
         assert got.shape == want.shape and np.array_equal(got, want), name
+
+
+def test_read_poses_txt_cached_reparses_a_changed_file(tmp_path):
+    from perception_amd import io as pio
+    import os
+    p = str(tmp_path / "poses.txt")
+    rows = np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]])
+    pio.write_poses_txt(p, rows)
+    a = pio.read_poses_txt_cached(p)
+    assert np.array_equal(a, pio.read_poses_txt(p)) and pio.read_poses_txt_cached(p) is a
+    pio.write_poses_txt(p, np.vstack([rows, rows * 2]))
+    os.utime(p, ns=(os.stat(p).st_atime_ns, os.stat(p).st_mtime_ns + 1000))
+    b = pio.read_poses_txt_cached(p)
+    assert b.shape == (2, 7) and not b.flags.writeable

@@ -24,7 +24,7 @@ from perception_amd.recognizer import (CAM_TO_BODY, CameraIntrinsics, ModelMetaD
 def loop_pose_in_cam(self, states):
     cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
     mats = np.empty((len(states), 4, 4))
-    for i, (mid, _, p) in enumerate(states):
+    for i, (mid, _, p) in enumerate(states):  # States iterates as (model, required, pose) tuples
         mats[i] = cam_matrix @ pose_matrix(p[:3], p[3:7]) @ self.preprocess[mid]
     return init_from_eigen_batch(mats, 100)
 
