@@ -35,12 +35,14 @@ namespace {
 constexpr int kGThreads = 256;
 constexpr int kMaxK = 16;
 // Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only):
-// [0] nearest-target search, [1] covariance loads + contributions, [2] wave reduction, [3] lane-0 solve.
+// [0] linearisation (search + contributions), [2] wave reduction, [3] LM iteration, which splits into [4] damped
+// solves, [5] se3_exp + compose, [6] the trials' error sums and their reduction, [7] the decisions.
 // Each wave sums its clocks in registers and adds them once at exit (no atomics inside the loop); each
 // clock read is ordered after its phase's last result by an asm input dependency.
 #ifdef PCORE_GICP_PROFILE
-__device__ unsigned long long g_gicp_prof[4];
-#define GPROF_DECL unsigned long long gp_acc[4] = {0, 0, 0, 0}
+constexpr int kGprof = 8;
+__device__ unsigned long long g_gicp_prof[kGprof];
+#define GPROF_DECL unsigned long long gp_acc[kGprof] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define GPROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
 #define GPROF_TD(v, dep)                                                                   \
     unsigned long long v;                                                                  \
@@ -48,13 +50,17 @@ __device__ unsigned long long g_gicp_prof[4];
 #define GPROF_ADD(k, a, b) gp_acc[k] += (unsigned long long)((b) - (a))
 #define GPROF_FLUSH \
     if (lane == 0)  \
-        for (int k_ = 0; k_ < 4; k_++) atomicAdd(&g_gicp_prof[k_], gp_acc[k_])
+        for (int k_ = 0; k_ < kGprof; k_++) atomicAdd(&g_gicp_prof[k_], gp_acc[k_])
+#define GPROF_PARAM , unsigned long long (&gp_acc)[kGprof]
+#define GPROF_ARG , gp_acc
 #else
 #define GPROF_DECL
 #define GPROF_T(v)
 #define GPROF_TD(v, dep)
 #define GPROF_ADD(k, a, b)
 #define GPROF_FLUSH
+#define GPROF_PARAM
+#define GPROF_ARG
 #endif
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -581,15 +587,18 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
 template <typename CorrPtr>
 __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double& lambda, const float4* src,
                                             CorrPtr corr, const double* mah, const float4* tgt, int ns, int lane,
-                                            double rot_eps, double trans_eps) {
+                                            double rot_eps, double trans_eps GPROF_PARAM) {
     const double y0 = uniform_d(sys[gicpm::kErr]);
     if (lambda < 0.0) lambda = uniform_d(gicpm::lm_init_lambda(sys));
     double nu = 2.0;
     for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
+        GPROF_T(p0);
         double d[6];
         gicpm::lm_solve(sys, lambda, d);
 #pragma unroll
         for (int a = 0; a < 6; a++) d[a] = uniform_d(d[a]);
+        GPROF_TD(p1, d[5]);
+        GPROF_ADD(4, p0, p1);
         if (!gicpm::all_finite6(d)) return gicpm::kLmFailed;  // guard: a non-finite system
         double Rd[3][3], td[3];
         gicpm::se3_exp(d, Rd, td);
@@ -601,6 +610,8 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
             for (int c = 0; c < 3; c++) xi.R[r][c] = uniform_d(xi.R[r][c]);
             xi.t[r] = uniform_d(xi.t[r]);
         }
+        GPROF_TD(p2, xi.t[2]);
+        GPROF_ADD(5, p1, p2);
         // the error at x_i (FastGICP::compute_error: this iteration's correspondences and Mahalanobis matrices)
         double ea = 0.0;
         for (int i0 = 0; i0 < ns; i0 += 64) {
@@ -625,7 +636,11 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) ea = ea + __shfl_down(ea, off, 64);
         const double yi = uniform_d(ea);  // lane 0: the tree's sum
+        GPROF_TD(p3, yi);
+        GPROF_ADD(6, p2, p3);
         const double rho = uniform_d(gicpm::lm_rho(sys, lambda, d, y0, yi));
+        GPROF_TD(p4, rho);
+        GPROF_ADD(7, p3, p4);
         if (rho < 0.0) {
             if (gicpm::is_converged(Rd, td, rot_eps, trans_eps)) return gicpm::kLmConverged;
             lambda = nu * lambda;
@@ -753,7 +768,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 const double* sys = lds_tree_sum(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
                 const int st = lm_iteration(sys, x, lambda, P.src, P.corr, P.mah, P.tgt, P.ns, lane, g.rot_eps,
-                                            g.trans_eps);
+                                            g.trans_eps GPROF_ARG);
                 GPROF_TD(t_d, st);
                 GPROF_ADD(2, t_b, t_c);
                 GPROF_ADD(3, t_c, t_d);
@@ -827,8 +842,11 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                                            P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, acc);
                 }
                 const double* sys = lds_tree_sum(acc, sRed, lane);
+#ifdef PCORE_GICP_PROFILE
+                unsigned long long gp_acc[kGprof] = {0, 0, 0, 0, 0, 0, 0, 0};  // not reported
+#endif
                 const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, g.rot_eps,
-                                            g.trans_eps);
+                                            g.trans_eps GPROF_ARG);
                 if (lane == 0) {
                     sFlag = st;
 #pragma unroll
@@ -859,9 +877,9 @@ constexpr size_t kGicpWideMaxLds = 96 * 1024;  // correspondence buffer: src_cap
 
 #ifdef PCORE_GICP_PROFILE
 extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gicp_prof), sizeof(unsigned long long) * 4);
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gicp_prof), sizeof(unsigned long long) * kGprof);
     if (e == hipSuccess && reset) {
-        const unsigned long long z[4] = {0, 0, 0, 0};
+        const unsigned long long z[kGprof] = {0, 0, 0, 0, 0, 0, 0, 0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_gicp_prof), z, sizeof(z));
     }
     return e == hipSuccess ? 0 : 1;

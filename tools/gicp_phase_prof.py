@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Per-phase shader clocks of gicp_kernel (build with -DPCORE_GICP_PROFILE, load with PCORE_LIB):
-scan+contributions / 28-term wave reduction / lane-0 solve, per pose-iteration."""
+linearisation (correspondence search + contributions) / 28-term wave reduction / LM iteration (damped solves,
+se3_exp, the trials' error sums), per pose-iteration."""
 import ctypes
 import os
 import sys
@@ -26,7 +27,7 @@ def main():
     lib = _native.load()
     fn = lib.pcore_debug_gicp_profile
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 4)()
+    buf = (ctypes.c_ulonglong * 8)()
     w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
     torch.cuda.synchronize()
     fn(buf, 1)
@@ -35,10 +36,11 @@ def main():
     torch.cuda.synchronize()
     fn(buf, 0)
     it = iters.cpu().numpy()
-    total = int(it.sum()) + int((it < 150).sum())  # + the final non-updating solve
-    names = ["nn search", "contrib", "reduction", "solve"]
+    total = int(it.sum())  # one linearisation + one LM iteration per counted iteration
+    names = ["linearise", "-", "reduction", "LM iteration", "  solves", "  se3 + compose", "  trial errors",
+             "  decisions"]
     print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())
-    for k in range(4):
+    for k in range(8):
         print(f"{names[k]:14s} {buf[k] / max(total, 1):10.0f} clk per pose-iteration")
 
 
