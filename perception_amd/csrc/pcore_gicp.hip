@@ -520,6 +520,42 @@ __device__ __forceinline__ const double* lds_tree_sum(const double (&acc)[gicpm:
     return out;
 }
 
+// Lane 0's value of the wave shuffle-down tree x <- x + shfl_down(x, off), off = 32 ... 1 (the oracle's reduction
+// order: ((x0 + x32) + (x16 + x48)) + ...), without the LDS pipe: the 32- and 16-lane levels through
+// v_permlane32_swap / v_permlane16_swap (lane l < 32 receives lane l + 32, lane l of an even row lane l + 16), the
+// 8 ... 1 levels through DPP row_shl (lane l of a row receives lane l + off).  Other lanes end with partial sums
+// (read lane 0).
+__device__ __forceinline__ double wave_sum_lane0(double x) {
+    auto halves = [](double v, unsigned& lo, unsigned& hi) {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+        lo = (unsigned)u;
+        hi = (unsigned)(u >> 32);
+    };
+    auto join = [](unsigned lo, unsigned hi) {
+        return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+    };
+    unsigned lo, hi;
+    halves(x, lo, hi);
+    x = x + join(__builtin_amdgcn_permlane32_swap(lo, lo, false, false)[1],
+                 __builtin_amdgcn_permlane32_swap(hi, hi, false, false)[1]);
+    halves(x, lo, hi);
+    x = x + join(__builtin_amdgcn_permlane16_swap(lo, lo, false, false)[1],
+                 __builtin_amdgcn_permlane16_swap(hi, hi, false, false)[1]);
+    halves(x, lo, hi);
+    x = x + join(__builtin_amdgcn_update_dpp(0u, lo, 0x108, 0xf, 0xf, false),   // row_shl:8
+                 __builtin_amdgcn_update_dpp(0u, hi, 0x108, 0xf, 0xf, false));
+    halves(x, lo, hi);
+    x = x + join(__builtin_amdgcn_update_dpp(0u, lo, 0x104, 0xf, 0xf, false),   // row_shl:4
+                 __builtin_amdgcn_update_dpp(0u, hi, 0x104, 0xf, 0xf, false));
+    halves(x, lo, hi);
+    x = x + join(__builtin_amdgcn_update_dpp(0u, lo, 0x102, 0xf, 0xf, false),   // row_shl:2
+                 __builtin_amdgcn_update_dpp(0u, hi, 0x102, 0xf, 0xf, false));
+    halves(x, lo, hi);
+    x = x + join(__builtin_amdgcn_update_dpp(0u, lo, 0x101, 0xf, 0xf, false),   // row_shl:1
+                 __builtin_amdgcn_update_dpp(0u, hi, 0x101, 0xf, 0xf, false));
+    return x;
+}
+
 // the pose's state in double: rotation and translation of the GICP transform (source -> target, metres)
 struct Xform {
     double R[3][3];
@@ -633,9 +669,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
                 ea += gicpm::mahal_err(M6, e);
             }
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) ea = ea + __shfl_down(ea, off, 64);
-        const double yi = uniform_d(ea);  // lane 0: the tree's sum
+        const double yi = uniform_d(wave_sum_lane0(ea));  // lane 0: the tree's sum
         GPROF_TD(p3, yi);
         GPROF_ADD(6, p2, p3);
         const double rho = uniform_d(gicpm::lm_rho(sys, lambda, d, y0, yi));

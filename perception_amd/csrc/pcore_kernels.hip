@@ -670,12 +670,20 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
                 // ballot round each; full 64-record batches are flushed after every round (<= 127 pending)
                 const bool qd = nk > 0 && nk <= kSmallK;
                 const uint64_t bq = __ballot(qd);
+#if PCORE_RING_DISCARD
                 {  // the record keeps the whole triangle slot word (the flush reads its 27 slot bits); lanes with
                    // nothing to queue write the discard record instead of branching around the store
                     const int slot = qd ? (rec_total + mbcnt64(bq)) & (kRecCap - 1) : kRecCap;
                     ring[slot] = make_uint2(ct, pos);
                     if (IDPASS) ring_id[slot] = cidt;
                 }
+#else
+                if (qd) {  // the record keeps the whole triangle slot word (the flush reads its 27 slot bits)
+                    const int slot = (rec_total + mbcnt64(bq)) & (kRecCap - 1);
+                    ring[slot] = make_uint2(ct, pos);
+                    if (IDPASS) ring_id[slot] = cidt;
+                }
+#endif
                 rec_total += __popcll(bq);
                 while (rec_total - rec_done >= kWave) flush(kWave);  // full batches only
                 if (__ballot(qd && nk > 1)) {

@@ -239,6 +239,7 @@ class ObjectRecognizer:
         self.model_names: List[str] = []
         self.preprocess: List[np.ndarray] = []
         self.last_stats = EnvStats()
+        self.last_timing: dict = {}
 
     # -- ObjectRecognizer::SetStaticInput -> LoadObjFiles (search_env.cpp:253-307) -----------------
     def set_static_input(self, model_names: Sequence[str], six_dof: bool = True):
@@ -351,6 +352,7 @@ class ObjectRecognizer:
         t0 = time.perf_counter()
         p = self.params
         states = self.generate_successor_states(inp)
+        t_states = time.perf_counter()
         n_total = len(states)
         K = len(self.models)
         world, rank = 1, 0
@@ -361,7 +363,9 @@ class ObjectRecognizer:
         keys = torch.full((K,), PCORE_KEY_NONE, dtype=torch.int64, device=self.device)
         adj_all = None
         icp_time = 0.0
+        gpu_s = 0.0
         peak_mb = float(torch.cuda.max_memory_allocated(self.device)) / 1024.0 / 1024.0
+        t_build = t_states
         if len(mine):
             poses = torch.from_numpy(self._pose_in_cam(mine)).to(self.device)
             pm = torch.from_numpy(mine.model.copy()).to(self.device)
@@ -374,6 +378,7 @@ class ObjectRecognizer:
             df = torch.empty_like(rc)
             adj_all = poses.clone()
             iters = torch.zeros(n, dtype=torch.int32, device=self.device)
+            t_build = time.perf_counter()
             # The reference loops over gpu_batch_size batches (search_env.cpp:2504-2525) only to bound its
             # per-call device allocations; the results are batch-invariant (the keys fold across batches, tests/
             # test_gpu_fullsize.py::test_c2_permutation_and_chunking_invariance) and the context chunks GICP by
@@ -392,7 +397,8 @@ class ObjectRecognizer:
                                    occlusion_threshold=p.gpu_occlusion_threshold, out=(rc, oc, df))
             self.core.select(rc, oc, pm, K, index_base=lo, keys=keys)
             torch.cuda.synchronize(self.device)
-            icp_time = time.perf_counter() - ti if (p.icp_type == 3 and inp.use_icp) else 0.0
+            gpu_s = time.perf_counter() - ti
+            icp_time = gpu_s if (p.icp_type == 3 and inp.use_icp) else 0.0
             if p.icp_type == 3 and inp.use_icp:
                 peak_mb = self.core.stats(reset=True)["peak_memory_usage"]  # gpu_stats.peak_memory_usage (MB)
             self._last_costs = (rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy())
@@ -417,6 +423,11 @@ class ObjectRecognizer:
             q = matrix_to_quat_xyzw(Tm[:3, :3])
             cont = np.concatenate([Tm[:3, 3], q])
             results.append((m, int(cost[m]), int(idx[m]), cont))
+        t_end = time.perf_counter()
+        # host-side breakdown of the last search (seconds): successor states (poses.txt + IsValidPose), per-state
+        # inputs of the GPU call, the GPU search (launch .. synchronise, incl. the exchange), results
+        self.last_timing = {"states_s": t_states - t0, "inputs_s": t_build - t_states,
+                            "gpu_s": gpu_s, "total_s": t_end - t0}
         self.last_stats = EnvStats(scenes_rendered=n_total, scenes_valid=0, time=time.perf_counter() - t0,
                                    icp_time=icp_time, peak_gpu_mem=peak_mb)
         return results
@@ -425,8 +436,11 @@ class ObjectRecognizer:
     def localize_objects_greedy_render(self, inp: RecognitionInput) -> LocalizationResult:
         if not self.models or self.model_names != list(inp.model_names):
             self.set_static_input(inp.model_names, six_dof=inp.use_external_pose_list == 1)
+        t0 = time.perf_counter()
         self.set_input(inp)
+        t_input = time.perf_counter() - t0
         res = self.compute_greedy_render_poses(inp)
+        self.last_timing["set_input_s"] = t_input
         out = LocalizationResult([], [], [], [], [], [], self.last_stats)
         for m, cost, idx, cont in res:
             # GetRawModelToSceneTransform (object_model.cpp:502-510): ContPose transform * preprocessing

@@ -219,3 +219,126 @@ def test_c3_scene_icp_sweep_bit_exact_vs_oracle():
     assert np.array_equal(_bits(oc.cpu().numpy()), _bits(ooc))
     assert np.array_equal(_bits(df.cpu().numpy()), _bits(odf))
     assert oit.max() == 150 and oit.min() < 20  # converging and non-converging poses both present
+
+
+# ---- true per-GPU sizes of C3, C4 and C5 (BASELINE.json configs[2..4]) ----------------------------------
+
+def _label_ranges(w):
+    xyz = w.obs_xyz.cpu().numpy()
+    lab = w.obs_label.cpu().numpy()
+    order = np.argsort(lab, kind="stable")
+    oxyz, olab = xyz[order], lab[order]
+    nl = int(olab.max()) + 1
+    ls = np.array([np.searchsorted(olab, L, "left") for L in range(nl)], np.int32)
+    le = np.array([np.searchsorted(olab, L, "right") for L in range(nl)], np.int32)
+    return oxyz, ls, le
+
+
+def _check_invariance(w, fn, outs, chunks):
+    """Permutation and chunking invariance of per-pose outputs over the whole batch (poses are independent)."""
+    n = int(w.poses.shape[0])
+    perm = torch.from_numpy(np.random.default_rng(7).permutation(n)).to(w.poses.device)
+    p = perm.cpu().numpy()
+    got = fn(w.poses[perm].contiguous(), w.pose_model[perm].contiguous(), w.pose_label[perm].contiguous(),
+             w.pose_obs_total[perm].contiguous())
+    for g, o in zip(got, outs):
+        assert np.array_equal(g.cpu().numpy().view(np.uint32), o[p].view(np.uint32))
+    parts = [fn(w.poses[lo:hi], w.pose_model[lo:hi], w.pose_label[lo:hi], w.pose_obs_total[lo:hi])
+             for lo, hi in chunks]
+    for k, o in enumerate(outs):
+        cat = np.concatenate([q[k].cpu().numpy() for q in parts])
+        assert np.array_equal(cat.view(np.uint32), o.view(np.uint32))
+
+
+def _check_selection(w, rc, oc):
+    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=w.poses.device)
+    w.core.select(torch.from_numpy(rc).to(w.poses.device), torch.from_numpy(oc).to(w.poses.device), w.pose_model,
+                  w.num_models, keys=keys)
+    cost, idx = decode_keys(keys)
+    ocost, oidx = oracle.select(rc, oc, w.pose_model.cpu().numpy(), w.num_models)
+    assert np.array_equal(idx, oidx) and np.array_equal(cost, ocost)
+    return cost, idx
+
+
+def test_c3_full_50k_icp_subset_and_properties(monkeypatch):
+    """C3 at its full size: 5 objects x 10,000 candidates with GICP in one call.  A seeded subset of 200 poses (and
+    every ground-truth candidate) equals the oracle's GICP + re-score bit for bit (adjusted poses, iterations,
+    costs); over all 50k poses the outputs are invariant under a permutation of the batch and under the context's
+    chunking (a 1 GiB scratch budget: ~26 chunks); the per-model selection equals the oracle rule over the GPU
+    costs."""
+    names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
+    w = workloads.build(names=names, poses_per_model=10000)
+
+    def icp(poses, pm, pl, tot):
+        return w.core.evaluate_icp(poses, pm, pl, tot, stride=w.stride)
+
+    outs = [x.cpu().numpy() for x in icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total)]
+    adj, its, rc, oc, df = outs
+    assert len(rc) == 50000
+    idx = np.sort(np.random.default_rng(33).choice(len(rc), 200, replace=False))
+    idx = np.unique(np.concatenate([idx, w.gt_index]))
+    sc = w.scene
+    oxyz, ls, le = _label_ranges(w)
+    cov = np.zeros((len(oxyz), 6))
+    for L in range(len(ls)):
+        if le[L] > ls[L]:
+            cov[ls[L]:le[L]] = oracle.covariances(oxyz[ls[L]:le[L]])
+    pm = w.pose_model.cpu().numpy()
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, w.poses.cpu().numpy()[idx], pm[idx], pm[idx], sc.width, sc.height,
+        sc.proj, sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, cov, ls, le,
+        w.pose_obs_total.cpu().numpy()[idx], 2, True, 0.01)
+    assert np.array_equal(its[idx], oit)
+    assert np.array_equal(_bits(adj[idx]), _bits(oadj))
+    assert np.array_equal(_bits(rc[idx]), _bits(orc))
+    assert np.array_equal(_bits(oc[idx]), _bits(ooc))
+    assert np.array_equal(_bits(df[idx]), _bits(odf))
+    monkeypatch.setenv("PCORE_ICP_SCRATCH_GIB", "1")
+    _check_invariance(w, icp, outs, ((0, 17), (17, 25000), (25000, 50000)))
+    monkeypatch.delenv("PCORE_ICP_SCRATCH_GIB")
+    _check_selection(w, rc, oc)
+
+
+def test_c4_share_25k_21_models_subset_and_properties():
+    """C4's per-GPU share at its full size: 21 models x 1,190 candidates (24,990 poses, the 200k grid over 8 GPUs).
+    A seeded subset of 105 poses equals the oracle; the batch is permutation and chunk invariant; every model's
+    winner equals the oracle rule over the GPU costs and is its ground-truth candidate."""
+    w = workloads.build(names=list(syn.YCB_PROXIES), poses_per_model=1190)
+
+    def ev(poses, pm, pl, tot):
+        return w.core.evaluate(poses, pm, pl, tot, stride=w.stride)
+
+    outs = [x.cpu().numpy() for x in ev(w.poses, w.pose_model, w.pose_label, w.pose_obs_total)]
+    rc, oc, df = outs
+    assert len(rc) == 24990 and w.num_models == 21
+    sub = np.sort(np.random.default_rng(9).choice(len(rc), 105, replace=False))
+    orc, ooc, odf = _oracle_subset(w, sub)
+    assert np.array_equal(_bits(rc[sub]), _bits(orc))
+    assert np.array_equal(_bits(oc[sub]), _bits(ooc))
+    assert np.array_equal(_bits(df[sub]), _bits(odf))
+    _check_invariance(w, ev, outs, ((0, 1), (1, 12345), (12345, 24990)))
+    cost, idx = _check_selection(w, rc, oc)
+    assert list(idx) == list(w.gt_index)
+
+
+def test_c5_share_125k_1280x720_subset_and_properties():
+    """C5's per-GPU share at its full size: 125,000 poses of the fine grid at 1280x720.  A seeded subset of 40 poses
+    (and the ground truth) equals the oracle; the whole batch is permutation and chunk invariant; the selection
+    equals the oracle rule over the GPU costs and picks the ground truth."""
+    w = workloads.build(poses_per_model=125000, cam=syn.CAM_1280)
+
+    def ev(poses, pm, pl, tot):
+        return w.core.evaluate(poses, pm, pl, tot, stride=w.stride)
+
+    outs = [x.cpu().numpy() for x in ev(w.poses, w.pose_model, w.pose_label, w.pose_obs_total)]
+    rc, oc, df = outs
+    assert len(rc) == 125000
+    sub = np.sort(np.random.default_rng(5).choice(len(rc), 40, replace=False))
+    sub = np.unique(np.concatenate([sub, w.gt_index]))
+    orc, ooc, odf = _oracle_subset(w, sub)
+    assert np.array_equal(_bits(rc[sub]), _bits(orc))
+    assert np.array_equal(_bits(oc[sub]), _bits(ooc))
+    assert np.array_equal(_bits(df[sub]), _bits(odf))
+    _check_invariance(w, ev, outs, ((0, 62500), (62500, 125000)))
+    cost, idx = _check_selection(w, rc, oc)
+    assert int(idx[0]) == w.gt_index[0]

@@ -93,6 +93,16 @@ def run(name, names, per_model, cam, icp, steps, warmup):
         errs_adds.append(float(s_[0]))
     res["add_m"] = errs_add
     res["adds_m"] = errs_adds
+    # the ground-truth candidates' own final costs (search_env.cpp:2022-2048 int conversion and filter), to explain a
+    # winner other than the ground truth: a symmetric proxy (cylinder) renders the same at other yaws (ADD-S ~ 0)
+    rcs, ocs = out[-3].cpu().numpy() if icp else out[0].cpu().numpy(), out[-2].cpu().numpy() if icp else out[1].cpu().numpy()
+    gt_cost = []
+    for g in w.gt_index:
+        r, o = float(rcs[g]), float(ocs[g])
+        gt_cost.append({"cost": int(np.float32(r) + np.float32(o)) if r >= 0 else -1, "rc": r, "oc": o,
+                        "passes_filter": bool(r >= 0 and abs(int(r) - int(o)) < 30)})
+    res["gt_candidate"] = gt_cost
+    res["shapes"] = [syn.YCB_PROXIES[nm][0] if nm in syn.YCB_PROXIES else "?" for nm in names]
     res["adds_auc"] = metrics.compute_pose_metrics(np.array(errs_adds))["auc"]
     print(json.dumps(res), flush=True)
     del w

@@ -67,7 +67,10 @@ def main():
         dp = time.perf_counter() - t1
         print({"icp": icp, "states": len(states), "localize_s": round(dt, 4), "search_s": round(rec.last_stats.time, 4),
                "icp_s": round(rec.last_stats.icp_time, 4), "pose_building_s": round(dp, 4),
-               "loop_poses": a.loop_poses, "found": len(res.model_names)}, flush=True)
+               "loop_poses": a.loop_poses, "found": len(res.model_names),
+               "poses_per_s": round(len(states) / dt, 1),
+               "timing": {k: (round(v, 5) if v is not None else None) for k, v in rec.last_timing.items()}},
+              flush=True)
 
 
 if __name__ == "__main__":
