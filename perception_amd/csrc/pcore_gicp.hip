@@ -35,7 +35,7 @@ namespace {
 constexpr int kGThreads = 256;
 constexpr int kMaxK = 16;
 // Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only):
-// [0] linearisation (search + contributions), [2] wave reduction, [3] LM iteration, which splits into [4] damped
+// [0] correspondence search, [1] contributions (+ M stores), [2] wave reduction, [3] LM iteration, which splits into [4] damped
 // solves, [5] se3_exp + compose, [6] the trials' error sums and their reduction, [7] the decisions.
 // Each wave sums its clocks in registers and adds them once at exit (no atomics inside the loop); each
 // clock read is ordered after its phase's last result by an asm input dependency.
@@ -61,6 +61,10 @@ __device__ unsigned long long g_gicp_prof[kGprof];
 #define GPROF_FLUSH
 #define GPROF_PARAM
 #define GPROF_ARG
+#endif
+
+#ifndef PCORE_LM_PREFETCH
+#define PCORE_LM_PREFETCH 0  // A/B: the first round of the trials' error inputs loaded before the first solve
 #endif
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -580,7 +584,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
                                                 const float4* src, const double* scov, const float4* tgt,
                                                 const double* tcov, int ns, int i, bool use_grid, const LabelGrid& G,
                                                 const GicpArgs& g, const float* tquads, int nt, int j_in,
-                                                int32_t* corr, double* mah, double (&acc)[gicpm::kTerms]) {
+                                                int32_t* corr, double* mah, double (&acc)[gicpm::kTerms] GPROF_PARAM) {
+    GPROF_T(t_s0);
     const bool act = i < ns;
     const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     int j = j_in;
@@ -598,6 +603,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
         }
         if (act) corr[i] = j;
     }
+    GPROF_TD(t_s1, j);
+    GPROF_ADD(0, t_s0, t_s1);
     if (act && j >= 0) {
         const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
         double q[3];
@@ -614,6 +621,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
         m2[1] = make_double2(M6[2], M6[3]);
         m2[2] = make_double2(M6[4], M6[5]);
     }
+    GPROF_TD(t_s2, acc[gicpm::kErr]);
+    GPROF_ADD(1, t_s1, t_s2);
 }
 
 // One Levenberg-Marquardt iteration of one wave (LsqRegistration::step_lm) on the reduced system `sys` (28 sums in
@@ -627,6 +636,19 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
     const double y0 = uniform_d(sys[gicpm::kErr]);
     if (lambda < 0.0) lambda = uniform_d(gicpm::lm_init_lambda(sys));
     double nu = 2.0;
+#if PCORE_LM_PREFETCH
+    // the first round's inputs of the trials' error sums, loaded before the first solve (they do not depend on it)
+    const int pf_j = lane < ns ? corr[lane] : -1;
+    float4 pf_s = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pf_t = pf_s;
+    double pf_m[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (pf_j >= 0) {
+        pf_s = src[lane];
+        pf_t = tgt[pf_j];
+        const double2* m2 = reinterpret_cast<const double2*>(mah + (size_t)6 * lane);
+        const double2 a = m2[0], b = m2[1], c = m2[2];
+        pf_m[0] = a.x; pf_m[1] = a.y; pf_m[2] = b.x; pf_m[3] = b.y; pf_m[4] = c.x; pf_m[5] = c.y;
+    }
+#endif
     for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
         GPROF_T(p0);
         double d[6];
@@ -649,24 +671,30 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
         GPROF_TD(p2, xi.t[2]);
         GPROF_ADD(5, p1, p2);
         // the error at x_i (FastGICP::compute_error: this iteration's correspondences and Mahalanobis matrices)
+        auto err_of = [&](const float4& sp, const float4& tj, const double (&M6)[6]) {
+            const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+            double e[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
+                e[r] = (double)(r == 0 ? tj.x : r == 1 ? tj.y : tj.z) - q;
+            }
+            return gicpm::mahal_err(M6, e);
+        };
         double ea = 0.0;
-        for (int i0 = 0; i0 < ns; i0 += 64) {
+        int i0 = 0;
+#if PCORE_LM_PREFETCH
+        if (pf_j >= 0) ea += err_of(pf_s, pf_t, pf_m);
+        i0 = 64;
+#endif
+        for (; i0 < ns; i0 += 64) {
             const int i = i0 + lane;
             const int j = i < ns ? corr[i] : -1;
             if (j >= 0) {
-                const float4 sp = src[i];
-                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-                const float4 tj = tgt[j];
-                double e[3];
-#pragma unroll
-                for (int r = 0; r < 3; r++) {
-                    const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
-                    e[r] = (double)(r == 0 ? tj.x : r == 1 ? tj.y : tj.z) - q;
-                }
                 const double2* m2 = reinterpret_cast<const double2*>(mah + (size_t)6 * i);
                 const double2 a = m2[0], b = m2[1], c = m2[2];
                 const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-                ea += gicpm::mahal_err(M6, e);
+                ea += err_of(src[i], tgt[j], M6);
             }
         }
         const double yi = uniform_d(wave_sum_lane0(ea));  // lane 0: the tree's sum
@@ -791,13 +819,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 double acc[gicpm::kTerms];
 #pragma unroll
                 for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-                for (int i0 = 0; i0 < P.ns; i0 += 64) {
-                    GPROF_T(t_r0);
+                for (int i0 = 0; i0 < P.ns; i0 += 64)
                     linearize_round<true>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
-                                          P.tquads, P.nt, -1, P.corr, P.mah, acc);
-                    GPROF_TD(t_r1, acc[gicpm::kErr]);
-                    GPROF_ADD(0, t_r0, t_r1);
-                }
+                                          P.tquads, P.nt, -1, P.corr, P.mah, acc GPROF_ARG);
                 GPROF_T(t_b);
                 const double* sys = lds_tree_sum(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
@@ -867,18 +891,18 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
             }
             __syncthreads();
             if (wave == 0) {
+#ifdef PCORE_GICP_PROFILE
+                unsigned long long gp_acc[kGprof] = {0, 0, 0, 0, 0, 0, 0, 0};  // not reported
+#endif
                 double acc[gicpm::kTerms];
 #pragma unroll
                 for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
                 for (int i0 = 0; i0 < P.ns; i0 += 64) {
                     const int i = i0 + lane;
                     linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
-                                           P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, acc);
+                                           P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, acc GPROF_ARG);
                 }
                 const double* sys = lds_tree_sum(acc, sRed, lane);
-#ifdef PCORE_GICP_PROFILE
-                unsigned long long gp_acc[kGprof] = {0, 0, 0, 0, 0, 0, 0, 0};  // not reported
-#endif
                 const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, g.rot_eps,
                                             g.trans_eps GPROF_ARG);
                 if (lane == 0) {

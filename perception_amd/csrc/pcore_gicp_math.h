@@ -104,6 +104,46 @@ constexpr int kErr = 27;
 // index of H[a][a] in the upper triangle
 PCORE_GHD constexpr int hdiag(int a) { return a * 6 - (a * (a - 1)) / 2; }
 
+// Lane-parallel evaluation of a few uniform operations (device only).  The LM step is uniform work that every
+// lane of the wave repeats; where it holds several independent IEEE divisions (a pivot column of the LDLT, the
+// pseudo-inverse of D, se3_exp's three quotients) or several sin / cos, lane i evaluates the i-th one in a single
+// instruction sequence and the results return through v_readlane.  Every lane still performs the same IEEE
+// operation on the same operands as the scalar code, so the results are bit-identical to the host's (the oracle
+// runs the scalar path).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PCORE_LANE_PAR 1
+__device__ __forceinline__ int lane_index() {
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+template <int LANE>
+__device__ __forceinline__ double read_lane_d(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, LANE);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), LANE);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// q[i] = num[i] / den[i] for i < N, one division sequence across lanes 0..N-1
+template <int N>
+__device__ __forceinline__ void lane_div(const double (&num)[N], const double (&den)[N], double (&q)[N]) {
+    const int l = lane_index();
+    double a = num[0], b = den[0];
+PCORE_UNROLL
+    for (int i = 1; i < N; i++) {
+        a = l == i ? num[i] : a;
+        b = l == i ? den[i] : b;
+    }
+    const double r = a / b;
+    if constexpr (N > 0) q[0] = read_lane_d<0>(r);
+    if constexpr (N > 1) q[1] = read_lane_d<1>(r);
+    if constexpr (N > 2) q[2] = read_lane_d<2>(r);
+    if constexpr (N > 3) q[3] = read_lane_d<3>(r);
+    if constexpr (N > 4) q[4] = read_lane_d<4>(r);
+    if constexpr (N > 5) q[5] = read_lane_d<5>(r);
+}
+#else
+#define PCORE_LANE_PAR 0
+#endif
+
 // e^T M e with M given by its upper triangle (xx, xy, xz, yy, yz, zz): Me row by row, then the dot product
 PCORE_GHD double mahal_err(const double (&M6)[6], const double (&e)[3]) {
     const double me0 = M6[0] * e[0] + M6[1] * e[1] + M6[2] * e[2];
@@ -265,8 +305,23 @@ PCORE_UNROLL
             break;
         }
         if (valid) {
+#if PCORE_LANE_PAR
+            if (k < 5) {
+                constexpr int MAXN = 5;
+                double num[MAXN], den[MAXN], q[MAXN];
+PCORE_UNROLL
+                for (int i = 0; i < MAXN; i++) {
+                    num[i] = k + 1 + i < 6 ? A[k + 1 + i < 6 ? k + 1 + i : 5][k] : 0.0;
+                    den[i] = akk;
+                }
+                lane_div<MAXN>(num, den, q);
+PCORE_UNROLL
+                for (int i = k + 1; i < 6; i++) A[i][k] = q[i - k - 1];
+            }
+#else
 PCORE_UNROLL
             for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
+#endif
         }
     }
     double x[6];
@@ -287,11 +342,22 @@ PCORE_UNROLL
     for (int j = 0; j < 6; j++)
 PCORE_UNROLL
         for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
+#if PCORE_LANE_PAR
+    {
+        double Dd[6], q[6];
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) Dd[i] = A[i][i];
+        lane_div<6>(x, Dd, q);
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) x[i] = __builtin_fabs(Dd[i]) > 2.2250738585072014e-308 ? q[i] : 0.0;
+    }
+#else
 PCORE_UNROLL
     for (int i = 0; i < 6; i++) {
         const double Di = A[i][i];
         x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
     }
+#endif
 PCORE_UNROLL
     for (int i = 4; i >= 0; i--) {
         double s = A[i + 1][i] * x[i + 1];
@@ -314,16 +380,33 @@ PCORE_UNROLL
 PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]) {
     const double w0 = a[0], w1 = a[1], w2 = a[2];
     const double theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
+    const double theta = __builtin_sqrt(theta_sq);  // so3_exp's and se3_exp's sqrt(omega . omega)
+#if PCORE_LANE_PAR
+    // the four sin / cos on lanes 0..3 and the three quotients on lanes 0..2, one sequence each (same values)
+    const int l = lane_index();
+    const double half_theta = 0.5 * theta;
+    const double tv = dmath::sincos_d(l < 2 ? half_theta : theta, (l & 1) != 0);
+    const double sin_h = read_lane_d<0>(tv), cos_h = read_lane_d<1>(tv);
+    const double sin_t = read_lane_d<2>(tv), cos_t = read_lane_d<3>(tv);
+    const double th2 = theta * theta;
+    const double num[3] = {sin_h, 1.0 - cos_t, theta - sin_t}, den[3] = {theta, th2, th2 * theta};
+    double quo[3];
+    lane_div<3>(num, den, quo);
+#endif
     double imag, real;
     if (theta_sq < 1e-10) {
         const double theta_quad = theta_sq * theta_sq;
         imag = 0.5 - 1.0 / 48.0 * theta_sq + 1.0 / 3840.0 * theta_quad;
         real = 1.0 - 1.0 / 8.0 * theta_sq + 1.0 / 384.0 * theta_quad;
     } else {
-        const double th = __builtin_sqrt(theta_sq);
-        const double half_theta = 0.5 * th;
-        imag = dmath::sin_d(half_theta) / th;
+#if PCORE_LANE_PAR
+        imag = quo[0];
+        real = cos_h;
+#else
+        const double half_theta = 0.5 * theta;
+        imag = dmath::sin_d(half_theta) / theta;
         real = dmath::cos_d(half_theta);
+#endif
     }
     const double qw = real, qx = imag * w0, qy = imag * w1, qz = imag * w2;
     const double tx = 2.0 * qx, ty = 2.0 * qy, tz = 2.0 * qz;
@@ -339,7 +422,6 @@ PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]
     Rd[2][0] = txz - twy;
     Rd[2][1] = tyz + twx;
     Rd[2][2] = 1.0 - (txx + tyy);
-    const double theta = __builtin_sqrt(theta_sq);
     double V[3][3];
     if (theta < 1e-10) {
 PCORE_UNROLL
@@ -353,9 +435,14 @@ PCORE_UNROLL
         for (int r = 0; r < 3; r++)
 PCORE_UNROLL
             for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
+#if PCORE_LANE_PAR
+        const double c1 = quo[1];
+        const double c2 = quo[2];
+#else
         const double th2 = theta * theta;
         const double c1 = (1.0 - dmath::cos_d(theta)) / th2;
         const double c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
+#endif
 PCORE_UNROLL
         for (int r = 0; r < 3; r++)
 PCORE_UNROLL

@@ -37,7 +37,7 @@ def main():
     fn(buf, 0)
     it = iters.cpu().numpy()
     total = int(it.sum())  # one linearisation + one LM iteration per counted iteration
-    names = ["linearise", "-", "reduction", "LM iteration", "  solves", "  se3 + compose", "  trial errors",
+    names = ["search", "contributions", "reduction", "LM iteration", "  solves", "  se3 + compose", "  trial errors",
              "  decisions"]
     print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())
     for k in range(8):
