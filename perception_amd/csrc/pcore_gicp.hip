@@ -63,10 +63,6 @@ __device__ unsigned long long g_gicp_prof[kGprof];
 #define GPROF_ARG
 #endif
 
-#ifndef PCORE_LM_PREFETCH
-#define PCORE_LM_PREFETCH 0  // A/B: the first round of the trials' error inputs loaded before the first solve
-#endif
-
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -575,6 +571,15 @@ __device__ __forceinline__ void xform_identity(Xform& x) {
     }
 }
 
+// The first round of source points' inputs to the trials' errors, kept in the wave's LDS (SoA, conflict-free):
+// M as three double2 per lane, the source point and the correspondence's target (w = 1 when the point has one).
+// Later rounds go through the per-pose scratch slots in HBM / L2.  ~4.6 KB per wave.
+struct Round0 {
+    double2 (*m)[64];
+    float4* s;
+    float4* t;
+};
+
 // Linearisation of one round of 64 source points (point i on lane i % 64), fast_gicp linearize /
 // update_correspondences: the correspondence of the float query, then -- for points with one -- the shared
 // contribution into acc; the correspondence and M go to the iteration's scratch (corr[i], mah[6 i ..]) for the
@@ -584,7 +589,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
                                                 const float4* src, const double* scov, const float4* tgt,
                                                 const double* tcov, int ns, int i, bool use_grid, const LabelGrid& G,
                                                 const GicpArgs& g, const float* tquads, int nt, int j_in,
-                                                int32_t* corr, double* mah, double (&acc)[gicpm::kTerms] GPROF_PARAM) {
+                                                int32_t* corr, double* mah, const Round0& r0,
+                                                double (&acc)[gicpm::kTerms] GPROF_PARAM) {
     GPROF_T(t_s0);
     const bool act = i < ns;
     const float4 sp = act ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -605,6 +611,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
     }
     GPROF_TD(t_s1, j);
     GPROF_ADD(0, t_s0, t_s1);
+    const bool first = i < 64;
+    if (first && !(act && j >= 0)) r0.t[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (act && j >= 0) {
         const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
         double q[3];
@@ -616,10 +624,18 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
         const float4 tj = tgt[j];
         const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
         gicpm::contrib(x.R, q, cs, t3, ct, acc, M6);
-        double2* m2 = reinterpret_cast<double2*>(mah + (size_t)6 * i);
-        m2[0] = make_double2(M6[0], M6[1]);
-        m2[1] = make_double2(M6[2], M6[3]);
-        m2[2] = make_double2(M6[4], M6[5]);
+        if (first) {
+            r0.m[0][i] = make_double2(M6[0], M6[1]);
+            r0.m[1][i] = make_double2(M6[2], M6[3]);
+            r0.m[2][i] = make_double2(M6[4], M6[5]);
+            r0.s[i] = sp;
+            r0.t[i] = make_float4(tj.x, tj.y, tj.z, 1.0f);
+        } else {
+            double2* m2 = reinterpret_cast<double2*>(mah + (size_t)6 * i);
+            m2[0] = make_double2(M6[0], M6[1]);
+            m2[1] = make_double2(M6[2], M6[3]);
+            m2[2] = make_double2(M6[4], M6[5]);
+        }
     }
     GPROF_TD(t_s2, acc[gicpm::kErr]);
     GPROF_ADD(1, t_s1, t_s2);
@@ -632,23 +648,10 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
 template <typename CorrPtr>
 __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double& lambda, const float4* src,
                                             CorrPtr corr, const double* mah, const float4* tgt, int ns, int lane,
-                                            double rot_eps, double trans_eps GPROF_PARAM) {
+                                            const Round0& r0, double rot_eps, double trans_eps GPROF_PARAM) {
     const double y0 = uniform_d(sys[gicpm::kErr]);
     if (lambda < 0.0) lambda = uniform_d(gicpm::lm_init_lambda(sys));
     double nu = 2.0;
-#if PCORE_LM_PREFETCH
-    // the first round's inputs of the trials' error sums, loaded before the first solve (they do not depend on it)
-    const int pf_j = lane < ns ? corr[lane] : -1;
-    float4 pf_s = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pf_t = pf_s;
-    double pf_m[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    if (pf_j >= 0) {
-        pf_s = src[lane];
-        pf_t = tgt[pf_j];
-        const double2* m2 = reinterpret_cast<const double2*>(mah + (size_t)6 * lane);
-        const double2 a = m2[0], b = m2[1], c = m2[2];
-        pf_m[0] = a.x; pf_m[1] = a.y; pf_m[2] = b.x; pf_m[3] = b.y; pf_m[4] = c.x; pf_m[5] = c.y;
-    }
-#endif
     for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
         GPROF_T(p0);
         double d[6];
@@ -682,12 +685,16 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
             return gicpm::mahal_err(M6, e);
         };
         double ea = 0.0;
-        int i0 = 0;
-#if PCORE_LM_PREFETCH
-        if (pf_j >= 0) ea += err_of(pf_s, pf_t, pf_m);
-        i0 = 64;
-#endif
-        for (; i0 < ns; i0 += 64) {
+        // round 0 from the wave's LDS copy (written by the linearisation), the later rounds from the scratch slots
+        {
+            const float4 t0 = r0.t[lane];
+            if (t0.w != 0.0f) {
+                const double2 a = r0.m[0][lane], b = r0.m[1][lane], c = r0.m[2][lane];
+                const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+                ea += err_of(r0.s[lane], t0, M6);
+            }
+        }
+        for (int i0 = 64; i0 < ns; i0 += 64) {
             const int i = i0 + lane;
             const int j = i < ns ? corr[i] : -1;
             if (j >= 0) {
@@ -792,8 +799,11 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
 gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ double sRed[kRedDoubles];
+    __shared__ double2 sM0[3][64];
+    __shared__ float4 sS0[64], sT0[64];
     __shared__ int sPose;
     const int lane = threadIdx.x;
+    const Round0 r0{sM0, sS0, sT0};
     GPROF_DECL;
     for (;;) {
         wave_lds_sync();  // the previous pose's reads of sPose are done
@@ -821,11 +831,11 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
                 for (int i0 = 0; i0 < P.ns; i0 += 64)
                     linearize_round<true>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
-                                          P.tquads, P.nt, -1, P.corr, P.mah, acc GPROF_ARG);
+                                          P.tquads, P.nt, -1, P.corr, P.mah, r0, acc GPROF_ARG);
                 GPROF_T(t_b);
                 const double* sys = lds_tree_sum(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
-                const int st = lm_iteration(sys, x, lambda, P.src, P.corr, P.mah, P.tgt, P.ns, lane, g.rot_eps,
+                const int st = lm_iteration(sys, x, lambda, P.src, P.corr, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
                                             g.trans_eps GPROF_ARG);
                 GPROF_TD(t_d, st);
                 GPROF_ADD(2, t_b, t_c);
@@ -849,9 +859,12 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
     constexpr int NT = 64 * WPP;
     extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
     __shared__ double sRed[kRedDoubles];
+    __shared__ double2 sM0[3][64];
+    __shared__ float4 sS0[64], sT0[64];
     __shared__ double sX[12];
     __shared__ int sPose, sFlag;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const Round0 r0{sM0, sS0, sT0};  // wave 0's
     for (;;) {
         __syncthreads();
         if (tid == 0) {
@@ -900,10 +913,10 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 for (int i0 = 0; i0 < P.ns; i0 += 64) {
                     const int i = i0 + lane;
                     linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
-                                           P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, acc GPROF_ARG);
+                                           P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, r0, acc GPROF_ARG);
                 }
                 const double* sys = lds_tree_sum(acc, sRed, lane);
-                const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, g.rot_eps,
+                const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
                                             g.trans_eps GPROF_ARG);
                 if (lane == 0) {
                     sFlag = st;
