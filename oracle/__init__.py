@@ -267,7 +267,7 @@ def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EP
 
 def gicp_trace(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS):
     """orc_gicp with its per-iteration trace: (T, iterations, trace (iterations, 16): R (9), t (3) after each
-    iteration, the lambda of its first trial, 0, 0, the LM status)."""
+    iteration, the lambda of its first trial, its number of trials, 0, the LM status)."""
     src = _c(src, np.float32).reshape(-1, 3)
     tgt = _c(tgt, np.float32).reshape(-1, 3)
     T = np.zeros(16, np.float64)

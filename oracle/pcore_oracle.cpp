@@ -636,7 +636,7 @@ void gicp_linearize_spec(const OXform& x, const float* src_xyz, const double* sr
 // One LM iteration (LsqRegistration::step_lm) on the reduced system, as the GPU's lm_iteration
 int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double& lambda, const float* src_xyz, int ns,
                       const float* tgt_xyz, const int32_t* corr, const double* mah, double rot_eps, double trans_eps,
-                      double* lambda_used) {
+                      double* lambda_used, int* trials = nullptr) {
     namespace gm = pcore::gicpm;
     const double y0 = sys[gm::kErr];
     if (lambda < 0.0) lambda = gm::lm_init_lambda(sys);
@@ -644,6 +644,7 @@ int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double&
     std::vector<double> part(64);
     *lambda_used = lambda;
     for (int trial = 0; trial < gm::kLmMaxTrials; trial++) {
+        if (trials) *trials = trial + 1;
         double d[6];
         gm::lm_solve(sys, lambda, d);
         if (!gm::all_finite6(d)) return gm::kLmFailed;
@@ -783,7 +784,7 @@ void orc_covariances(const float* xyz, int n, int k, double* out_cov6) {
 }
 
 // The spec's GICP with an optional per-iteration trace (max_iter x 16: R, t after the iteration, the lambda of its
-// first trial, 0, 0, the LM status).
+// first trial, its number of trials, 0, the LM status).
 int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
                    int nt, int max_iter, double rot_eps, double trans_eps, double* out_T, double* trace) {
     namespace gm = pcore::gicpm;
@@ -807,15 +808,16 @@ int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const fl
             gicp_linearize_spec(x, src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, keys.empty() ? nullptr : keys.data(),
                                 org, corr.data(), mah.data(), sys);
             double lam_used;
+            int trials = 0;
             const int st = gicp_lm_iteration(sys, x, lambda, src_xyz, ns, tgt_xyz, corr.data(), mah.data(), rot_eps,
-                                             trans_eps, &lam_used);
+                                             trans_eps, &lam_used, &trials);
             if (trace) {
                 double* tr = trace + (size_t)16 * k;
                 for (int r = 0; r < 3; r++) {
                     for (int c = 0; c < 3; c++) tr[3 * r + c] = x.R[r][c];
                     tr[9 + r] = x.t[r];
                 }
-                tr[12] = lam_used; tr[13] = 0.0; tr[14] = 0.0; tr[15] = st;
+                tr[12] = lam_used; tr[13] = trials; tr[14] = 0.0; tr[15] = st;
             }
             if (st != gm::kLmAccepted) break;
         }
