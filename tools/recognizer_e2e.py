@@ -39,8 +39,18 @@ def main():
     from perception_amd import workloads
     centers = workloads.object_centers(len(names))
     gts = np.stack([syn.default_gt_pose(rng, c) for c in centers])
-    from tests.helpers import oracle_render_fn
-    sc = syn.make_scene(names, gts, oracle_render_fn, rng=rng)
+    from perception_amd.core import PoseCore
+    from perception_amd.model import compute_proj
+    cam = syn.CAM_640
+    rcore = PoseCore(0)  # the scene's GT render (GPU raster, empty observation)
+    rb = syn.model_bank(names)
+    rcore.upload_meshes(rb.tris, rb.tris_model_count, rb.colors)
+    rcore.set_camera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"],
+                     compute_proj(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["width"], cam["height"]))
+    z = torch.zeros((cam["height"], cam["width"]), dtype=torch.int32, device="cuda:0")
+    rcore.set_observation(z, None, torch.zeros((0, 3), dtype=torch.float32, device="cuda:0"), None, 0.01)
+    sc = syn.make_scene(names, gts, workloads.gpu_render_fn(rcore, torch.device("cuda", 0)), rng=rng)
+    del rcore
     root = tempfile.mkdtemp()
     for k, name in enumerate(names):
         P = syn.candidate_poses(gts[k][:3, 3], a.poses, rng, include=gts[k])
