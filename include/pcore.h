@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PCORE_ABI_VERSION 4
+#define PCORE_ABI_VERSION 5
 
 enum pcore_status {
     PCORE_OK = 0,
@@ -190,6 +190,25 @@ typedef struct pcore_gpu_stats {
     int32_t icp_chunks;
 } pcore_gpu_stats;
 int pcore_get_stats(pcore_ctx* ctx, pcore_gpu_stats* out, int32_t reset);
+
+/* GenerateSuccessorStates / GetStateImagesUnifiedGPU host work on the device (search_env.cpp:7056-7254,
+ * 1535-1576), for the drop-in recognizer's states:
+ *
+ * pcore_count_within: IsValidPose's neighbour count (search_env.cpp:359-396, pcl::search::KdTree radiusSearch):
+ * for every query i, the points of observed label segment d_labels[i] (as set by pcore_set_observation; a label
+ * outside the segments counts 0) strictly within the radius -- float query and points, d_radius_sq[i] = float(r *
+ * r), ((0 + dx^2) + dy^2) + dz^2 < r^2 in float.  d_queries: n x 3 float; d_out_counts: n int32.
+ *
+ * pcore_state_poses: the states' poses for the GPU search: for state i (x y z qx qy qz qw, double), cam_from_world
+ * (HOST, 16 doubles row-major: inv(camera_pose * cam_to_body)) * ContPose::GetTransform (normalised quaternion,
+ * object_state.cpp:83-97) * d_preprocess[d_model[i]] (16 doubles row-major per model, PreprocessModel), every
+ * product summed in index order in double, then mat4x4::init_from_eigen(., 100) (model.h:89-107) into
+ * d_out_poses (n x 16 float).  Model ids must lie in [0, num_models). */
+int pcore_count_within(pcore_ctx* ctx, const float* d_queries, const int32_t* d_labels, const float* d_radius_sq,
+                       int32_t n, int32_t* d_out_counts, pcore_stream stream);
+int pcore_state_poses(pcore_ctx* ctx, const double* d_states, const int32_t* d_model, const double* cam_from_world,
+                      const double* d_preprocess, int32_t num_models, int32_t n, float* d_out_poses,
+                      pcore_stream stream);
 
 /* Stage "CLOUD": compute_point_clouds (compute_point_clouds.cuh:188-367) over N z-buffers: stride mask,
  * pose-major / row / column compaction, unprojection.  xyz AoS (cap x 3).  d_label_mask (H x W) only

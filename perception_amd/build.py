@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpcore.so")
-SOURCES = ["pcore_kernels.hip", "pcore_gicp.hip", "pcore_metrics.hip", "pcore_api.hip"]
+SOURCES = ["pcore_kernels.hip", "pcore_gicp.hip", "pcore_metrics.hip", "pcore_states.hip", "pcore_api.hip"]
 HEADERS = ["pcore_internal.h", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h", os.path.join("..", "..", "include", "pcore.h")]
 ARCH = os.environ.get("PCORE_OFFLOAD_ARCH", "gfx950")
 

@@ -280,6 +280,34 @@ class PoseCore:
             _ptr(keys, torch.int64, "keys"), _stream(stream)))
         return keys
 
+    def count_within(self, queries: torch.Tensor, labels: torch.Tensor, radius_sq: torch.Tensor,
+                     out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """IsValidPose neighbour counts (pcore_count_within): for every query (n x 3 float32), the points of its
+        observed label segment strictly within sqrt(radius_sq) (float32 per query), PCL radiusSearch semantics."""
+        n = int(queries.shape[0])
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=queries.device)
+        self._check(self.lib.pcore_count_within(
+            self._h, _ptr(queries.contiguous(), torch.float32, "queries"), _ptr(labels.contiguous(), torch.int32, "labels"),
+            _ptr(radius_sq.contiguous(), torch.float32, "radius_sq"), n, _ptr(out, torch.int32, "counts"),
+            _stream(stream)))
+        return out
+
+    def state_poses(self, states: torch.Tensor, model: torch.Tensor, cam_from_world, preprocess: torch.Tensor,
+                    out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """The states' search poses (pcore_state_poses): init_from_eigen(cam_from_world * T(state) *
+        preprocess[model], 100) for states (n x 7 float64: x y z qx qy qz qw), as N x 16 float32."""
+        n = int(states.shape[0])
+        if out is None:
+            out = torch.empty((n, 16), dtype=torch.float32, device=states.device)
+        cam = (ctypes.c_double * 16)(*[float(v) for v in np.asarray(cam_from_world, np.float64).reshape(16)])
+        k = int(preprocess.shape[0])
+        self._check(self.lib.pcore_state_poses(
+            self._h, _ptr(states.contiguous(), torch.float64, "states"), _ptr(model.contiguous(), torch.int32, "model"),
+            cam, _ptr(preprocess.contiguous(), torch.float64, "preprocess"), k, n, _ptr(out, torch.float32, "poses"),
+            _stream(stream)))
+        return out
+
 
 class PoseLanes:
     """Batches in flight on one device: `lanes` independent contexts, each with its own HIP stream.

@@ -1098,6 +1098,33 @@ int pcore_select(pcore_ctx* c, const float* d_rc, const float* d_oc, const int32
     return PCORE_OK;
 }
 
+int pcore_count_within(pcore_ctx* c, const float* d_queries, const int32_t* d_labels, const float* d_radius_sq,
+                       int32_t n, int32_t* d_out_counts, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (n < 0 || (n > 0 && (!d_queries || !d_labels || !d_radius_sq || !d_out_counts)))
+        return fail(c, PCORE_E_INVALID_ARG, "count_within: null pointer");
+    if (!c->have_obs) return fail(c, PCORE_E_STATE, "count_within: the observation must be set first");
+    if (n == 0) return PCORE_OK;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, launch_count_within(d_queries, d_labels, d_radius_sq, n, c->tgt.p, c->seg_lo.p, c->seg_hi.p,
+                                c->num_obs > 0 ? c->num_grids : 0, d_out_counts, (hipStream_t)stream));
+    return PCORE_OK;
+}
+
+int pcore_state_poses(pcore_ctx* c, const double* d_states, const int32_t* d_model, const double* cam_from_world,
+                      const double* d_preprocess, int32_t num_models, int32_t n, float* d_out_poses,
+                      pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (n < 0 || !cam_from_world || num_models <= 0 ||
+        (n > 0 && (!d_states || !d_model || !d_preprocess || !d_out_poses)))
+        return fail(c, PCORE_E_INVALID_ARG, "state_poses: bad arguments");
+    if (n == 0) return PCORE_OK;
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, launch_state_poses(d_states, d_model, d_preprocess, cam_from_world, num_models, n, d_out_poses,
+                               (hipStream_t)stream));
+    return PCORE_OK;
+}
+
 int pcore_pose_distances(pcore_ctx* c, const float* d_pts, int32_t n, const double* d_T_gt, const double* d_T_est,
                          int32_t num_pairs, double* d_add, double* d_adds, pcore_stream stream) {
     if (!c) return PCORE_E_INVALID_ARG;

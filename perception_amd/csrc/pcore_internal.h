@@ -204,6 +204,12 @@ size_t gicp_order_temp_bytes(int n);
 // descending src_count x segment size
 hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32_t* keys_out, int32_t* idx_in,
                              int32_t* order_out, void* temp, size_t temp_bytes, hipStream_t s);
+// pcore_states.hip: the recognizer's per-state pose building and IsValidPose neighbour counts
+hipError_t launch_state_poses(const double* states, const int32_t* model, const double* preprocess,
+                              const double cam[16], int num_models, int n, float* out, hipStream_t s);
+hipError_t launch_count_within(const float* q, const int32_t* labels, const float* r2, int n, const float4* pts,
+                               const int32_t* seg_lo, const int32_t* seg_hi, int num_segs, int32_t* out,
+                               hipStream_t s);
 // pcore_metrics.hip
 int pose_dist_blocks(int n);
 hipError_t launch_pose_distances(const float* pts, int n, const double* T_gt, const double* T_est, int pairs,

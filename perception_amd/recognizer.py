@@ -244,6 +244,7 @@ class ObjectRecognizer:
     # -- ObjectRecognizer::SetStaticInput -> LoadObjFiles (search_env.cpp:253-307) -----------------
     def set_static_input(self, model_names: Sequence[str], six_dof: bool = True):
         self.models, self.preprocess, self.model_names = [], [], list(model_names)
+        self._pre_dev = None  # device copy of the preprocessing transforms (_poses_device)
         for name in model_names:
             meta = self.bank[name]
             m = meta.model if meta.model is not None else pio.load_ply(meta.file, name)
@@ -306,7 +307,10 @@ class ObjectRecognizer:
                                self.params.min_neighbor_points_for_valid_pose, self.device)
 
     def generate_successor_states(self, inp: RecognitionInput) -> States:
-        parts = []
+        """GenerateSuccessorStates (search_env.cpp:7056-7254) over every model's pose list, IsValidPose for all of
+        them in one device call (pcore_count_within: PCL radiusSearch counts in the required object's segment)."""
+        t0 = time.perf_counter()
+        Ps, models, reqs, r2s = [], [], [], []
         for ii, name in enumerate(self.model_names):
             if inp.pose_lists is not None and name in inp.pose_lists:
                 P = np.asarray(inp.pose_lists[name], np.float64).reshape(-1, 7)
@@ -315,12 +319,27 @@ class ObjectRecognizer:
                 P = pio.read_poses_txt_cached(path) if os.path.exists(path) else np.zeros((0, 7))
             else:
                 P = np.zeros((0, 7))
+            if not len(P):
+                continue
             req = self.segmented_object_names.index(name) if name in self.segmented_object_names else \
                 len(self.segmented_object_names)
-            ok = self._valid_pose_mask(ii, P[:, :3], req) if len(P) else np.zeros(0, bool)
-            k = int(ok.sum())
-            parts.append(States(np.full(k, ii, np.int32), np.full(k, req, np.int32), P[ok]))
-        return States.concat(parts)
+            rad = self._search_radius(ii)
+            Ps.append(P)
+            models.append(np.full(len(P), ii, np.int32))
+            reqs.append(np.full(len(P), req, np.int32))
+            r2s.append(np.full(len(P), np.float32(rad * rad), np.float32))
+        if not Ps:
+            return States()
+        P, model, req, r2 = np.concatenate(Ps), np.concatenate(models), np.concatenate(reqs), np.concatenate(r2s)
+        t1 = time.perf_counter()
+        dev = self.device
+        q = torch.from_numpy(np.ascontiguousarray(P[:, :3])).to(dev).float()  # float PointXYZ of the translation
+        counts = self.core.count_within(q, torch.from_numpy(req).to(dev), torch.from_numpy(r2).to(dev)).cpu().numpy()
+        t2 = time.perf_counter()
+        ok = counts >= self.params.min_neighbor_points_for_valid_pose
+        out = States(model[ok], req[ok], P[ok])
+        self.states_timing = {"lists_s": t1 - t0, "valid_s": t2 - t1, "filter_s": time.perf_counter() - t2}
+        return out
 
     # -- per-state inputs of the GPU call (GetStateImagesUnifiedGPU, search_env.cpp:1577-1620) -------
     def _cost_type(self) -> int:
@@ -335,9 +354,21 @@ class ObjectRecognizer:
         seg = np.append(self.segmented_count, 0.0).astype(np.float32)
         return seg[np.minimum(states.req, len(seg) - 1)]
 
+    def _poses_device(self, states) -> torch.Tensor:
+        """The states' search poses on the device (pcore_state_poses: _pose_in_cam's arithmetic, bit for bit)."""
+        cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
+        if not len(states):
+            return torch.zeros((0, 16), dtype=torch.float32, device=self.device)
+        if getattr(self, "_pre_dev", None) is None or self._pre_dev.shape[0] != len(self.preprocess):
+            self._pre_dev = torch.from_numpy(np.stack(self.preprocess).reshape(-1, 16).astype(np.float64)).to(self.device)
+        st = torch.from_numpy(np.ascontiguousarray(states.pose, np.float64)).to(self.device)
+        return self.core.state_poses(st, torch.from_numpy(states.model.copy()).to(self.device), cam_matrix,
+                                     self._pre_dev)
+
     def _pose_in_cam(self, states) -> np.ndarray:
-        """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576): inv(cam_z_front) * T(state) *
-        preprocess, vectorised over the states (model.chain_matmul_batch: index-order 4x4 products)."""
+        """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576) on the host: inv(cam_z_front) *
+        T(state) * preprocess, vectorised over the states (model.chain_matmul_batch: index-order 4x4 products);
+        the restatement pcore_state_poses is held to."""
         cam_z_front = self.camera_pose @ CAM_TO_BODY
         cam_matrix = np.linalg.inv(cam_z_front)
         if not len(states):
@@ -367,7 +398,7 @@ class ObjectRecognizer:
         peak_mb = float(torch.cuda.max_memory_allocated(self.device)) / 1024.0 / 1024.0
         t_build = t_states
         if len(mine):
-            poses = torch.from_numpy(self._pose_in_cam(mine)).to(self.device)
+            poses = self._poses_device(mine)
             pm = torch.from_numpy(mine.model.copy()).to(self.device)
             pl = self._pose_labels(mine)
             tot = torch.from_numpy(self._obs_totals(mine)).to(self.device)
@@ -427,7 +458,7 @@ class ObjectRecognizer:
         # host-side breakdown of the last search (seconds): successor states (poses.txt + IsValidPose), per-state
         # inputs of the GPU call, the GPU search (launch .. synchronise, incl. the exchange), results
         self.last_timing = {"states_s": t_states - t0, "inputs_s": t_build - t_states,
-                            "gpu_s": gpu_s, "total_s": t_end - t0}
+                            "gpu_s": gpu_s, "total_s": t_end - t0, **getattr(self, "states_timing", {})}
         self.last_stats = EnvStats(scenes_rendered=n_total, scenes_valid=0, time=time.perf_counter() - t0,
                                    icp_time=icp_time, peak_gpu_mem=peak_mb)
         return results

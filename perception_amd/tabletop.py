@@ -230,6 +230,9 @@ class TabletopRecognizer(ObjectRecognizer):
                                     self.device, cap=self.cam.width * self.cam.height)  # max_nn = kNumPixels
         return out
 
+    def _poses_device(self, states) -> torch.Tensor:
+        return torch.from_numpy(self._pose_in_cam(states)).to(self.device)
+
     def _pose_in_cam(self, states) -> np.ndarray:
         """The 3-DoF states' poses in the camera, vectorised (yaw quaternions with math.sin / math.cos per
         state, as yaw_pose_matrix; index-order 4x4 products, model.chain_matmul_batch)."""
