@@ -257,11 +257,11 @@ def main():
             keys_ring[b].fill_(PCORE_KEY_NONE)
             if ev is not None:
                 ev[0].record(st)
-            core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=s, out=outs[b], stream=st)
+            # stage COST with the per-model argmin folded into the same launch (pcore_evaluate_select)
+            core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=s, out=outs[b], stream=st,
+                          select=(keys_ring[b], w.index_base, w.num_models))
             if ev is not None:
                 ev[1].record(st)
-            core.select(outs[b][0], outs[b][1], w.pose_model, w.num_models, index_base=w.index_base,
-                        keys=keys_ring[b], stream=st)
             works[b] = pdist.allreduce_min_keys_async(keys_ring[b])
 
     for i in range(args.warmup + L):  # every lane warmed (tile tier picked from its own first call)

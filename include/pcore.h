@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PCORE_ABI_VERSION 5
+#define PCORE_ABI_VERSION 6
 
 enum pcore_status {
     PCORE_OK = 0,
@@ -80,7 +80,9 @@ int pcore_abi_version(void);
  * pcore_upload_meshes, pcore_set_camera, pcore_set_observation, pcore_set_observation_colors, a new
  * sampling stride, and every reallocation of per-batch scratch.  A replay is valid only while the
  * generation equals the one read right after the capture (no reference counterpart: the reference
- * re-uploads everything per call, renderer.cu:1532-1544).  0 for a NULL context. */
+ * re-uploads everything per call, renderer.cu:1532-1544).  0 for a NULL context.  A C caller that captures
+ * pcore_evaluate into a graph compares pcore_generation before every replay, and orders its setup calls
+ * after any replay still in flight on its stream (the check runs when the replay is enqueued). */
 uint64_t pcore_generation(const pcore_ctx* ctx);
 
 /* ---- static inputs ----------------------------------------------------------------------------- */
@@ -154,6 +156,15 @@ typedef struct pcore_icp_params {
     double rotation_epsilon;        /* 2e-3 */
     double transformation_epsilon;  /* 5e-4 */
 } pcore_icp_params;
+
+/* pcore_evaluate followed by pcore_select in one launch: every pose's argmin key (pcore_select's, global index
+ * index_base + i) is folded into d_keys[model] (atomic MIN) by the workgroup that scores the pose, so the batch
+ * needs no separate selection pass.  The costs are written as by pcore_evaluate (d_out_oc may not be null); the
+ * keys equal pcore_evaluate + pcore_select's. */
+int pcore_evaluate_select(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_model,
+                          const int32_t* d_pose_label, const float* d_pose_obs_total, int32_t num_poses,
+                          const pcore_eval_params* params, float* d_out_rc, float* d_out_oc, float* d_out_diff,
+                          int64_t index_base, int32_t num_models, int64_t* d_keys, pcore_stream stream);
 
 /* Stage "COST" with do_icp = true (renderer.cu:1688-1817): render, unproject at stride, per-pose GICP of
  * the rendered cloud onto the pose's observed label segment (FastGICPCudaCore::optimize_multi), compose

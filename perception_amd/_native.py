@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "pcore_render",
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
     "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation", "pcore_get_stats",
-    "pcore_count_within", "pcore_state_poses",
+    "pcore_count_within", "pcore_state_poses", "pcore_evaluate_select",
 )
 
 
@@ -120,6 +120,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     L.pcore_observed_cloud_bounded.argtypes = [vp, vp, vp, i32, i32, i32, f32, vp, vp, vp, vp, i32,
                                                ctypes.POINTER(i32), vp]
     L.pcore_generation.argtypes = [vp]
+    L.pcore_evaluate_select.argtypes = [vp, vp, vp, vp, vp, i32, ctypes.POINTER(EvalParams), vp, vp, vp, i64, i32,
+                                        vp, vp]
     L.pcore_count_within.argtypes = [vp, vp, vp, vp, i32, vp, vp]
     L.pcore_state_poses.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_double), vp, i32, i32, vp, vp]
     for name in EXPORTED_SYMBOLS:

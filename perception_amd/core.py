@@ -149,8 +149,11 @@ class PoseCore:
                  calc_obs_cost: bool = True, stride: int = 8, depth_factor: float = 100.0,
                  sensor_resolution: float = 0.01, occlusion_threshold: float = 1.0,
                  out: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                 dbg_zs: Optional[torch.Tensor] = None, color_distance_threshold: float = 15.0, stream=None):
-        """Stage COST (do_icp = false).  Returns (rendered_cost, observed_cost, points_diff_cost)."""
+                 dbg_zs: Optional[torch.Tensor] = None, color_distance_threshold: float = 15.0, stream=None,
+                 select: Optional[Tuple[torch.Tensor, int, int]] = None):
+        """Stage COST (do_icp = false).  Returns (rendered_cost, observed_cost, points_diff_cost).  With
+        select = (keys, index_base, num_models) the launch also folds every pose's argmin key into `keys`
+        (pcore_evaluate_select: the same keys as a following select() call)."""
         n = int(poses.shape[0])
         dev = poses.device
         if out is None:
@@ -158,6 +161,17 @@ class PoseCore:
         rc, oc, df = out
         p = EvalParams(int(cost_type), int(bool(calc_obs_cost)), int(stride), float(depth_factor),
                        float(sensor_resolution), float(occlusion_threshold), float(color_distance_threshold))
+        if select is not None:
+            keys, index_base, num_models = select
+            if dbg_zs is not None:
+                raise ValueError("evaluate: dbg_zs and select are exclusive")
+            self._check(self.lib.pcore_evaluate_select(
+                self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
+                _ptr(pose_label, torch.int32, "pose_label"), _ptr(pose_obs_total, torch.float32, "pose_obs_total"),
+                n, ctypes.byref(p), _ptr(rc, torch.float32, "rc"), _ptr(oc, torch.float32, "oc"),
+                _ptr(df, torch.float32, "diff"), int(index_base), int(num_models), _ptr(keys, torch.int64, "keys"),
+                _stream(stream)))
+            return rc, oc, df
         self._check(self.lib.pcore_evaluate(
             self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
             _ptr(pose_label, torch.int32, "pose_label"), _ptr(pose_obs_total, torch.float32, "pose_obs_total"),
@@ -177,7 +191,8 @@ class PoseCore:
         pointers, tile size).  Any later setup call (upload_meshes, set_camera, set_observation,
         set_observation_colors), a new stride or a larger batch that reallocates scratch changes the
         context's generation (pcore_generation), and replay() then raises PcoreError(PCORE_E_STATE)
-        instead of running stale launches: capture again."""
+        instead of running stale launches: capture again.  The check runs when replay() enqueues the graph, so a
+        setup call must be stream-ordered after any replay still in flight."""
         n = int(poses.shape[0])
         out = tuple(torch.empty(n, dtype=torch.float32, device=poses.device) for _ in range(3))
         self.evaluate(poses, pose_model, pose_label, pose_obs_total, out=out, **kw)

@@ -758,9 +758,10 @@ static int validate_eval(pcore_ctx* c, const char* who, const float* d_poses, co
     return PCORE_OK;
 }
 
-int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
-                   const float* d_pose_obs_total, int32_t num_poses, const pcore_eval_params* p, float* d_out_rc,
-                   float* d_out_oc, float* d_out_diff, int32_t* d_dbg_zs, pcore_stream stream) {
+static int evaluate_impl(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
+                         const float* d_pose_obs_total, int32_t num_poses, const pcore_eval_params* p, float* d_out_rc,
+                         float* d_out_oc, float* d_out_diff, int32_t* d_dbg_zs, int64_t* d_keys, int64_t index_base,
+                         int32_t num_models, pcore_stream stream) {
     if (!c || !p) return PCORE_E_INVALID_ARG;
     const int vr = validate_eval(c, "evaluate", d_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p,
                                  d_out_rc, d_out_oc, d_out_diff);
@@ -819,9 +820,30 @@ int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_mod
         a.cid = c->colour_id.p;
     }
     if (const char* e = getenv("PCORE_DEBUG_SKIP")) a.dbg_skip = atoi(e);
+    a.sel_keys = d_keys;
+    a.sel_base = index_base;
+    a.sel_models = num_models;
     HIPC(c, set_fused_tiles(c, num_poses, a));
     HIPC(c, launch_fused_cost(a, s));
     return PCORE_OK;
+}
+
+int pcore_evaluate(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model, const int32_t* d_pose_label,
+                   const float* d_pose_obs_total, int32_t num_poses, const pcore_eval_params* p, float* d_out_rc,
+                   float* d_out_oc, float* d_out_diff, int32_t* d_dbg_zs, pcore_stream stream) {
+    return evaluate_impl(c, d_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p, d_out_rc, d_out_oc,
+                         d_out_diff, d_dbg_zs, nullptr, 0, 0, stream);
+}
+
+int pcore_evaluate_select(pcore_ctx* c, const float* d_poses, const int32_t* d_pose_model,
+                          const int32_t* d_pose_label, const float* d_pose_obs_total, int32_t num_poses,
+                          const pcore_eval_params* p, float* d_out_rc, float* d_out_oc, float* d_out_diff,
+                          int64_t index_base, int32_t num_models, int64_t* d_keys, pcore_stream stream) {
+    if (!c) return PCORE_E_INVALID_ARG;
+    if (num_models <= 0 || index_base < 0 || index_base + num_poses > 0x7fffffffLL || (num_poses > 0 && !d_keys))
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_select: bad selection arguments");
+    return evaluate_impl(c, d_poses, d_pose_model, d_pose_label, d_pose_obs_total, num_poses, p, d_out_rc, d_out_oc,
+                         d_out_diff, nullptr, d_keys, index_base, num_models, stream);
 }
 
 static int fill_fused_args(pcore_ctx* c, const pcore_eval_params* p, FusedArgs& a) {

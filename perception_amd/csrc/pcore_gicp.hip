@@ -428,8 +428,9 @@ typedef __attribute__((address_space(4))) const f4v cf4v;
 #define PCORE_SCAN_UNROLL 4  // quad pairs per loop trip (C3: 2 -> 4: 20.60 -> 20.45 ms per step; 1: 21.25)
 #endif
 
-__device__ __forceinline__ void scan_quads(const float* seg_quads, int nq, float qx, float qy, float qz, float& best,
+__device__ __forceinline__ void scan_quads(const float* seg_quads, int nt, float qx, float qy, float qz, float& best,
                                            int& j) {
+    const int nq = (nt + 3) >> 2;
     const cf4v* hq = (const cf4v*)seg_quads;
     const f4v org = hq[0];
     qx = qx - org.x;
@@ -471,7 +472,9 @@ __device__ __forceinline__ void scan_quads(const float* seg_quads, int nq, float
                     : gicpm::nn_key(X.y, Y.y, Z.y, T.y, qx, qy, qz) == bA ? 1
                     : gicpm::nn_key(X.z, Y.z, Z.z, T.z, qx, qy, qz) == bA ? 2 : 3;
         best = bA;
-        j = 4 * oA + k;
+        // one of the four recomputed keys equals bA (same FMAs); the clamp only keeps a broken match (which would
+        // pick slot 3, padding in a segment's last quad) inside the segment
+        j = min(4 * oA + k, nt - 1);
     }
 }
 
@@ -605,7 +608,7 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
         if (use_grid) {
             if (act) grid_nn(G, g.cell_start, g.grid_pts, tgt, nt, qf[0], qf[1], qf[2], best, j);
         } else {
-            scan_quads(tquads, (nt + 3) >> 2, qf[0], qf[1], qf[2], best, j);
+            scan_quads(tquads, nt, qf[0], qf[1], qf[2], best, j);
         }
         if (act) corr[i] = j;
     }
@@ -898,7 +901,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 if (P.use_grid) {
                     if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
                 } else {
-                    scan_quads(P.tquads, (P.nt + 3) >> 2, qf[0], qf[1], qf[2], best, j);
+                    scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, j);
                 }
                 if (act) jbuf[i] = j;
             }

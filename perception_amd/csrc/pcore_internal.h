@@ -125,6 +125,11 @@ struct FusedArgs {
     // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
     // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
     int32_t dbg_skip;
+    // pcore_evaluate_select: each pose's argmin key (select_kernel's) folded into sel_keys[model] by the launch
+    // that scores it (nullptr: plain pcore_evaluate)
+    int64_t* sel_keys;
+    int64_t sel_base;
+    int32_t sel_models;
 };
 
 // GICP over a chunk of poses (pcore_kernels.hip, gicp_kernel)

@@ -781,6 +781,19 @@ __device__ SampleWin pose_window(const FusedArgs& a, int model, const float (&m)
 }
 
 // One pose of stage COST on the workgroup's LDS tile (sw.nx * sw.ny <= tile capacity).
+// select_kernel's per-pose key (search_env.cpp:1987-2051: int conversion, the |target - source| < 30 filter, cost
+// -1 / -2 / INT_MAX excluded): ((cost ^ 0x80000000) << 31) | global index, or PCORE_KEY_NONE_DEV
+__device__ __forceinline__ int64_t select_key(float rc, float oc, int m, int num_models, int64_t gidx) {
+    const int32_t target = cvt_i32_x86(rc);
+    const int32_t source = cvt_i32_x86(oc);
+    const int32_t cost = (target < 0) ? -1 : cvt_i32_x86(rc + oc);
+    const int32_t adiff = iabs_wrap(target, source);
+    const bool ok = !(cost == -1 || cost == -2) && adiff < 30 && cost != INT_MAX && m >= 0 && m < num_models;
+    if (!ok) return PCORE_KEY_NONE_DEV;
+    const uint64_t hi = (uint64_t)((uint32_t)cost ^ 0x80000000u);
+    return (int64_t)((hi << 31) | ((uint64_t)gidx & 0x7fffffffull));
+}
+
 template <int STRIDE, bool COLOUR>
 __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw) {
     const int tid = threadIdx.x;
@@ -968,16 +981,23 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
         float rc = (num == 0.0f) ? -1.0f : badf / num;
         rc = (rc == -1.0f) ? -1.0f : rc * 100.0f;
         a.out_rc[pose] = rc;
+        float ocw = 0.0f;  // the observed cost as stored
         if (a.calc_obs) {
             const float expl = (float)sm.counters[1];
             const float tot = a.pose_obs_total[pose];
             a.out_diff[pose] = rendered_explained - expl;
             float oc = tot - expl;
             oc = oc / tot;
-            a.out_oc[pose] = oc * 100.0f;
+            ocw = oc * 100.0f;
+            a.out_oc[pose] = ocw;
         } else {
             if (a.out_oc) a.out_oc[pose] = 0.0f;
             if (a.out_diff) a.out_diff[pose] = 0.0f;
+        }
+        if (a.sel_keys) {
+            const int m = a.pose_model[pose];
+            const int64_t key = select_key(rc, ocw, m, a.sel_models, a.sel_base + pose);
+            if (key != PCORE_KEY_NONE_DEV) atomicMin((unsigned long long*)&a.sel_keys[m], (unsigned long long)key);
         }
     }
     fp.mark(6);
@@ -1569,15 +1589,7 @@ __global__ void select_kernel(const float* rc, const float* oc, const int32_t* p
     int m = -1;
     if (i < num_poses) {
         m = pose_model[i];
-        const int32_t target = cvt_i32_x86(rc[i]);
-        const int32_t source = cvt_i32_x86(oc[i]);
-        const int32_t cost = (target < 0) ? -1 : cvt_i32_x86(rc[i] + oc[i]);
-        const int32_t adiff = iabs_wrap(target, source);
-        const bool ok = !(cost == -1 || cost == -2) && adiff < 30 && cost != INT_MAX && m >= 0 && m < num_models;
-        if (ok) {
-            const uint64_t hi = (uint64_t)((uint32_t)cost ^ 0x80000000u);
-            key = (int64_t)((hi << 31) | ((uint64_t)(index_base + i) & 0x7fffffffull));
-        }
+        key = select_key(rc[i], oc[i], m, num_models, index_base + i);
     }
     // wave-level minimum when the wave's poses share one model (the common case)
     const int m0 = __shfl(m, 0);

@@ -147,9 +147,9 @@ inline std::vector<int> sweep_order(const std::vector<int>& tv, const std::vecto
     return order;
 }
 
-constexpr int kNever = -(1 << 20);
+constexpr int kNever = -(1 << 20);              // "latest pass" of a vertex no pass of the stream has loaded
 constexpr uint32_t kStepVertexPass = 1u << 30;  // every triangle slot of a step that begins with a vertex pass
-constexpr uint32_t kSlotPadding = 1u << 31;     // a triangle slot past the batch  // "latest pass" of a vertex no pass of the stream has loaded
+constexpr uint32_t kSlotPadding = 1u << 31;     // a triangle slot past the batch
 
 // Append the streams of one model in the triangle order order0.  tri_base: index of the model's first triangle in the
 // upload.  The order is cut into num_streams * chunks chunks and stream s concatenates chunks s, s + num_streams,

@@ -283,11 +283,21 @@ class ObjectRecognizer:
         self.segmented_object_names = list(inp.model_names)
 
     # -- GenerateSuccessorStates (search_env.cpp:7056-7254) ----------------------------------------
+    def _model_dims(self, model_id: int) -> np.ndarray:
+        """_dims of a model, computed once per model list (the min / max over every triangle corner is the
+        slowest part of a search's state generation otherwise)."""
+        memo = getattr(self, "_dims_memo", None)
+        if memo is None or memo[0] is not self.models:
+            memo = self._dims_memo = (self.models, {})
+        if model_id not in memo[1]:
+            memo[1][model_id] = _dims(self.models[model_id])
+        return memo[1][model_id]
+
     def _search_radius(self, model_id: int) -> float:
         """IsValidPose's search radius, 6-DoF branch (search_env.cpp:336-390): max(inflation * circumscribed
         radius 3D, grid-cell circumscribing radius hypot(res / 2, res / 2)); after_refinement is false on the
         greedy path (search_env.cpp:7140), so the cell term stays."""
-        dims = _dims(self.models[model_id])
+        dims = self._model_dims(model_id)
         circ3d = float(max(dims)) / 2.0  # GetCircumscribedRadius3D, object_model.cpp:464-466
         inscribed = float(min(dims[0], dims[1])) / 2.0
         infl = 1.0 + K_MESH_ADDITIVE_INFLATION / inscribed if inscribed > 0 else 1.0  # object_model.cpp:381-383
@@ -422,11 +432,12 @@ class ObjectRecognizer:
                                        max_iterations=p.icp_max_iterations, rotation_epsilon=p.icp_rotation_epsilon,
                                        transformation_epsilon=p.icp_transformation_epsilon,
                                        out=(adj_all, iters, rc, oc, df))
-            else:
+                self.core.select(rc, oc, pm, K, index_base=lo, keys=keys)
+            else:  # the argmin keys folded in the scoring launch (pcore_evaluate_select)
                 self.core.evaluate(poses, pm, pl, tot, cost_type=cost_type, stride=p.gpu_stride,
                                    depth_factor=p.gpu_depth_factor, sensor_resolution=p.sensor_resolution,
-                                   occlusion_threshold=p.gpu_occlusion_threshold, out=(rc, oc, df))
-            self.core.select(rc, oc, pm, K, index_base=lo, keys=keys)
+                                   occlusion_threshold=p.gpu_occlusion_threshold, out=(rc, oc, df),
+                                   select=(keys, lo, K))
             torch.cuda.synchronize(self.device)
             gpu_s = time.perf_counter() - ti
             icp_time = gpu_s if (p.icp_type == 3 and inp.use_icp) else 0.0

@@ -150,6 +150,25 @@ def test_c4_21_models_selection_bit_exact_vs_oracle():
     assert np.array_equal(_bits(oc[sub]), _bits(ooc))
 
 
+@pytest.mark.parametrize("tier", ["auto", "tcap64"])
+def test_evaluate_select_keys_equal_evaluate_then_select(tier, monkeypatch):
+    """pcore_evaluate_select folds every pose's key in the launch that scores it (the window launch or, with a
+    64-sample tile, the overflow launch): the keys and costs equal pcore_evaluate + pcore_select's, 21 models."""
+    if tier == "tcap64":
+        monkeypatch.setenv("PCORE_FUSED_TCAP", "64")
+    w = workloads.build(names=list(syn.YCB_PROXIES), poses_per_model=120)
+    rc, oc, df = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
+    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=rc.device)
+    w.core.select(rc, oc, w.pose_model, w.num_models, index_base=1000, keys=keys)
+    keys2 = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=rc.device)
+    rc2, oc2, df2 = w.core.evaluate(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride,
+                                    select=(keys2, 1000, w.num_models))
+    assert torch.equal(keys, keys2)
+    for a, b in ((rc, rc2), (oc, oc2), (df, df2)):
+        assert np.array_equal(_bits(a.cpu().numpy()), _bits(b.cpu().numpy()))
+    assert (keys != PCORE_KEY_NONE).sum().item() >= w.num_models // 2
+
+
 @pytest.mark.parametrize("cam,tier", [("640", "auto"), ("640", "0"), ("640", "99"), ("640", "tcap64"),
                                       ("1280", "auto")])
 def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, monkeypatch):

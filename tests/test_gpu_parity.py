@@ -493,6 +493,57 @@ def test_evaluate_icp_dense_targets_matches_oracle(one_object, obs_stride):
     assert _bits_equal(oc.cpu().numpy(), ooc)
 
 
+def test_evaluate_icp_tied_and_near_zero_keys_matches_oracle(three_objects):
+    """Correspondence ties across key quads and keys near zero: every label segment gets exact
+    copies of every third of its points appended after it (equal distances at indices in other quads: the first
+    index must win), one point at the segment's key origin and one a float ulp away from another point.  GICP
+    poses, iteration counts and costs bit-exact vs the oracle."""
+    case, core, t = three_objects
+    sc = case.scene
+    xyz = case.obs_xyz_raw.astype(np.float32)
+    lab = case.obs_label_raw.astype(np.int32)
+    extra_p, extra_l = [], []
+    for L in range(case.K):
+        seg = xyz[lab == L]
+        if len(seg) == 0:
+            continue
+        lo, hi = seg.min(0), seg.max(0)
+        origin = ((lo + hi) * np.float32(0.5)).astype(np.float32)  # the key origin: t' = 0, key = 0 exactly
+        near = seg[0].copy()
+        near[0] = np.nextafter(near[0], np.float32(np.inf))
+        add = np.concatenate([seg[::3], origin[None], near[None]])
+        extra_p.append(add)
+        extra_l.append(np.full(len(add), L, np.int32))
+    xyz2 = np.concatenate([xyz] + extra_p).astype(np.float32)
+    lab2 = np.concatenate([lab] + extra_l)
+    order = np.argsort(lab2, kind="stable")
+    oxyz, olab = xyz2[order], lab2[order]
+    ls = np.array([np.searchsorted(olab, L, "left") for L in range(case.K)], np.int32)
+    le = np.array([np.searchsorted(olab, L, "right") for L in range(case.K)], np.int32)
+    tot = (le - ls).astype(np.float32)[case.pose_label]
+    ocov = np.zeros((len(oxyz), 6))
+    for L in range(case.K):
+        ocov[ls[L]:le[L]] = oracle.covariances(oxyz[ls[L]:le[L]])
+    n = 24
+    dev = t["poses"].device
+    try:
+        core.set_observation(t["src"], t["mask"], torch.from_numpy(xyz2).to(dev), torch.from_numpy(lab2).to(dev),
+                             0.01)
+        adj, iters, rc, oc, df = core.evaluate_icp(t["poses"][:n], t["pm"][:n], t["pl"][:n],
+                                                   torch.from_numpy(tot[:n]).to(dev), cost_type=2,
+                                                   stride=case.stride)
+    finally:
+        core.set_observation(t["src"], t["mask"], t["obs_xyz"], t["obs_lab"], 0.01)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n], case.pose_label[:n],
+        sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy,
+        100.0, oxyz, ocov, ls, le, tot[:n], 2, True, 0.01)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+
+
 def test_observed_cloud_bounded_matches_oracle(one_object):
     """3-DoF depth2cloud_global: world-frame table bounds filter and colours (f4)."""
     case, core, t = one_object

@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--poses", type=int, default=10000)
     ap.add_argument("--loop-poses", action="store_true")
+    ap.add_argument("--reps", type=int, default=7)
     a = ap.parse_args()
     names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
     rng = np.random.default_rng(syn.SEED)
@@ -67,10 +68,14 @@ def main():
                                use_icp=icp)
         rec.localize_objects_greedy_render(inp)  # warm-up (scratch, tiers)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        res = rec.localize_objects_greedy_render(inp)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        runs = []
+        for _ in range(a.reps):  # the median of several searches (the first ones pay one-off host costs)
+            t0 = time.perf_counter()
+            res = rec.localize_objects_greedy_render(inp)
+            torch.cuda.synchronize()
+            runs.append((time.perf_counter() - t0, dict(rec.last_timing)))
+        runs.sort(key=lambda r: r[0])
+        dt, timing = runs[len(runs) // 2]
         states = rec.generate_successor_states(inp)
         t1 = time.perf_counter()
         rec._pose_in_cam(states)
@@ -79,7 +84,8 @@ def main():
                "icp_s": round(rec.last_stats.icp_time, 4), "pose_building_s": round(dp, 4),
                "loop_poses": a.loop_poses, "found": len(res.model_names),
                "poses_per_s": round(len(states) / dt, 1),
-               "timing": {k: (round(v, 5) if v is not None else None) for k, v in rec.last_timing.items()}},
+               "localize_s_all": [round(r[0], 4) for r in runs],
+               "timing": {k: (round(v, 5) if v is not None else None) for k, v in timing.items()}},
               flush=True)
 
 
