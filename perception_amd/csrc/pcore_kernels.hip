@@ -239,7 +239,9 @@ __device__ __forceinline__ void raster_sample(const TriRec& r, int kx, int ky, i
     if constexpr (IDPASS) {
         if (in && d == zbuf[k]) atomicMin(&cid[k], (int32_t)id);
     } else {
-        atomicMin(&zbuf[k], in ? d : INT_MAX);  // INT_MAX leaves the sample as it is
+        // only inside lanes take part: an outside lane's INT_MAX min changed nothing but still collided with the
+        // inside lanes on the same bank (C2: SQ_LDS_BANK_CONFLICT 15.1 M -> 11.0 M per launch, time unchanged)
+        if (in) atomicMin(&zbuf[k], d);
     }
 }
 
