@@ -156,7 +156,7 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
     g_ms = float(np.mean(gicp_ms)) if gicp_ms else None
     iter_total = int(its.sum())
     valu_peak = VALU_SIMDS * VALU_CLOCK_HZ / 2.0
-    instr_per_iter, sq_note = None, "no profiles/sq_counters_gicp.json"
+    instr_per_iter, cyc_per_iter, sq_note = None, None, "no profiles/sq_counters_gicp.json"
     sq_path = os.path.join(ROOT, "profiles", "sq_counters_gicp.json")
     if os.path.exists(sq_path):
         try:
@@ -167,11 +167,16 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
                 sq_note = "counter profile of other GICP sources (stale): not used"
             else:
                 instr_per_iter = float(sq["gicp_kernel"]["derived_valu_instr_per_pose_iteration"])
+                cyc_per_iter = sq["gicp_kernel"].get("derived_valu_cycles_per_pose_iteration")
                 sq_note = ("profiles/sq_counters_gicp.json (SQ_INSTS_VALU / pose-iterations, counters-only rocprofv3 "
                            "pass of the same GICP sources)")
         except (OSError, ValueError, KeyError) as e:
             sq_note = f"unreadable counter profile: {e}"
     achieved = instr_per_iter * iter_total / (g_ms * 1e-3) if (instr_per_iter and g_ms) else None
+    # the same work priced in SIMD cycles (f64 and transcendental instructions 4 cycles per wave64 instruction,
+    # the rest 2) against 1024 SIMDs x 2.4 GHz
+    busy = (float(cyc_per_iter) * iter_total / (g_ms * 1e-3) / (VALU_SIMDS * VALU_CLOCK_HZ)
+            if (cyc_per_iter and g_ms) else None)
     return {
         "metric": "candidate poses rendered+GICP-refined+scored/sec @640x480 (C3)",
         "value": n * world * steps / elapsed,
@@ -191,6 +196,7 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
                      "achieved": achieved / 1e9 if achieved else None, "peak": valu_peak / 1e9,
                      "unit": "Gwave-instr/s", "frac": achieved / valu_peak if achieved else None,
                      "traffic": None, "valu_instr_per_pose_iteration": instr_per_iter, "valu_source": sq_note,
+                     "frac_cycle_weighted": busy, "valu_cycles_per_pose_iteration": cyc_per_iter,
                      "note": "a serial chain of <= 150 dependent iterations per pose (one wave each): latency-bound "
                              "by design, so the VALU issue fraction is the figure of merit; HBM traffic is a few KB "
                              "per pose-iteration, L2-resident"},

@@ -43,6 +43,16 @@ def main(out_dir, tag, rnd=None):
             gk["derived_" + c[9:].lower() + "_per_pose_iteration"] = gk[c] / pi
     if "SQ_WAIT_INST_ANY" in gk and "SQ_WAVE_CYCLES" in gk:
         gk["derived_wait_inst_any_frac"] = gk["SQ_WAIT_INST_ANY"] / gk["SQ_WAVE_CYCLES"]
+    f64 = sum(gk.get(c, 0.0) for c in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64"))
+    trans = gk.get("SQ_INSTS_VALU_TRANS_F64", 0.0) + gk.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+    if "SQ_INSTS_VALU_FMA_F64" in gk:
+        # SIMD cycles the VALU work occupies: f64 FMA / MUL / ADD and transcendentals 4 cycles per wave64
+        # instruction (tools/exec_half.hip: v_fma_f64 4.15 cycles at full occupancy; MI355X_MICROARCH.md: the
+        # transcendentals twice an FMA's issue cost), every other VALU instruction 2
+        cyc = 2.0 * (gk["SQ_INSTS_VALU"] - f64 - trans) + 4.0 * (f64 + trans)
+        gk["derived_f64_frac_of_valu"] = f64 / gk["SQ_INSTS_VALU"]
+        gk["derived_valu_cycles_per_pose_iteration"] = cyc / pi
+        gk["derived_valu_busy_frac_cycle_weighted"] = cyc / (1024.0 * gk["GRBM_GUI_ACTIVE"] / 8.0)
     if "SQ_LDS_BANK_CONFLICT" in gk and "SQ_LDS_IDX_ACTIVE" in gk:
         gk["derived_lds_bank_conflict_frac"] = gk["SQ_LDS_BANK_CONFLICT"] / max(gk["SQ_LDS_IDX_ACTIVE"], 1.0)
     d = {"gicp_kernel": gk, "poses": it["poses"], "pose_iterations": pi, "gicp_source_digest": gicp_source_digest(),
