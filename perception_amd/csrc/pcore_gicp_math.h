@@ -140,8 +140,12 @@ PCORE_UNROLL
     if constexpr (N > 4) q[4] = read_lane_d<4>(r);
     if constexpr (N > 5) q[5] = read_lane_d<5>(r);
 }
+// a value every lane holds equally, moved to an SGPR: branches on it are scalar branches (the LDLT's pivot
+// swaps run as one taken block instead of a select chain over every candidate block)
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 #else
 #define PCORE_LANE_PAR 0
+inline int uniform_i(int v) { return v; }
 #endif
 
 // e^T M e with M given by its upper triangle (xx, xy, xz, yy, yz, zz): Me row by row, then the dot product
@@ -158,16 +162,16 @@ PCORE_GHD void contrib(const double (&R)[3][3], const double (&q)[3], const doub
                        const double (&ct)[6], double (&acc)[kTerms], double (&M6)[6]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
-    double RC[3][3], A[3][3];
+    // A = C_t + R C_s R^T row by row (row r of R C_s, then A's row r): only one row of R C_s is live at a time
+    double A[3][3];
 PCORE_UNROLL
-    for (int r = 0; r < 3; r++)
+    for (int r = 0; r < 3; r++) {
+        double RC[3];
 PCORE_UNROLL
-        for (int c = 0; c < 3; c++) RC[r][c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
+        for (int c = 0; c < 3; c++) RC[c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
 PCORE_UNROLL
-    for (int r = 0; r < 3; r++)
-PCORE_UNROLL
-        for (int c = r; c < 3; c++)
-            A[r][c] = Ct[r][c] + (RC[r][0] * R[c][0] + RC[r][1] * R[c][1] + RC[r][2] * R[c][2]);
+        for (int c = r; c < 3; c++) A[r][c] = Ct[r][c] + (RC[0] * R[c][0] + RC[1] * R[c][1] + RC[2] * R[c][2]);
+    }
     A[1][0] = A[0][1];
     A[2][0] = A[0][2];
     A[2][1] = A[1][2];
@@ -192,30 +196,29 @@ PCORE_UNROLL
     M6[0] = M[0][0]; M6[1] = M[0][1]; M6[2] = M[0][2];
     M6[3] = M[1][1]; M6[4] = M[1][2]; M6[5] = M[2][2];
     const double e[3] = {tj[0] - q[0], tj[1] - q[1], tj[2] - q[2]};
-    // MJ columns 0..2 (skew part); columns 3..5 are -M's columns
-    double MJ[3][3];
+    // H[a][b] (a <= b) column by column: column b of M J as a 3-vector (b < 3: the skew part; b >= 3: -M's column),
+    // then its J^T product for every a <= b into acc[hdiag(a) + b - a].  Each sum takes one term per point, so the
+    // column order of the updates changes no sum, and only one column is live at a time.
 PCORE_UNROLL
-    for (int r = 0; r < 3; r++) {
-        MJ[r][0] = M[r][1] * q[2] - M[r][2] * q[1];
-        MJ[r][1] = M[r][2] * q[0] - M[r][0] * q[2];
-        MJ[r][2] = M[r][0] * q[1] - M[r][1] * q[0];
-    }
-    // column b of M J as a 3-vector, then its J^T product gives H[a][b] for every a
-    int h = 0;
+    for (int b = 0; b < 6; b++) {
+        double cb[3];
 PCORE_UNROLL
-    for (int a = 0; a < 6; a++)
+        for (int r = 0; r < 3; r++) {
+            if (b == 0) cb[r] = M[r][1] * q[2] - M[r][2] * q[1];
+            else if (b == 1) cb[r] = M[r][2] * q[0] - M[r][0] * q[2];
+            else if (b == 2) cb[r] = M[r][0] * q[1] - M[r][1] * q[0];
+            else cb[r] = -M[r][b - 3];
+        }
 PCORE_UNROLL
-        for (int b = a; b < 6; b++) {
-            const double cb[3] = {b < 3 ? MJ[0][b] : -M[0][b - 3], b < 3 ? MJ[1][b] : -M[1][b - 3],
-                                  b < 3 ? MJ[2][b] : -M[2][b - 3]};
+        for (int a = 0; a <= b; a++) {
             double v;
             if (a == 0) v = q[2] * cb[1] - q[1] * cb[2];
             else if (a == 1) v = q[0] * cb[2] - q[2] * cb[0];
             else if (a == 2) v = q[1] * cb[0] - q[0] * cb[1];
             else v = -cb[a - 3];
-            acc[h] += v;
-            h++;
+            acc[hdiag(a) + b - a] += v;
         }
+    }
     double Me[3];
 PCORE_UNROLL
     for (int r = 0; r < 3; r++) Me[r] = M[r][0] * e[0] + M[r][1] * e[1] + M[r][2] * e[2];
@@ -270,6 +273,7 @@ PCORE_UNROLL
             const double v = __builtin_fabs(A[i][i]);
             if (v > big) { big = v; p = i; }
         }
+        p = uniform_i(p);  // identical on every lane
         tr[k] = p;
 PCORE_UNROLL
         for (int c = k + 1; c < 6; c++)
@@ -299,7 +303,7 @@ PCORE_UNROLL
             }
         }
         const double akk = A[k][k];
-        const bool valid = __builtin_fabs(akk) > 0.0;
+        const bool valid = uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0;
         if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
             zero = true;
             break;
