@@ -145,11 +145,19 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
 // minimum of (float distance, index).
 // Returns false when the cell budget runs out first (or the query is far outside the grid): the caller
 // then scans the whole segment.  Non-finite queries are the caller's business.
-constexpr int kShellBudget = 343;  // cells, r <= 3 around an in-grid query
+// Cell budget of one search: a visited cell costs about as much as two points of the in-order scan (its lower-bound
+// test, the CSR range loads, the loop), so the shells may visit up to half the segment's point count before the scan
+// would have been cheaper, and at least 343 cells (r <= 3 around an in-grid query).  C1 (a 19.2 k-point whole-scene
+// target, `tools/c1_gicp_stats.py`): a fixed 343-cell budget sent the queries of poses that GICP walks away from the
+// scene into the 19.2 k-point scan, 64.7 ms per GICP call; budgets of 2,197 / 9,261 / 35,937 cells gave 18.6 / 18.4 /
+// 18.2 ms, and this rule 19.7 ms (profiles/r03x/).  Measured and dropped: the 343-cell shells followed by an exact
+// search over the grid's list of non-empty cells (an upper bound from the least farthest-corner distance, then the
+// cells whose lower bound is within it) instead of the in-order scan, 37.1 ms.
+__device__ __forceinline__ int shell_budget(int n) { return max(343, n >> 1); }
 
 template <typename Visit, typename Limit>
 __device__ __forceinline__ bool grid_shells(const LabelGrid& g, const int32_t* cell_start, float qx, float qy,
-                                            float qz, Visit&& visit, Limit&& limit) {
+                                            float qz, int budget, Visit&& visit, Limit&& limit) {
     const float fx = (qx - g.ox) * g.inv_c, fy = (qy - g.oy) * g.inv_c, fz = (qz - g.oz) * g.inv_c;
     const float fm = fmaxf(fabsf(fx), fmaxf(fabsf(fy), fabsf(fz)));
     if (!(fm < 65536.0f)) return false;
@@ -203,7 +211,7 @@ __device__ __forceinline__ bool grid_shells(const LabelGrid& g, const int32_t* c
         if (B == INFINITY) return true;  // every cell visited
         B -= e;
         if (B > 0.0f && limit() < B * B * c2) return true;
-        if (visited >= kShellBudget) return false;
+        if (visited >= budget) return false;
     }
 }
 
@@ -337,7 +345,8 @@ __global__ void __launch_bounds__(kGThreads) covariance_grid_kernel(const float4
         }
     };
     const bool ok = isfinite(xi.x) && isfinite(xi.y) && isfinite(xi.z) &&
-                    grid_shells(g, cell_start, xi.x, xi.y, xi.z, visit, [&] { return cnt == k ? nd[k - 1] : INFINITY; });
+                    grid_shells(g, cell_start, xi.x, xi.y, xi.z, shell_budget(n), visit,
+                                [&] { return cnt == k ? nd[k - 1] : INFINITY; });
     if (!ok) {
         cnt = 0;
         for (int j = 0; j < n; j++) {
@@ -401,7 +410,7 @@ __device__ __forceinline__ void grid_nn(const LabelGrid& G, const int32_t* cell_
             if (d < best || (d == best && j >= 0 && oi < j)) { best = d; j = oi; }
         }
     };
-    if (grid_shells(G, cell_start, qx, qy, qz, visit, [&] { return best; })) return;
+    if (grid_shells(G, cell_start, qx, qy, qz, shell_budget(nt), visit, [&] { return best; })) return;
     best = INFINITY;
     j = -1;
     for (int i = 0; i < nt; i++) {
@@ -868,6 +877,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
     __shared__ int sPose, sFlag;
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const Round0 r0{sM0, sS0, sT0};  // wave 0's
+    GPROF_DECL;  // wave 0's phases: [0] the searches of all waves (to the barrier), [1] contributions, [2] tree, [3] LM
     for (;;) {
         __syncthreads();
         if (tid == 0) {
@@ -889,6 +899,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
             iters++;
             float Rf[3][3], tf[3];
             xform_float(x, Rf, tf);
+            GPROF_T(t_w0);
             // correspondences, all waves
             for (int i0 = wave * 64; i0 < P.ns; i0 += NT) {
                 const int i = i0 + lane;
@@ -906,10 +917,9 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 if (act) jbuf[i] = j;
             }
             __syncthreads();
+            GPROF_TD(t_w1, Rf[0][0]);
+            GPROF_ADD(0, t_w0, t_w1);
             if (wave == 0) {
-#ifdef PCORE_GICP_PROFILE
-                unsigned long long gp_acc[kGprof] = {0, 0, 0, 0, 0, 0, 0, 0};  // not reported
-#endif
                 double acc[gicpm::kTerms];
 #pragma unroll
                 for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
@@ -918,9 +928,14 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                     linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
                                            P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, r0, acc GPROF_ARG);
                 }
+                GPROF_TD(t_w2, acc[0]);
                 const double* sys = lds_tree_sum(acc, sRed, lane);
+                GPROF_TD(t_w3, sys[0]);
                 const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
                                             g.trans_eps GPROF_ARG);
+                GPROF_TD(t_w4, st);
+                GPROF_ADD(2, t_w2, t_w3);  // [1]: linearize_round's own marks
+                GPROF_ADD(3, t_w3, t_w4);
                 if (lane == 0) {
                     sFlag = st;
 #pragma unroll
@@ -944,6 +959,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
         __syncthreads();
         if (tid == 0) write_pose(g, P.gp, x, iters);
     }
+    if (wave == 0) GPROF_FLUSH;
 }
 
 constexpr int kGicpWideWpp = 8;
