@@ -604,6 +604,49 @@ def test_evaluate_icp_3dof_whole_scene_targets_matches_oracle(kernel, monkeypatc
     assert _bits_equal(oc.cpu().numpy(), ooc)
 
 
+@pytest.mark.parametrize("kernel", ["narrow", "wide"])
+def test_evaluate_icp_3dof_far_queries_match_oracle(kernel, monkeypatch):
+    """C1's poses that GICP walks away from the scene (the most iterations of the 128): their queries end far from
+    every point of the 19.2 k-point whole-scene target, where the shell search runs past its 343-cell minimum (the
+    budget scales with the segment) or falls back to the in-order scan.  Adjusted poses, iteration counts and costs
+    bit-exact vs the oracle's brute force."""
+    from perception_amd import workloads
+    from tests.helpers import oracle_render_fn
+    c1 = workloads.c1_tabletop(oracle_render_fn)
+    sc = c1.scene
+    core = PoseCore(0)
+    core.upload_meshes(sc.bank.tris, sc.bank.tris_model_count)
+    core.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+    dev = torch.device("cuda", 0)
+    xyz, _ = core.observed_cloud_bounded(torch.from_numpy(sc.depth_raw).to(dev), 4, sc.depth_factor)
+    core.set_observation(torch.from_numpy(c1.src_depth_cm).to(dev), None, xyz, None, 0.0075)
+    monkeypatch.setenv("PCORE_GICP_KERNEL", kernel)
+    n_all = len(c1.poses)
+    tot_all = torch.full((n_all,), float(xyz.shape[0]), dtype=torch.float32, device=dev)
+    _, it_all, _, _, _ = core.evaluate_icp(torch.from_numpy(c1.poses).to(dev), torch.zeros(n_all, dtype=torch.int32,
+                                           device=dev), None, tot_all, cost_type=0, stride=4, sensor_resolution=0.0075)
+    it_all = it_all.cpu().numpy()
+    idx = np.argsort(-it_all, kind="stable")[:2]
+    assert it_all[idx].min() >= 100, it_all[idx]
+    n = len(idx)
+    poses = c1.poses[idx]
+    tot = np.full(n, xyz.shape[0], np.float32)
+    adj, iters, rc, oc, df = core.evaluate_icp(torch.from_numpy(poses).to(dev), torch.zeros(n, dtype=torch.int32,
+                                               device=dev), None, torch.from_numpy(tot).to(dev), cost_type=0,
+                                               stride=4, sensor_resolution=0.0075)
+    assert np.array_equal(iters.cpu().numpy(), it_all[idx])  # batch-invariant
+    oxyz = xyz.cpu().numpy()
+    ocov = oracle.covariances(oxyz)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, poses, np.zeros(n, np.int32), None, sc.width, sc.height, sc.proj,
+        c1.src_depth_cm, None, 1.0, 4, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, ocov, None, None, tot, 0, True,
+        0.0075)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+
+
 def test_pose_lanes_overlapped_batches_match_oracle(three_objects):
     """core.PoseLanes (the bench's two batches in flight): batches submitted round-robin to two contexts on two
     streams, with no synchronisation between them, each give the oracle's costs bit for bit."""
