@@ -108,3 +108,66 @@ extern "C" int stream_check(const float* tri_xyz, int T, int num_streams, int vr
     info[0] = b.passes; info[1] = b.steps; info[2] = (long long)vxyz.size() / 3; info[3] = (long long)b.streams.size();
     return 0;
 }
+
+// LDS bank conflicts of the fused kernel's triangle stage (its three ds_read_b64 gathers of vertex bounds per step,
+// vbd[(slot & 127)], which every step issues for all 64 lanes whatever the pose) under a placement of the ring slots:
+// physical lane of (buffer b, lane l) = mode 0: l; 1: l ^ 16 (b odd); 2: l ^ (8 b); 3: (l + 16 b) mod 64; 4: l ^ (16 b).
+// ds_read_b64 serves two 32-lane groups; a 8-byte entry at index i sits on bank pair i mod 32, and each extra
+// distinct address on a bank pair costs one cycle.  out: [0] extra cycles, [1] group-reads, [2] steps.
+extern "C" int stream_bank_sim(const float* tri_xyz, int T, int num_streams, int vring, int ref_passes, int chunks,
+                               int mode, long long* out) {
+    struct K { uint32_t x, y, z; bool operator==(const K& o) const { return x == o.x && y == o.y && z == o.z; } };
+    struct H { size_t operator()(const K& k) const { return (size_t)k.x * 73856093u ^ (size_t)k.y * 19349663u ^ (size_t)k.z * 83492791u; } };
+    std::unordered_map<K, int, H> idx;
+    std::vector<int> tv(3 * (size_t)T);
+    std::vector<float> vxyz;
+    for (int t = 0; t < T; t++)
+        for (int k = 0; k < 3; k++) {
+            const float* p = tri_xyz + 9 * (size_t)t + 3 * k;
+            K key;
+            std::memcpy(&key.x, p, 4); std::memcpy(&key.y, p + 1, 4); std::memcpy(&key.z, p + 2, 4);
+            auto it = idx.find(key);
+            int id;
+            if (it == idx.end()) { id = (int)vxyz.size() / 3; idx.emplace(key, id); vxyz.insert(vxyz.end(), p, p + 3); }
+            else id = it->second;
+            tv[3 * (size_t)t + k] = id;
+        }
+    pcore::streams::Built b;
+    pcore::streams::build_model(tv, vxyz, 0, num_streams, vring, ref_passes, b, chunks);
+    auto place = [mode](int buf, int l) {
+        switch (mode) {
+            case 1: return (buf & 1) ? (l ^ 16) : l;
+            case 2: return l ^ ((8 * buf) & 63);
+            case 3: return (l + 16 * buf) & 63;
+            case 4: return l ^ ((16 * buf) & 63);
+            default:
+                if (mode >= 100) return (l >= 32) ? (l ^ (mode - 100)) : l;  // upper half XOR m (m < 32)
+                return l;
+        }
+    };
+    long long extra = 0, reads = 0;
+    const long long steps = (long long)b.stris.size() / 64;
+    for (long long s = 0; s < steps; s++) {
+        for (int k = 0; k < 3; k++)
+            for (int g = 0; g < 2; g++) {
+                int cnt[32] = {0};
+                int seen[32][32];
+                for (int l = 0; l < 32; l++) {
+                    const uint32_t ct = b.stris[64 * s + 32 * g + l];
+                    const int slot = (int)((ct >> (9 * k)) & 511u);
+                    const int buf = slot >> 6, ln = slot & 63;
+                    const int vi = (buf & 1) * 64 + place(buf, ln);  // vbd entry
+                    const int bank = vi & 31;
+                    bool dup = false;
+                    for (int q = 0; q < cnt[bank]; q++) dup = dup || seen[bank][q] == vi;
+                    if (!dup) seen[bank][cnt[bank]++] = vi;
+                }
+                int mx = 0;
+                for (int q = 0; q < 32; q++) mx = cnt[q] > mx ? cnt[q] : mx;
+                extra += mx > 0 ? mx - 1 : 0;
+                reads++;
+            }
+    }
+    out[0] = extra; out[1] = reads; out[2] = steps;
+    return 0;
+}
