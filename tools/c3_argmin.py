@@ -61,7 +61,10 @@ def main():
         ok = idx[c1[idx] >= 0]
         win = int(ok[np.argmin(c1[ok])]) if len(ok) else -1  # first minimum = lowest index
         gt_pose = P[g]
-        near = [i for i in ok if (lambda d: d[0] < 10.0 and d[1] < 2.0)(rel(A[i], gt_pose))]
+        def close(i):
+            dt, ang = rel(A[i], gt_pose)
+            return dt < 10.0 and ang < 2.0
+        near = [i for i in ok if close(i)]
         best_near = min((int(c1[i]) for i in near), default=None)
         r = {"object": NAMES[m], "gt_index": int(g), "gt_cost_before": int(c0[g]), "gt_cost_after": int(c1[g]),
              "gt_iters": int(it[g]), "gt_moved_mm_deg": rel(A[g], gt_pose),
