@@ -443,7 +443,7 @@ class ObjectRecognizer:
             icp_time = gpu_s if (p.icp_type == 3 and inp.use_icp) else 0.0
             if p.icp_type == 3 and inp.use_icp:
                 peak_mb = self.core.stats(reset=True)["peak_memory_usage"]  # gpu_stats.peak_memory_usage (MB)
-            self._last_costs = (rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy())
+            self._last_costs_dev = (rc, oc, df)  # read back only on request (_last_costs)
         allreduce_min_keys(keys)
         cost, idx = decode_keys(keys)
         # winning adjusted poses: the owning rank contributes, the others add zeros
@@ -473,6 +473,11 @@ class ObjectRecognizer:
         self.last_stats = EnvStats(scenes_rendered=n_total, scenes_valid=0, time=time.perf_counter() - t0,
                                    icp_time=icp_time, peak_gpu_mem=peak_mb)
         return results
+
+    @property
+    def _last_costs(self):
+        """The last search's per-state rendered / observed / points-diff costs as numpy arrays (diagnostics)."""
+        return tuple(t.cpu().numpy() for t in self._last_costs_dev)
 
     # -- ObjectRecognizer::LocalizeObjectsGreedyRender (object_recognizer.cpp:290-342) -------------
     def localize_objects_greedy_render(self, inp: RecognitionInput) -> LocalizationResult:
