@@ -28,17 +28,21 @@ def hipcc() -> str:
 def flags() -> list:
     # -fno-slp-vectorize: the SLP vectorizer packs adjacent f32 adds / muls into v_pk_*_f32, which gfx950 issues at
     # half the rate of two plain VALU instructions' worth of issue slots plus extra register moves; without it the
-    # fused COST kernel is 4.9 % faster (0.477 -> 0.454 ms per 10k C2 poses, same-box A/B; C3 unchanged)
-    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+    # fused COST kernel is 4.9 % faster (0.477 -> 0.454 ms per 10k C2 poses, same-box A/B; C3 unchanged).
+    # -O2: the fused kernel schedules slightly differently than at -O3 (same registers, 6 waves per SIMD) and the C2
+    # bench ran faster in 4 of 4 alternating pairs, 30.42 vs 30.04 M poses/s on average; C3 unchanged (25.6 / 25.5 ms
+    # per step); the whole GPU suite green (profiles/r03fl/).  The arithmetic is the same at either level
+    # (-ffp-contract=off, no fast-math).
+    return [f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
             "-fno-fast-math", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]
 
 
 def kernel_source_digest() -> str:
-    """SHA-256 (16 hex) of the sources that define the fused COST kernel: ties a committed counter profile
-    (profiles/sq_counters.json) to the code it measured."""
+    """SHA-256 (16 hex) of the compile flags and the sources that define the fused COST kernel: ties a committed
+    counter profile (profiles/sq_counters.json) to the build it measured."""
     import hashlib
 
-    h = hashlib.sha256()
+    h = hashlib.sha256(" ".join(flags()).encode())  # the compile flags too: a profile is of one build
     for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
@@ -50,7 +54,7 @@ def gicp_source_digest() -> str:
     it measured."""
     import hashlib
 
-    h = hashlib.sha256()
+    h = hashlib.sha256(" ".join(flags()).encode())
     for f in ("pcore_gicp.hip", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_internal.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
@@ -61,7 +65,7 @@ def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]  # flags live here
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
