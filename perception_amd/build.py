@@ -31,8 +31,8 @@ def flags() -> list:
     # fused COST kernel is 4.9 % faster (0.477 -> 0.454 ms per 10k C2 poses, same-box A/B; C3 unchanged).
     # -O2: the fused kernel schedules slightly differently than at -O3 (same registers, 6 waves per SIMD) and the C2
     # bench ran faster in 4 of 4 alternating pairs, 30.42 vs 30.04 M poses/s on average; C3 unchanged (25.6 / 25.5 ms
-    # per step); the whole GPU suite green (profiles/r03fl/).  The arithmetic is the same at either level
-    # (-ffp-contract=off, no fast-math).
+    # per step); the whole GPU suite green; -O1 / -Os / -O2 -fno-unroll-loops measured slower or equal (profiles/r03fl/).
+    # The arithmetic is the same at any level (-ffp-contract=off, no fast-math).
     return [f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
             "-fno-fast-math", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]
 
