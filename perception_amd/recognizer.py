@@ -226,6 +226,10 @@ def _dims(model: Model):
 class ObjectRecognizer:
     """ObjectRecognizer + EnvObjectRecognition for the greedy GPU search, driven by PoseCore."""
 
+    # 6-DoF: the successor states stay on the device between IsValidPose and the search launch (TabletopRecognizer
+    # builds its 3-DoF states and inputs on the host)
+    _device_state_path = True
+
     def __init__(self, model_bank: Dict[str, ModelMetaData], camera: CameraIntrinsics,
                  params: Optional[PerchParams] = None, device: int = 0):
         self.bank = model_bank
@@ -316,10 +320,9 @@ class ObjectRecognizer:
         return valid_pose_mask(translations, seg, self._search_radius(model_id),
                                self.params.min_neighbor_points_for_valid_pose, self.device)
 
-    def generate_successor_states(self, inp: RecognitionInput) -> States:
-        """GenerateSuccessorStates (search_env.cpp:7056-7254) over every model's pose list, IsValidPose for all of
-        them in one device call (pcore_count_within: PCL radiusSearch counts in the required object's segment)."""
-        t0 = time.perf_counter()
+    def _state_lists(self, inp: RecognitionInput):
+        """Every model's pose list (poses.txt rows or inp.pose_lists) with its model id, required object id and
+        IsValidPose's squared search radius as float32, concatenated in model order; None when there are none."""
         Ps, models, reqs, r2s = [], [], [], []
         for ii, name in enumerate(self.model_names):
             if inp.pose_lists is not None and name in inp.pose_lists:
@@ -339,8 +342,17 @@ class ObjectRecognizer:
             reqs.append(np.full(len(P), req, np.int32))
             r2s.append(np.full(len(P), np.float32(rad * rad), np.float32))
         if not Ps:
+            return None
+        return np.concatenate(Ps), np.concatenate(models), np.concatenate(reqs), np.concatenate(r2s)
+
+    def generate_successor_states(self, inp: RecognitionInput) -> States:
+        """GenerateSuccessorStates (search_env.cpp:7056-7254) over every model's pose list, IsValidPose for all of
+        them in one device call (pcore_count_within: PCL radiusSearch counts in the required object's segment)."""
+        t0 = time.perf_counter()
+        lists = self._state_lists(inp)
+        if lists is None:
             return States()
-        P, model, req, r2 = np.concatenate(Ps), np.concatenate(models), np.concatenate(reqs), np.concatenate(r2s)
+        P, model, req, r2 = lists
         t1 = time.perf_counter()
         dev = self.device
         q = torch.from_numpy(np.ascontiguousarray(P[:, :3])).to(dev).float()  # float PointXYZ of the translation
@@ -348,6 +360,26 @@ class ObjectRecognizer:
         t2 = time.perf_counter()
         ok = counts >= self.params.min_neighbor_points_for_valid_pose
         out = States(model[ok], req[ok], P[ok])
+        self.states_timing = {"lists_s": t1 - t0, "valid_s": t2 - t1, "filter_s": time.perf_counter() - t2}
+        return out
+
+    def _successor_states_device(self, inp: RecognitionInput):
+        """generate_successor_states with the states kept on the device: (model int32, required object int32, pose
+        float64 x 7) tensors of the states that pass IsValidPose, in the same order, or None.  The pose rows go to
+        the device once; the filter is a device index (the 6-DoF search path)."""
+        t0 = time.perf_counter()
+        lists = self._state_lists(inp)
+        if lists is None:
+            return None
+        P, model, req, r2 = lists
+        t1 = time.perf_counter()
+        dev = self.device
+        P_d = torch.from_numpy(P).to(dev)
+        req_d = torch.from_numpy(req).to(dev)
+        counts = self.core.count_within(P_d[:, :3].float(), req_d, torch.from_numpy(r2).to(dev))
+        keep = torch.nonzero(counts >= self.params.min_neighbor_points_for_valid_pose).squeeze(1)
+        t2 = time.perf_counter()
+        out = (torch.from_numpy(model).to(dev)[keep], req_d[keep], P_d[keep])
         self.states_timing = {"lists_s": t1 - t0, "valid_s": t2 - t1, "filter_s": time.perf_counter() - t2}
         return out
 
@@ -366,14 +398,17 @@ class ObjectRecognizer:
 
     def _poses_device(self, states) -> torch.Tensor:
         """The states' search poses on the device (pcore_state_poses: _pose_in_cam's arithmetic, bit for bit)."""
-        cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
         if not len(states):
             return torch.zeros((0, 16), dtype=torch.float32, device=self.device)
+        st = torch.from_numpy(np.ascontiguousarray(states.pose, np.float64)).to(self.device)
+        return self._state_poses_dev(st, torch.from_numpy(states.model.copy()).to(self.device))
+
+    def _state_poses_dev(self, pose: torch.Tensor, model: torch.Tensor) -> torch.Tensor:
+        """pcore_state_poses of device state rows (float64 x 7) and model ids."""
+        cam_matrix = np.linalg.inv(self.camera_pose @ CAM_TO_BODY)
         if getattr(self, "_pre_dev", None) is None or self._pre_dev.shape[0] != len(self.preprocess):
             self._pre_dev = torch.from_numpy(np.stack(self.preprocess).reshape(-1, 16).astype(np.float64)).to(self.device)
-        st = torch.from_numpy(np.ascontiguousarray(states.pose, np.float64)).to(self.device)
-        return self.core.state_poses(st, torch.from_numpy(states.model.copy()).to(self.device), cam_matrix,
-                                     self._pre_dev)
+        return self.core.state_poses(pose.contiguous(), model.contiguous(), cam_matrix, self._pre_dev)
 
     def _pose_in_cam(self, states) -> np.ndarray:
         """GetStateImagesUnifiedGPU pose building (search_env.cpp:1535-1576) on the host: inv(cam_z_front) *
@@ -392,28 +427,40 @@ class ObjectRecognizer:
     def compute_greedy_render_poses(self, inp: RecognitionInput):
         t0 = time.perf_counter()
         p = self.params
-        states = self.generate_successor_states(inp)
+        if self._device_state_path:
+            dstates = self._successor_states_device(inp)
+            n_total = 0 if dstates is None else int(dstates[0].shape[0])
+        else:
+            states = self.generate_successor_states(inp)
+            n_total = len(states)
         t_states = time.perf_counter()
-        n_total = len(states)
         K = len(self.models)
         world, rank = 1, 0
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
         lo, hi = shard_range(n_total, rank, world)
-        mine = states[lo:hi]
+        n = hi - lo
         keys = torch.full((K,), PCORE_KEY_NONE, dtype=torch.int64, device=self.device)
         adj_all = None
         icp_time = 0.0
         gpu_s = 0.0
         peak_mb = float(torch.cuda.max_memory_allocated(self.device)) / 1024.0 / 1024.0
         t_build = t_states
-        if len(mine):
-            poses = self._poses_device(mine)
-            pm = torch.from_numpy(mine.model.copy()).to(self.device)
-            pl = self._pose_labels(mine)
-            tot = torch.from_numpy(self._obs_totals(mine)).to(self.device)
+        if n > 0:
+            if self._device_state_path:
+                model_d, req_d, pose_d = (t[lo:hi] for t in dstates)
+                poses = self._state_poses_dev(pose_d, model_d)
+                pm = model_d.contiguous()
+                pl = req_d.contiguous()  # pose_segmentation_label: the required object id (6-DoF)
+                seg = torch.from_numpy(np.append(self.segmented_count, 0.0).astype(np.float32)).to(self.device)
+                tot = seg[torch.clamp(req_d, max=seg.shape[0] - 1).long()]  # _obs_totals on the device
+            else:
+                mine = states[lo:hi]
+                poses = self._poses_device(mine)
+                pm = torch.from_numpy(mine.model.copy()).to(self.device)
+                pl = self._pose_labels(mine)
+                tot = torch.from_numpy(self._obs_totals(mine)).to(self.device)
             cost_type = self._cost_type()
-            n = len(mine)
             rc = torch.empty(n, dtype=torch.float32, device=self.device)
             oc = torch.empty_like(rc)
             df = torch.empty_like(rc)

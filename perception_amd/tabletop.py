@@ -158,6 +158,8 @@ def grid_states(table: TableParams, model_id: int, dims, projected_xy: np.ndarra
 class TabletopRecognizer(ObjectRecognizer):
     """ObjectRecognizer in the 3-DoF GPU mode (use_external_pose_list = 0)."""
 
+    _device_state_path = False  # the 3-DoF grid states and their inputs are built on the host
+
     def __init__(self, model_bank: Dict[str, ModelMetaData], camera: CameraIntrinsics, table: TableParams,
                  params: Optional[PerchParams] = None, device: int = 0):
         super().__init__(model_bank, camera, params or pr2_gpu_params(), device)
