@@ -205,6 +205,39 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
     }
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(gpus: int) -> int:
+    """`bench.py --gpus N` run as a single process (no WORLD_SIZE in the environment): start N rank processes
+    (one per GPU, torch.distributed.run on 127.0.0.1) with the same arguments and return their exit code.  The
+    parent never touches the GPU (torch.cuda.device_count() does not initialise HIP on this image) and never
+    re-execs: the ranks are children, and rank 0 prints the JSON line."""
+    import subprocess
+
+    import torch
+
+    backend = os.environ.get("PCORE_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < gpus:
+        print(f"bench.py: --gpus {gpus} needs {gpus} GPUs for one RCCL rank per GPU, {ndev} visible "
+              f"(PCORE_DIST_BACKEND=gloo rehearses several ranks on one GPU)", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -217,6 +250,16 @@ def main():
     ap.add_argument("--c3-steps", type=int, default=3, help="timed C3 (GICP) steps; 0 skips the C3 leg")
     ap.add_argument("--c3-warmup", type=int, default=1)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # this process only waits for its N rank children
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU with matching "
+              f"--nproc-per-node and --gpus", file=sys.stderr, flush=True)
+        sys.exit(2)
 
     import torch
     from perception_amd import distributed as pdist
@@ -224,12 +267,16 @@ def main():
     from perception_amd._native import PCORE_KEY_NONE
     from perception_amd.core import decode_keys
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     # one rank per GPU; the modulo only matters for a several-ranks-per-GPU rehearsal (PCORE_DIST_BACKEND=gloo)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     pdist.init_from_env()
+    joined = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    if joined != world:
+        raise SystemExit(f"bench.py: {joined} ranks joined, WORLD_SIZE={world}")
+    # GPUs the ranks run on: one per rank over RCCL; fewer only in a gloo rehearsal (several ranks per GPU)
+    devices = min(world, max(torch.cuda.device_count(), 1))
     dev = torch.device("cuda", local)
 
     w = workloads.build(poses_per_model=args.poses, device=local, rank=rank)
@@ -394,7 +441,7 @@ def main():
         "metric": "candidate poses rendered+scored/sec @640x480",
         "value": value,
         "unit": "poses/s",
-        "n_gpus": world,
+        "n_gpus": joined,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
@@ -406,7 +453,8 @@ def main():
         "config": {"workload": "C2: 1 YCB mesh (12,288 tris), 10k 6-DoF poses/GPU render+score, 640x480, "
                                "stride 8, no ICP", "poses_per_gpu": n, "width": w.scene.width,
                    "height": w.scene.height, "stride": s, "parallelism": f"pose-shard x{world}",
-                   "batches_in_flight": L},
+                   "batches_in_flight": L, "ranks": joined, "devices": devices,
+                   "dist_backend": torch.distributed.get_backend() if joined > 1 else None},
         "roofline": roofline,
         "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},
     }

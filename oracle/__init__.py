@@ -234,6 +234,9 @@ def _gicp_lib():
         L.orc_sin_d.argtypes = [c_double]
         L.orc_cos_d.restype = c_double
         L.orc_cos_d.argtypes = [c_double]
+        for fn in (L.orc_cube_rn, L.orc_lm_gain):
+            fn.restype = c_double
+            fn.argtypes = [c_double]
         L.orc_gicp_nn.argtypes = [_f32p, c_int, _f32p, c_int, _i32p]
         L._gicp_typed = True
     return L
@@ -315,6 +318,14 @@ def sin_d(x):
 
 def cos_d(x):
     return _gicp_lib().orc_cos_d(float(x))
+
+
+def cube_rn(u):
+    return _gicp_lib().orc_cube_rn(float(u))
+
+
+def lm_gain(rho):
+    return _gicp_lib().orc_lm_gain(float(rho))
 
 
 def gicp_nn(q, tgt):

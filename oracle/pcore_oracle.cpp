@@ -895,6 +895,8 @@ void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d) {
 
 double orc_sin_d(double x) { return pcore::dmath::sin_d(x); }
 double orc_cos_d(double x) { return pcore::dmath::cos_d(x); }
+double orc_cube_rn(double u) { return pcore::gicpm::cube_rn(u); }
+double orc_lm_gain(double rho) { return pcore::gicpm::lm_gain(rho); }
 
 // The spec's correspondence of float queries (n x 3) in a target segment: key scan (segments <= kKeyScanMax) or
 // plain float squared distance; out_j: -1 for none.

@@ -137,6 +137,8 @@ void orc_gicp_se3_exp(const double* a6, double* out_T);
 void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d);
 double orc_sin_d(double x);
 double orc_cos_d(double x);
+double orc_cube_rn(double u);   // step_lm's std::pow(u, 3), rounded once
+double orc_lm_gain(double rho); // max(1/3, 1 - (2 rho - 1)^3)
 void orc_gicp_nn(const float* q, int n, const float* tgt_xyz, int nt, int32_t* out_j);
 
 /* concatenate_transforms (renderer.cu:1412-1429): pose' = init_from_eigen((float(T) * to_eigen(pose,100)), 100). */

@@ -498,10 +498,22 @@ PCORE_UNROLL
     return (y0 - yi) / den;
 }
 
-// accepted step: lambda <- lambda * max(1/3, 1 - (2 rho - 1)^3), the cube as (u u) u; lm_gain is the factor
+// u^3 rounded once, as fast_gicp's std::pow(2 rho - 1, 3) (glibc's pow is correctly rounded up to its < 0.52 ulp
+// worst cases; the two-rounding (u u) u differs from it by an ulp for ~1 in 4 inputs): u u = p + e and p u = c + e2
+// exactly (fma), so u^3 = c + e2 + e u and c + (e2 + e u) is the correctly rounded cube unless u^3 lies within
+// ~2^-104 |u^3| of a rounding boundary (tests/test_gicp_spec.py checks it against exact rationals and against pow)
+PCORE_GHD double cube_rn(double u) {
+    const double p = u * u;
+    const double e = fma(u, u, -p);
+    const double c = p * u;
+    const double e2 = fma(p, u, -c);
+    return c + (e2 + e * u);
+}
+
+// accepted step: lambda <- lambda * max(1/3, 1 - (2 rho - 1)^3); lm_gain is the factor
 PCORE_GHD double lm_gain(double rho) {
     const double u = 2.0 * rho - 1.0;
-    const double f = 1.0 - u * u * u;
+    const double f = 1.0 - cube_rn(u);
     const double third = 1.0 / 3.0;
     return third < f ? f : third;  // std::max(1/3, f)
 }

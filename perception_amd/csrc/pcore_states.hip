@@ -2,7 +2,7 @@
 // (the callers of render_cuda_multi_unified on the pose path):
 //
 //   state_pose_kernel    GetStateImagesUnifiedGPU's pose building (search_env.cpp:1535-1576): for every state
-//                        (x y z qx qy qz qw), inv(cam_z_front) * ContPose::GetTransform * preprocess[model], then
+//                        (x y z qx qy qz qw), inv(cam_z_front) * (ContPose::GetTransform * preprocess[model]), then
 //                        mat4x4::init_from_eigen(., 100) (model.h:89-107) -- one thread per state, double.
 //   count_within_kernel  IsValidPose's neighbour count (search_env.cpp:359-396): points of the query's label
 //                        segment strictly within the radius, PCL KdTreeFLANN radiusSearch semantics (float query
@@ -42,7 +42,8 @@ __global__ void __launch_bounds__(256) state_pose_kernel(StatePoseArgs a) {
     const double* s = a.states + (size_t)7 * i;
     // quat_xyzw_to_matrix: normalised quaternion -> rotation (Eigen::Quaterniond::toRotationMatrix)
     double x = s[3], y = s[4], z = s[5], w = s[6];
-    const double nrm = sqrt(((x * x + y * y) + z * z) + w * w);
+    // Eigen's squaredNorm of the 4 coefficients (x, y, z, w) in 2-wide SSE2 packets: (x^2 + z^2) + (y^2 + w^2)
+    const double nrm = sqrt((x * x + z * z) + (y * y + w * w));
     x = x / nrm;
     y = y / nrm;
     z = z / nrm;
@@ -67,19 +68,20 @@ __global__ void __launch_bounds__(256) state_pose_kernel(StatePoseArgs a) {
     int m = a.model[i];
     m = m < 0 ? 0 : (m >= a.num_models ? a.num_models - 1 : m);  // the caller checks the ids
     const double* B = a.preprocess + (size_t)16 * m;
+    // search_env.cpp:1567-1571: transform = T * preprocess first, then pose_in_cam = cam_matrix * transform
     double M1[4][4];
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++)
-            M1[r][c] = dot4(a.cam[4 * r], a.cam[4 * r + 1], a.cam[4 * r + 2], a.cam[4 * r + 3], T[0][c], T[1][c],
-                            T[2][c], T[3][c]);
+            M1[r][c] = dot4(T[r][0], T[r][1], T[r][2], T[r][3], B[c], B[4 + c], B[8 + c], B[12 + c]);
     float* o = a.out + (size_t)16 * i;
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            const double v = dot4(M1[r][0], M1[r][1], M1[r][2], M1[r][3], B[c], B[4 + c], B[8 + c], B[12 + c]);
+            const double v = dot4(a.cam[4 * r], a.cam[4 * r + 1], a.cam[4 * r + 2], a.cam[4 * r + 3], M1[0][c],
+                                  M1[1][c], M1[2][c], M1[3][c]);
             o[4 * r + c] = r < 3 ? (float)(v * 100.0) : (float)v;
         }
 }

@@ -12,7 +12,9 @@
 """
 from __future__ import annotations
 
+import hashlib
 import os
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -194,7 +196,10 @@ def read_poses_txt(path: str) -> np.ndarray:
     line (what write_poses_txt and the reference's scripts produce) are parsed in one pass; anything else
     line by line."""
     with open(path) as f:
-        text = f.read()
+        return _parse_poses_text(f.read())
+
+
+def _parse_poses_text(text: str) -> np.ndarray:
     lines = text.split("\n")
     end = next((i for i, ln in enumerate(lines) if not ln), len(lines))
     lines = lines[:end]
@@ -205,22 +210,30 @@ def read_poses_txt(path: str) -> np.ndarray:
     return np.asarray(rows, np.float64).reshape(-1, 7)
 
 
-_POSES_CACHE: dict = {}
+_POSES_CACHE: "OrderedDict[tuple, np.ndarray]" = OrderedDict()
+_POSES_CACHE_MAX = 64
 
 
-def read_poses_txt_cached(path: str) -> np.ndarray:
-    """read_poses_txt, parsed once per file version: keyed by (path, size, mtime_ns), so an unchanged poses.txt
-    is not parsed again on the next search (the reference re-reads it every GenerateSuccessorStates; the content,
-    and so the result, is the same).  Returns a read-only array."""
-    st = os.stat(path)
-    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns)
+def read_poses_txt_cached(path: str, use_cache: bool = True) -> np.ndarray:
+    """read_poses_txt, parsed once per file CONTENT: keyed by (path, BLAKE2b digest of the bytes), so a poses.txt
+    rewritten in place -- whatever its size and timestamps -- is parsed again, and an unchanged one is only read and
+    hashed (the reference re-reads and re-parses it every GenerateSuccessorStates; the content, and so the result, is
+    the same).  Least-recently-used eviction past 64 files.  use_cache=False (or PCORE_POSES_CACHE=0) parses
+    every time.  Returns a read-only array."""
+    if not use_cache or os.environ.get("PCORE_POSES_CACHE", "1") == "0":
+        return read_poses_txt(path)
+    with open(path, "rb") as f:
+        data = f.read()
+    key = (os.path.abspath(path), hashlib.blake2b(data, digest_size=16).digest())
     hit = _POSES_CACHE.get(key)
     if hit is None:
-        hit = read_poses_txt(path)
+        hit = _parse_poses_text(data.decode())
         hit.setflags(write=False)
-        if len(_POSES_CACHE) > 64:
-            _POSES_CACHE.clear()
         _POSES_CACHE[key] = hit
+        while len(_POSES_CACHE) > _POSES_CACHE_MAX:
+            _POSES_CACHE.popitem(last=False)
+    else:
+        _POSES_CACHE.move_to_end(key)
     return hit
 
 

@@ -61,7 +61,7 @@ def to_eigen(mat: np.ndarray, scale_factor: int = 100) -> np.ndarray:
 def quat_xyzw_to_matrix(q: Sequence[float]) -> np.ndarray:
     """Normalised quaternion (x, y, z, w) -> 3x3 rotation (Eigen::Quaterniond::toRotationMatrix)."""
     x, y, z, w = (float(v) for v in q)
-    n = np.sqrt(x * x + y * y + z * z + w * w)
+    n = np.sqrt((x * x + z * z) + (y * y + w * w))  # Eigen squaredNorm in 2-wide packets (SSE2)
     x, y, z, w = x / n, y / n, z / n, w / n
     return np.array([
         [1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
@@ -105,7 +105,7 @@ def quat_xyzw_to_matrix_batch(q: np.ndarray) -> np.ndarray:
     """quat_xyzw_to_matrix over (N, 4) quaternions: the same float64 operations per element."""
     q = np.asarray(q, dtype=np.float64).reshape(-1, 4)
     x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
-    n = np.sqrt(x * x + y * y + z * z + w * w)
+    n = np.sqrt((x * x + z * z) + (y * y + w * w))
     x, y, z, w = x / n, y / n, z / n, w / n
     R = np.empty((len(q), 3, 3))
     R[:, 0, 0] = 1 - 2 * (y * y + z * z)
@@ -131,12 +131,13 @@ def pose_matrix_batch(translations: np.ndarray, quats_xyzw: np.ndarray) -> np.nd
 
 
 def chain_matmul_batch(A: np.ndarray, T: np.ndarray, B: np.ndarray) -> np.ndarray:
-    """A @ T[i] @ B[i] for every i, each product summed over k in index order as a plain 4x4 matmul loop
-    ((a0 b0 + a1 b1) + a2 b2) + a3 b3, independent of BLAS blocking and thread count."""
+    """A @ (T[i] @ B[i]) for every i -- the grouping of search_env.cpp:1567-1571 (transform = T * preprocess, then
+    cam_matrix * transform) -- each product summed over k in index order as Eigen's 4x4 lazy product does without
+    FMA, ((a0 b0 + a1 b1) + a2 b2) + a3 b3, independent of BLAS blocking and thread count."""
     def mm(X, Y):
         return (((X[..., :, 0, None] * Y[..., None, 0, :] + X[..., :, 1, None] * Y[..., None, 1, :])
                  + X[..., :, 2, None] * Y[..., None, 2, :]) + X[..., :, 3, None] * Y[..., None, 3, :])
-    return mm(mm(np.broadcast_to(A, T.shape), T), B)
+    return mm(np.broadcast_to(A, T.shape), mm(T, B))
 
 
 def pose_matrix(translation: Sequence[float], quat_xyzw: Sequence[float]) -> np.ndarray:

@@ -396,6 +396,28 @@ class ObjectRecognizer:
         seg = np.append(self.segmented_count, 0.0).astype(np.float32)
         return seg[np.minimum(states.req, len(seg) - 1)]
 
+    # the same two inputs on the device path (_device_state_path): device tensors of the states' required object ids
+    # in, device tensors out.  A subclass that overrides a host hook overrides its device twin too, or turns the
+    # device path off (_check_state_hooks refuses the mix, which would silently use the 6-DoF inputs).
+    def _pose_labels_dev(self, req: torch.Tensor) -> Optional[torch.Tensor]:
+        """_pose_labels on the device: the required object id (6-DoF)."""
+        return req.contiguous()
+
+    def _obs_totals_dev(self, req: torch.Tensor) -> torch.Tensor:
+        """_obs_totals on the device: segmented_observed_point_count[req], 0 past the segmented objects."""
+        seg = torch.from_numpy(np.append(self.segmented_count, 0.0).astype(np.float32)).to(req.device)
+        return seg[torch.clamp(req, max=seg.shape[0] - 1).long()]
+
+    def _check_state_hooks(self):
+        if not self._device_state_path:
+            return
+        cls = type(self)
+        for host, dev in (("_pose_labels", "_pose_labels_dev"), ("_obs_totals", "_obs_totals_dev")):
+            if getattr(cls, host) is not getattr(ObjectRecognizer, host) and \
+                    getattr(cls, dev) is getattr(ObjectRecognizer, dev):
+                raise TypeError(f"{cls.__name__} overrides {host} but not {dev}: override both, or set "
+                                f"_device_state_path = False")
+
     def _poses_device(self, states) -> torch.Tensor:
         """The states' search poses on the device (pcore_state_poses: _pose_in_cam's arithmetic, bit for bit)."""
         if not len(states):
@@ -427,6 +449,7 @@ class ObjectRecognizer:
     def compute_greedy_render_poses(self, inp: RecognitionInput):
         t0 = time.perf_counter()
         p = self.params
+        self._check_state_hooks()
         if self._device_state_path:
             dstates = self._successor_states_device(inp)
             n_total = 0 if dstates is None else int(dstates[0].shape[0])
@@ -451,9 +474,8 @@ class ObjectRecognizer:
                 model_d, req_d, pose_d = (t[lo:hi] for t in dstates)
                 poses = self._state_poses_dev(pose_d, model_d)
                 pm = model_d.contiguous()
-                pl = req_d.contiguous()  # pose_segmentation_label: the required object id (6-DoF)
-                seg = torch.from_numpy(np.append(self.segmented_count, 0.0).astype(np.float32)).to(self.device)
-                tot = seg[torch.clamp(req_d, max=seg.shape[0] - 1).long()]  # _obs_totals on the device
+                pl = self._pose_labels_dev(req_d)  # pose_segmentation_label
+                tot = self._obs_totals_dev(req_d)  # pose_observed_points_total
             else:
                 mine = states[lo:hi]
                 poses = self._poses_device(mine)
@@ -487,9 +509,12 @@ class ObjectRecognizer:
                                    select=(keys, lo, K))
             torch.cuda.synchronize(self.device)
             gpu_s = time.perf_counter() - ti
-            icp_time = gpu_s if (p.icp_type == 3 and inp.use_icp) else 0.0
             if p.icp_type == 3 and inp.use_icp:
-                peak_mb = self.core.stats(reset=True)["peak_memory_usage"]  # gpu_stats.peak_memory_usage (MB)
+                # gpu_stats of the call (renderer.cu:1736-1739): the GICP stage's own time and the peak memory;
+                # search_env.cpp:1715-1716 adds icp_runtime (seconds) to env_stats_.icp_time
+                st = self.core.stats(reset=True)
+                icp_time = float(st["icp_runtime"])
+                peak_mb = st["peak_memory_usage"]  # gpu_stats.peak_memory_usage (MB)
             self._last_costs_dev = (rc, oc, df)  # read back only on request (_last_costs)
         allreduce_min_keys(keys)
         cost, idx = decode_keys(keys)
@@ -500,6 +525,10 @@ class ObjectRecognizer:
                 win[m] = adj_all[int(idx[m]) - lo]
         if world > 1:
             torch.distributed.all_reduce(win, op=torch.distributed.ReduceOp.SUM)
+            # stats: the slowest rank's GICP stage and the largest peak memory (the shards run concurrently)
+            st = torch.tensor([icp_time, peak_mb], dtype=torch.float64, device=self.device)
+            torch.distributed.all_reduce(st, op=torch.distributed.ReduceOp.MAX)
+            icp_time, peak_mb = float(st[0]), float(st[1])
         win = win.cpu().numpy()
         results = []
         for m in range(K):
@@ -535,6 +564,12 @@ class ObjectRecognizer:
         t_input = time.perf_counter() - t0
         res = self.compute_greedy_render_poses(inp)
         self.last_timing["set_input_s"] = t_input
+        return self.localization_result(res)
+
+    def localization_result(self, res) -> LocalizationResult:
+        """compute_greedy_render_poses' (model, cost, index, ContPose) tuples -> the outputs of
+        LocalizeObjectsGreedyRender (object_recognizer.cpp:318-337): per detected object the raw-model-to-scene
+        transform, the preprocessing transform, the pose and the model name."""
         out = LocalizationResult([], [], [], [], [], [], self.last_stats)
         for m, cost, idx, cont in res:
             # GetRawModelToSceneTransform (object_model.cpp:502-510): ContPose transform * preprocessing
@@ -555,5 +590,7 @@ class ObjectRecognizer:
                     result.preprocessing_transforms)]
         pio.write_output_poses(os.path.join(out_dir, "output_poses.txt"), objs)
         s = result.stats
-        pio.write_output_stats(os.path.join(out_dir, "output_stats.txt"), s.scenes_rendered, s.scenes_valid, 0,
-                               s.time, 0, s.icp_time, s.peak_gpu_mem)
+        # object_recognizer.cpp:312-318: the planning stats of the greedy search are expands = scenes_rendered,
+        # time = the env's time, cost 0
+        pio.write_output_stats(os.path.join(out_dir, "output_stats.txt"), s.scenes_rendered, s.scenes_valid,
+                               s.scenes_rendered, s.time, 0, s.icp_time, s.peak_gpu_mem)

@@ -1,6 +1,7 @@
 """Independent numpy restatement of fast_gicp's published GICP (test reference only).
 
-Shares no arithmetic with perception_amd/csrc/pcore_gicp_math.h: the per-point step is the dense 3x3 form
+Shares no arithmetic with perception_amd/csrc/pcore_gicp_math.h or the oracle's covariances: the source / target
+covariances are numpy's (covariances: lexsort k-NN, eigh normal), the per-point step is the dense 3x3 form
 (M = inv(C_t + R C_s R^T) by numpy, J = [skew(T s) | -I], H = sum J^T M J, b = sum J^T M e, y = sum e^T M e),
 the solve is numpy.linalg.solve, the SE(3) exponential is scipy's matrix exponential of the twist, and the
 Levenberg-Marquardt control is LsqRegistration::step_lm / computeTransformation as published (lm_init_lambda_factor
@@ -15,6 +16,50 @@ import numpy as np
 import scipy.linalg as sla
 
 import oracle
+
+
+def covariances(xyz, k=oracle.GICP_K):
+    """fast_gicp calculate_covariances (k nearest points of the same cloud, the point itself included; double mean and
+    covariance over them) with the PLANE regularisation U diag(1, 1, 1e-3) V^T, here through numpy: float squared
+    distances ordered by (distance, index) with lexsort, numpy means, and the normal as eigh's smallest eigenvector
+    (U diag(1, 1, 1e-3) U^T = I - (1 - 1e-3) n n^T for a symmetric covariance).  -> (n, 6) upper triangles."""
+    p = np.asarray(xyz, np.float32).reshape(-1, 3)
+    n = len(p)
+    out = np.zeros((n, 6))
+    if n == 0:
+        return out
+    ke = min(k, n)
+    for a in range(0, n, 256):  # blocks of query rows: whole-scene clouds (~20k points) fit in memory
+        d = p[a:a + 256, None, :] - p[None, :, :]
+        d2 = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]  # float32
+        kth = np.partition(d2, ke - 1, axis=1)[:, ke - 1]
+        for r in range(len(d2)):
+            cand = np.nonzero(d2[r] <= kth[r])[0]  # every point that can be among the k nearest, index order
+            nb = cand[np.lexsort((cand, d2[r, cand]))][:ke]
+            q = p[nb].astype(np.float64)
+            c = q - q.mean(0)
+            C = c.T @ c / ke
+            w, V = np.linalg.eigh(C)
+            nrm = V[:, 0]
+            R = np.eye(3) - (1.0 - 1e-3) * np.outer(nrm, nrm)
+            out[a + r] = R[[0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]]
+    return out
+
+
+def concat_pose(T, pose16):
+    """concatenate_transforms (renderer.cu:1412-1429): init_from_eigen((Isometry3f T).matrix() * to_eigen(pose, 100),
+    100) -- rows 0-2 of the mat4x4 divided by 100 in float (model.h:108-127), the float 4x4 product summed in index
+    order (Eigen's Matrix4f lazy product without FMA), then rows 0-2 times 100 in double and rounded to float
+    (model.h:89-107)."""
+    P = np.asarray(pose16, np.float32).reshape(4, 4).copy()
+    P[:3, :] = P[:3, :] / np.float32(100.0)
+    Tf = np.asarray(T, np.float64).astype(np.float32)
+    out = np.zeros((4, 4), np.float32)
+    for r in range(4):
+        for c in range(4):
+            out[r, c] = ((Tf[r, 0] * P[0, c] + Tf[r, 1] * P[1, c]) + Tf[r, 2] * P[2, c]) + Tf[r, 3] * P[3, c]
+    out[:3, :] = (out[:3, :].astype(np.float64) * 100.0).astype(np.float32)
+    return out.reshape(16)
 
 
 def sym3(c6):

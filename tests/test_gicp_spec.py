@@ -198,3 +198,89 @@ def test_max_iteration_poses_are_two_cycles(c3_pairs):
             for P in range(1, 9):
                 assert not any(np.array_equal(X[k].view(np.uint64), X[k - P].view(np.uint64)) for k in range(P, 150))
     assert n_cycles >= 2
+
+
+def test_cube_rn_is_correctly_rounded():
+    """step_lm's (2 rho - 1)^3 (fast_gicp: std::pow(.., 3)) is computed as one correctly rounded cube
+    (pcore_gicp_math.h cube_rn), checked against exact rationals; the two-rounding (u u) u it replaced differs from
+    the exact cube on ~1 in 4 inputs, glibc's pow on ~1 in 1000.  lm_gain = max(1/3, 1 - cube)."""
+    from fractions import Fraction
+
+    rng = np.random.default_rng(12)
+    us = np.concatenate([rng.uniform(-1, 1, 6000), rng.uniform(-3, 3, 1000), np.geomspace(1e-200, 1, 200),
+                         -np.geomspace(1e-12, 1, 100), [0.0, -0.0, 1.0, -1.0, 0.5, 2.0 ** -30]])
+    naive = 0
+    for u in us:
+        exact = float(Fraction(float(u)) ** 3)
+        assert oracle.cube_rn(u) == exact, u
+        naive += ((u * u) * u) != exact
+    assert naive > len(us) // 20  # the rounding mattered
+    for rho in (-5.0, -0.3, 0.0, 0.25, 0.5, 0.75, 0.9, 1.0, 1.7, 3.0):
+        u = Fraction(2.0 * rho - 1.0)  # 2 rho - 1 as the double the code forms
+        assert oracle.lm_gain(rho) == max(1.0 / 3.0, 1.0 - float(u ** 3)), rho
+
+
+@pytest.fixture(scope="module")
+def c3_pairs_120():
+    """120 C3-style candidates (24 per object around the ground truth), their clouds, and BOTH covariance sets: the
+    oracle's and tests/gicp_reference.py's numpy ones (lexsort k-NN, eigh normal)."""
+    case = SceneCase(names=C3_NAMES, n_poses=24, seed=7)
+    sc = case.scene
+    depth = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses, case.pose_model, case.pose_label,
+                                sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0)
+    seg = {}
+    out = []
+    for i in range(len(case.poses)):
+        xyz = oracle.depth_to_cloud(depth[i], 8, sc.cx, sc.cy, sc.fx, sc.fy, 100.0)[0]
+        lab = int(case.pose_label[i])
+        tgt = case.obs_xyz[case.label_start[lab]:case.label_end[lab]]
+        if len(xyz) == 0 or len(tgt) == 0:
+            continue
+        if lab not in seg:
+            seg[lab] = (oracle.covariances(tgt), gref.covariances(tgt))
+        out.append((xyz, oracle.covariances(xyz), gref.covariances(xyz), tgt) + seg[lab])
+    return out
+
+
+def test_gicp_independent_chain_120_c3_poses(c3_pairs_120):
+    """>= 100 C3 candidates, the capped (150-iteration) ones included, through a chain that
+    shares nothing with the product's GICP header -- numpy covariances on both clouds, numpy / scipy LM -- against the
+    oracle (the GPU's arithmetic, bit-exact with the kernels): equal iteration counts, transforms within 1e-9."""
+    iters = []
+    for src, scov_o, scov_g, tgt, tcov_o, tcov_g in c3_pairs_120:
+        assert np.abs(scov_o - scov_g).max() < 1e-12
+        T1, it1 = oracle.gicp(src, scov_o, tgt, tcov_o)
+        T2, it2 = gref.gicp(src, scov_g, tgt, tcov_g)
+        assert it1 == it2
+        assert np.abs(T1 - T2).max() < 1e-9
+        iters.append(it1)
+    iters = np.array(iters)
+    assert len(iters) >= 100 and (iters >= 150).sum() >= 20 and (iters < 150).sum() >= 20
+
+
+def test_gicp_whole_scene_targets_independent_chain():
+    """C1's 3-DoF table-top GICP against the WHOLE observed cloud (19.2 k targets at stride 4:
+    the segments above 2,048 targets that gicp_wide_kernel's exact grid shell search serves, and the plain float
+    distance rule), the two 150-iteration poses that GICP walks away from the scene included: oracle vs the numpy
+    chain with numpy covariances, equal iterations, transforms within 1e-9."""
+    from perception_amd import workloads
+    from tests.helpers import oracle_render_fn
+
+    c1 = workloads.c1_tabletop(oracle_render_fn)
+    sc = c1.scene
+    obs, _ = oracle.depth_to_cloud_bounded(sc.depth_raw, 4, sc.cx, sc.cy, sc.fx, sc.fy, sc.depth_factor)
+    assert len(obs) > 2048 * 4
+    tcov_o, tcov_g = oracle.covariances(obs), gref.covariances(obs)
+    assert np.abs(tcov_o - tcov_g).max() < 1e-12
+    idx = np.array([c1.gt_index, 90, 66, 3], np.int64)  # 90: 150 iterations, 66: 47 (oracle, this scene)
+    depth = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, c1.poses[idx], np.zeros(len(idx), np.int32),
+                                None, sc.width, sc.height, sc.proj, c1.src_depth_cm, None, 1.0)
+    iters = []
+    for i in range(len(idx)):
+        src = oracle.depth_to_cloud(depth[i], 4, sc.cx, sc.cy, sc.fx, sc.fy, 100.0)[0]
+        T1, it1 = oracle.gicp(src, oracle.covariances(src), obs, tcov_o)
+        T2, it2 = gref.gicp(src, gref.covariances(src), obs, tcov_g)
+        assert it1 == it2, (idx[i], it1, it2)
+        assert np.abs(T1 - T2).max() < 1e-9
+        iters.append(it1)
+    assert max(iters) == 150

@@ -1,0 +1,77 @@
+"""GPU GICP held directly to the independent numpy chain: no shared header anywhere between the
+two sides.  The GPU runs pcore_evaluate_icp (covariance_kernel + gicp_kernel / gicp_wide_kernel on
+pcore_gicp_math.h); the checker renders and unprojects the same candidates with the oracle's raster (a4-a7, not GICP
+arithmetic), computes BOTH covariance sets with numpy (tests/gicp_reference.covariances), runs fast_gicp's published
+LM in numpy / scipy (tests/gicp_reference.gicp) and composes the adjusted pose as concatenate_transforms does
+(renderer.cu:1412-1429, gicp_reference.concat_pose).  Settings are the reference's (renderer.cu:1696-1705: k 10,
+150 iterations, rotation / translation epsilons 2e-3 / 5e-4)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle  # noqa: E402
+from perception_amd.core import PoseCore  # noqa: E402
+from tests import gicp_reference as gref  # noqa: E402
+from tests.helpers import SceneCase  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+C3_NAMES = ("003_cracker_box", "004_sugar_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can")
+
+
+@pytest.fixture(scope="module")
+def c3_case():
+    case = SceneCase(names=C3_NAMES, n_poses=24, seed=7)
+    sc = case.scene
+    core = PoseCore(0)
+    core.upload_meshes(sc.bank.tris, sc.bank.tris_model_count)
+    core.set_camera(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy, sc.proj)
+    dev = torch.device("cuda", 0)
+    mask = torch.from_numpy(sc.mask).to(dev)
+    xyz, lab = core.observed_cloud(torch.from_numpy(sc.depth_raw).to(dev), mask, case.stride, sc.depth_factor)
+    assert np.array_equal(xyz.cpu().numpy(), case.obs_xyz)  # the label-sorted target both sides use
+    core.set_observation(torch.from_numpy(sc.src_depth_cm).to(dev), mask, xyz, lab, 0.01)
+    # the independent chain
+    depth = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses, case.pose_model, case.pose_label,
+                                sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0)
+    seg_cov = {}
+    ref = []
+    for i in range(len(case.poses)):
+        src = oracle.depth_to_cloud(depth[i], case.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0)[0]
+        L = int(case.pose_label[i])
+        tgt = case.obs_xyz[case.label_start[L]:case.label_end[L]]
+        if L not in seg_cov:
+            seg_cov[L] = gref.covariances(tgt)
+        if len(src) == 0 or len(tgt) == 0:
+            ref.append((np.eye(4), 0))
+            continue
+        ref.append(gref.gicp(src, gref.covariances(src), tgt, seg_cov[L]))
+    return case, core, dev, ref
+
+
+@pytest.mark.parametrize("kernel", ["narrow", "wide"])
+def test_gpu_gicp_matches_independent_numpy_chain(c3_case, kernel, monkeypatch):
+    """120 C3 candidates (about half run all 150 iterations): GPU iteration counts equal the numpy chain's, and the
+    GPU's adjusted float mat4x4 (cm-scaled rows) is within 1e-4 of the chain's composed pose per unit of the transform
+    (the north star's GICP tolerance; 1e-2 on the x100 rows)."""
+    case, core, dev, ref = c3_case
+    monkeypatch.setenv("PCORE_GICP_KERNEL", kernel)
+    adj, iters, _, _, _ = core.evaluate_icp(torch.from_numpy(case.poses).to(dev),
+                                            torch.from_numpy(case.pose_model).to(dev),
+                                            torch.from_numpy(case.pose_label).to(dev),
+                                            torch.from_numpy(case.pose_obs_total).to(dev), cost_type=2,
+                                            stride=case.stride)
+    adj = adj.cpu().numpy()
+    iters = iters.cpu().numpy()
+    want_it = np.array([it for _, it in ref])
+    assert np.array_equal(iters, want_it)
+    assert (want_it >= 150).sum() >= 20
+    want = np.stack([gref.concat_pose(T, case.poses[i]) if it > 0 else case.poses[i]
+                     for i, (T, it) in enumerate(ref)])
+    scale = np.where(np.arange(16) < 12, 100.0, 1.0)
+    err = np.abs(adj - want) / scale
+    assert err.max() <= 1e-4, err.max()
+    # the float composition of transforms within 1e-9 of each other is almost always bit-identical
+    same = np.all(adj.view(np.uint32) == want.view(np.uint32), axis=1)
+    assert same.mean() >= 0.9, same.mean()

@@ -1,0 +1,120 @@
+"""GPU: the perch_fat executable end to end (perception_amd/perch_fat.py; perch_fat.cpp:39-330) on a synthetic
+6-DoF YCB-style scene written to disk as the evaluation scripts lay it out -- PLY meshes, a 16-bit depth PNG, a label
+mask PNG, <rendered_root_dir>/<model>/poses.txt, the parameters as YAML -- with GICP on (icp_type 3):
+  - one process: output_poses.txt is byte-identical to ObjectRecognizer.localize_objects_greedy_render + write_outputs
+    run in the test process, and output_stats.txt / output_poses.txt parse with perch.py's own reader
+    (tests/perch_reader.py), the ICP-Time column holding the GICP stage's time;
+  - two ranks (torch.distributed.run, gloo, both on cuda:0 -- the pool's box has one GPU; RCCL refuses two ranks on a
+    device): every rank searches its shard of the states, the keys meet in all_reduce(MIN) and the winners' adjusted
+    poses in all_reduce(SUM) (recognizer.py), and rank 0 writes an output_poses.txt byte-identical to
+    the one-process run."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from perception_amd import io, synthetic as syn  # noqa: E402
+from perception_amd.model import matrix_to_quat_xyzw  # noqa: E402
+from perception_amd.recognizer import (CAM_TO_BODY, CameraIntrinsics, ModelMetaData, ObjectRecognizer,  # noqa: E402
+                                       RecognitionInput)
+from tests.helpers import oracle_render_fn  # noqa: E402
+from tests.perch_reader import read_perch_outputs  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = ["003_cracker_box", "005_tomato_soup_can", "061_foam_brick"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def scene_dir(tmp_path_factory):
+    root = tmp_path_factory.mktemp("perch")
+    rng = np.random.default_rng(5)
+    gts = np.stack([syn.default_gt_pose(rng, c) for c in [(-0.12, 0.0, 0.8), (0.0, 0.05, 0.85), (0.13, -0.03, 0.75)]])
+    sc = syn.make_scene(NAMES, gts, oracle_render_fn, rng=rng)
+    models = root / "models"
+    rendered = root / "rendered"
+    rows = []
+    for k, name in enumerate(NAMES):
+        os.makedirs(models / name, exist_ok=True)
+        io.save_ply(str(models / name / "textured.ply"), sc.bank.models[k])
+        P = syn.candidate_poses(gts[k][:3, 3], 80, rng, include=gts[k], num_viewpoints=20, inplane=4)
+        lst = np.array([np.concatenate([T[:3, 3], matrix_to_quat_xyzw(T[:3, :3])]) for T in P])
+        os.makedirs(rendered / name, exist_ok=True)
+        io.write_poses_txt(str(rendered / name / "poses.txt"), lst, decimals=6)
+        rows.append([name, str(models / name / "textured.ply"), False, False, 0, 0.06, 1])
+    io.save_png(str(root / "depth.png"), sc.depth_raw.astype(np.uint16))
+    io.save_png(str(root / "mask.png"), sc.mask)
+    import yaml
+
+    params = {
+        "perch_params": {"sensor_resolution_radius": 0.01, "min_neighbor_points_for_valid_pose": 30,
+                         "gpu_batch_size": 700, "gpu_stride": 8, "icp_type": 3, "use_color_cost": False,
+                         "use_cylinder_observed": False},
+        "model_bank": rows, "mesh_in_mm": False, "mesh_scaling_factor": 1.0,
+        "required_object": NAMES, "use_external_pose_list": 1, "use_icp": 1, "compute_type": 1,
+        "input_depth_image": str(root / "depth.png"), "predicted_mask_image": str(root / "mask.png"),
+        "input_color_image": "", "depth_factor": float(sc.depth_factor), "rendered_root_dir": str(rendered),
+        "camera_pose": np.linalg.inv(CAM_TO_BODY).reshape(-1).tolist(), "perch_debug_dir": str(root / "debug"),
+        "camera_width": sc.width, "camera_height": sc.height, "camera_fx": float(sc.fx), "camera_fy": float(sc.fy),
+        "camera_cx": float(sc.cx), "camera_cy": float(sc.cy),
+    }
+    with open(root / "params.yaml", "w") as f:
+        yaml.safe_dump(params, f)
+    return root, sc
+
+
+def _run(cmd, env_extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(env_extra or {}))
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    return r
+
+
+def test_perch_fat_one_process_matches_recognizer_and_parses(scene_dir):
+    root, sc = scene_dir
+    _run([sys.executable, "-u", "-m", "perception_amd.perch_fat", "scene_w1.png", "--params",
+          str(root / "params.yaml")])
+    out = root / "debug" / "scene_w1"
+    ann, stats = read_perch_outputs(str(root / "debug"), "scene_w1", {n: i + 1 for i, n in enumerate(NAMES)})
+    assert [a["category_id"] for a in ann] == [1, 2, 3]
+    assert stats["rendered"] == stats["expands"] > 0
+    assert 0.0 < stats["icp_runtime"] < stats["runtime"] + 1.0  # the GICP stage's own time (seconds)
+    for k, a in enumerate(ann):  # every object found near its GT pose
+        assert np.linalg.norm(np.array(a["location"]) / 100.0 - sc.gt_poses[k][:3, 3]) < 0.05
+    # the same search in this process through the Python API
+    from perception_amd import perch_fat as pf
+    ps = pf.ParamServer([str(root / "params.yaml")])
+    bank = {n: ModelMetaData(n, file=str(root / "models" / n / "textured.ply")) for n in NAMES}
+    cam = CameraIntrinsics(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy)
+    rec = ObjectRecognizer(bank, cam, pf.perch_params(ps), 0)
+    inp = RecognitionInput(NAMES, str(root / "depth.png"), str(root / "mask.png"), depth_factor=sc.depth_factor,
+                           rendered_root_dir=str(root / "rendered"), use_icp=1)
+    res = rec.localize_objects_greedy_render(inp)
+    rec.write_outputs(res, str(root / "api"))
+    assert (root / "api" / "output_poses.txt").read_bytes() == (out / "output_poses.txt").read_bytes()
+
+
+def test_perch_fat_two_ranks_output_poses_identical(scene_dir):
+    root, _ = scene_dir
+    if not (root / "debug" / "scene_w1" / "output_poses.txt").exists():
+        _run([sys.executable, "-u", "-m", "perception_amd.perch_fat", "scene_w1", "--params",
+              str(root / "params.yaml")])
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+              "127.0.0.1", "--master-port", str(_free_port()), "-m", "perception_amd.perch_fat", "scene_w2",
+              "--params", str(root / "params.yaml")], {"PCORE_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "1"})
+    one = (root / "debug" / "scene_w1" / "output_poses.txt").read_bytes()
+    two = (root / "debug" / "scene_w2" / "output_poses.txt").read_bytes()
+    assert one and one == two, r.stdout[-2000:]

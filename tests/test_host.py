@@ -120,8 +120,12 @@ def test_batched_pose_building_matches_per_state():
 
     out = chain_matmul_batch(A, T, B)
     for i in range(0, n, 37):
-        assert np.array_equal(out[i], mm(mm(A, T[i]), B[i]))
+        assert np.array_equal(out[i], mm(A, mm(T[i], B[i])))  # search_env.cpp:1567-1571 grouping
     assert np.allclose(out, np.stack([A @ T[i] @ B[i] for i in range(n)]), rtol=0, atol=1e-12)
+    # the quaternion norm in Eigen's packet order (x^2 + z^2) + (y^2 + w^2)
+    x, y, z, w = P[:, 3], P[:, 4], P[:, 5], P[:, 6]
+    nrm = np.sqrt((x * x + z * z) + (y * y + w * w))
+    assert np.array_equal(T[:, 2, 2], 1 - 2 * ((x / nrm) * (x / nrm) + (y / nrm) * (y / nrm)))
     # 3-DoF: the yaw quaternion path
     xyz = rng.uniform(-1, 1, (n, 3))
     yaw = rng.uniform(-7, 7, n)

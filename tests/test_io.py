@@ -129,3 +129,26 @@ def test_read_poses_txt_cached_reparses_a_changed_file(tmp_path):
     os.utime(p, ns=(os.stat(p).st_atime_ns, os.stat(p).st_mtime_ns + 1000))
     b = pio.read_poses_txt_cached(p)
     assert b.shape == (2, 7) and not b.flags.writeable
+
+
+def test_read_poses_txt_cached_same_size_same_mtime_rewrite(tmp_path):
+    """A poses.txt rewritten in place with the same size and the same timestamps is parsed again (the cache is keyed
+    by content); use_cache=False always parses."""
+    from perception_amd import io as pio
+    import os
+    p = str(tmp_path / "poses.txt")
+    rows = np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]])
+    pio.write_poses_txt(p, rows)
+    st = os.stat(p)
+    a = pio.read_poses_txt_cached(p)
+    pio.write_poses_txt(p, rows[:, [1, 0, 2, 3, 4, 5, 6]])  # same length: x and y swapped
+    os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert os.stat(p).st_size == st.st_size and os.stat(p).st_mtime_ns == st.st_mtime_ns
+    b = pio.read_poses_txt_cached(p)
+    assert b[0, 0] == 0.2 and a[0, 0] == 0.1
+    assert pio.read_poses_txt_cached(p, use_cache=False) is not b
+    for i in range(pio._POSES_CACHE_MAX + 5):  # LRU bound
+        q = str(tmp_path / f"p{i}.txt")
+        pio.write_poses_txt(q, rows * (i + 1))
+        pio.read_poses_txt_cached(q)
+    assert len(pio._POSES_CACHE) <= pio._POSES_CACHE_MAX
