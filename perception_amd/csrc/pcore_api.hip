@@ -79,6 +79,7 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_count;
     DevBuf<double> icp_cov;
     DevBuf<int32_t> icp_corr;   // GicpArgs::corr
+    DevBuf<int32_t> icp_corr_hist;  // GicpArgs::corr_hist
     DevBuf<double> icp_mahal;   // GicpArgs::mahal
     DevBuf<int32_t> icp_counter;
     DevBuf<uint32_t> icp_order_keys;  // 2 x chunk keys (in, out)
@@ -311,7 +312,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part); (void)dev_free(c->tri_rgb); (void)dev_free(c->render_tri);
     for (hipEvent_t e : c->icp_ev) (void)hipEventDestroy(e);
@@ -924,7 +925,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     // GICP scratch per pose: nsamp cloud slots (16 B) + covariances (48 B) + the iteration's correspondences (4 B)
     // and Mahalanobis matrices (48 B).  Chunks are as large as the budget below allows and equal in size: every
     // chunk ends with the tail of its slowest pose, so fewer chunks mean fewer tails.
-    const size_t per_pose = (size_t)nsamp * 116;
+    const size_t per_pose = (size_t)nsamp * 116 + (size_t)kCorrHist * std::min(nsamp, kCorrHistCap) * 4;
     // Up to 32 GiB (and at most 40 % of the free HBM): one chunk for 100k poses at 640x480 / stride 8.
     // Each chunk ends with the tail of its slowest pose, so on C3 (50k poses) one chunk instead of two
     // saves ~5 ms of a 37 ms step.
@@ -942,6 +943,11 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, dev_reserve(c->icp_count, (size_t)chunk));
     HIPC(c, dev_reserve(c->icp_cov, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_corr, (size_t)chunk * nsamp));
+    // gicp_kernel's correspondence history: kCorrHist sets per pose of up to hist_cap points (C3's rendered clouds
+    // hold <= 467 of 4,800 samples; larger clouds search every iteration)
+    const int hist_cap = std::min(nsamp, kCorrHistCap);
+    const bool use_hist = !getenv("PCORE_GICP_NO_HIST");  // A/B knob (same results)
+    if (use_hist) HIPC(c, dev_reserve(c->icp_corr_hist, (size_t)chunk * kCorrHist * hist_cap));
     HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 1));
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
@@ -971,6 +977,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.src_cov = c->icp_cov.p;
     g.corr = c->icp_corr.p;
     g.mahal = c->icp_mahal.p;
+    g.corr_hist = use_hist ? c->icp_corr_hist.p : nullptr;
+    g.corr_hist_cap = hist_cap;
     g.src_cap = nsamp;
     g.tgt = c->tgt.p;
     g.tgt_cov = six ? c->tgt_cov_label.p : c->tgt_cov_all.p;

@@ -156,10 +156,8 @@ PCORE_GHD double mahal_err(const double (&M6)[6], const double (&e)[3]) {
     return e[0] * me0 + e[1] * me1 + e[2] * me2;
 }
 
-// One point's contribution for the transformed point q (double), its correspondence tj and both covariances
-// (xx, xy, xz, yy, yz, zz); M6 receives the point's Mahalanobis matrix (kept for the trials' errors).
-PCORE_GHD void contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6], const double (&tj)[3],
-                       const double (&ct)[6], double (&acc)[kTerms], double (&M6)[6]) {
+// M = (C_t + R C_s R^T)^-1 of one point (xx, xy, xz, yy, yz, zz), contrib's first half
+PCORE_GHD void mahal_matrix(const double (&R)[3][3], const double (&cs)[6], const double (&ct)[6], double (&M6)[6]) {
     const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
     const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
     // A = C_t + R C_s R^T row by row (row r of R C_s, then A's row r): only one row of R C_s is live at a time
@@ -195,6 +193,15 @@ PCORE_UNROLL
         for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
     M6[0] = M[0][0]; M6[1] = M[0][1]; M6[2] = M[0][2];
     M6[3] = M[1][1]; M6[4] = M[1][2]; M6[5] = M[2][2];
+}
+
+// One point's contribution for the transformed point q (double), its correspondence tj and both covariances
+// (xx, xy, xz, yy, yz, zz); M6 receives the point's Mahalanobis matrix (kept for the trials' errors).  M is
+// symmetric bit for bit (m[r][c] = m[c][r], both scaled by the same 1 / det), so its 3x3 form is rebuilt from M6.
+PCORE_GHD void contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6], const double (&tj)[3],
+                       const double (&ct)[6], double (&acc)[kTerms], double (&M6)[6]) {
+    mahal_matrix(R, cs, ct, M6);
+    const double M[3][3] = {{M6[0], M6[1], M6[2]}, {M6[1], M6[3], M6[4]}, {M6[2], M6[4], M6[5]}};
     const double e[3] = {tj[0] - q[0], tj[1] - q[1], tj[2] - q[2]};
     // H[a][b] (a <= b) column by column: column b of M J as a 3-vector (b < 3: the skew part; b >= 3: -M's column),
     // then its J^T product for every a <= b into acc[hdiag(a) + b - a].  Each sum takes one term per point, so the
@@ -250,6 +257,9 @@ PCORE_UNROLL
 // column k updated with temp_j = D_j L_kj and divided by the pivot; a zero first pivot leaves L = I; the solve
 // permutes, runs the unit-lower forward substitution, divides by D (|D_i| <= DBL_MIN gives 0), runs the unit-upper
 // back substitution and permutes back.  Sums run in index order.  sys: 28 terms (upper H row-major, b).
+// WAVE: every lane of the wave solves the same system (the pivots move to SGPRs, the independent divisions run
+// lane-parallel); WAVE = false: each lane solves its own system (gicp_batch_kernel's per-slot LM step, the host).
+template <bool WAVE = (PCORE_LANE_PAR != 0)>
 PCORE_GHD void lm_solve(const double* sys, double lambda, double (&d)[6]) {
     double A[6][6];
     {
@@ -273,7 +283,7 @@ PCORE_UNROLL
             const double v = __builtin_fabs(A[i][i]);
             if (v > big) { big = v; p = i; }
         }
-        p = uniform_i(p);  // identical on every lane
+        if constexpr (WAVE) p = uniform_i(p);  // identical on every lane
         tr[k] = p;
 PCORE_UNROLL
         for (int c = k + 1; c < 6; c++)
@@ -303,14 +313,14 @@ PCORE_UNROLL
             }
         }
         const double akk = A[k][k];
-        const bool valid = uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0;
+        const bool valid = WAVE ? uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0 : __builtin_fabs(akk) > 0.0;
         if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
             zero = true;
             break;
         }
         if (valid) {
 #if PCORE_LANE_PAR
-            if (k < 5) {
+            if (WAVE && k < 5) {
                 constexpr int MAXN = 5;
                 double num[MAXN], den[MAXN], q[MAXN];
 PCORE_UNROLL
@@ -321,11 +331,12 @@ PCORE_UNROLL
                 lane_div<MAXN>(num, den, q);
 PCORE_UNROLL
                 for (int i = k + 1; i < 6; i++) A[i][k] = q[i - k - 1];
-            }
-#else
-PCORE_UNROLL
-            for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
+            } else if (!WAVE)
 #endif
+            {
+PCORE_UNROLL
+                for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
+            }
         }
     }
     double x[6];
@@ -347,21 +358,22 @@ PCORE_UNROLL
 PCORE_UNROLL
         for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
 #if PCORE_LANE_PAR
-    {
+    if constexpr (WAVE) {
         double Dd[6], q[6];
 PCORE_UNROLL
         for (int i = 0; i < 6; i++) Dd[i] = A[i][i];
         lane_div<6>(x, Dd, q);
 PCORE_UNROLL
         for (int i = 0; i < 6; i++) x[i] = __builtin_fabs(Dd[i]) > 2.2250738585072014e-308 ? q[i] : 0.0;
-    }
-#else
-PCORE_UNROLL
-    for (int i = 0; i < 6; i++) {
-        const double Di = A[i][i];
-        x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
-    }
+    } else
 #endif
+    {
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) {
+            const double Di = A[i][i];
+            x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
+        }
+    }
 PCORE_UNROLL
     for (int i = 4; i >= 0; i--) {
         double s = A[i + 1][i] * x[i + 1];
@@ -381,36 +393,39 @@ PCORE_UNROLL
 // se3_exp (fast_gicp so3.hpp): so3_exp quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
 // cos(theta/2)), Eigen's Quaternion::toRotationMatrix, translation V rho with
 // V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10)
+// WAVE: as lm_solve's (the sin / cos and quotients lane-parallel when every lane holds the same step)
+template <bool WAVE = (PCORE_LANE_PAR != 0)>
 PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]) {
     const double w0 = a[0], w1 = a[1], w2 = a[2];
     const double theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
     const double theta = __builtin_sqrt(theta_sq);  // so3_exp's and se3_exp's sqrt(omega . omega)
+    double quo[3] = {0.0, 0.0, 0.0}, cos_h = 0.0;
 #if PCORE_LANE_PAR
-    // the four sin / cos on lanes 0..3 and the three quotients on lanes 0..2, one sequence each (same values)
-    const int l = lane_index();
-    const double half_theta = 0.5 * theta;
-    const double tv = dmath::sincos_d(l < 2 ? half_theta : theta, (l & 1) != 0);
-    const double sin_h = read_lane_d<0>(tv), cos_h = read_lane_d<1>(tv);
-    const double sin_t = read_lane_d<2>(tv), cos_t = read_lane_d<3>(tv);
-    const double th2 = theta * theta;
-    const double num[3] = {sin_h, 1.0 - cos_t, theta - sin_t}, den[3] = {theta, th2, th2 * theta};
-    double quo[3];
-    lane_div<3>(num, den, quo);
+    if constexpr (WAVE) {
+        // the four sin / cos on lanes 0..3 and the three quotients on lanes 0..2, one sequence each (same values)
+        const int l = lane_index();
+        const double half_theta = 0.5 * theta;
+        const double tv = dmath::sincos_d(l < 2 ? half_theta : theta, (l & 1) != 0);
+        const double sin_h = read_lane_d<0>(tv);
+        cos_h = read_lane_d<1>(tv);
+        const double sin_t = read_lane_d<2>(tv), cos_t = read_lane_d<3>(tv);
+        const double th2 = theta * theta;
+        const double num[3] = {sin_h, 1.0 - cos_t, theta - sin_t}, den[3] = {theta, th2, th2 * theta};
+        lane_div<3>(num, den, quo);
+    }
 #endif
     double imag, real;
     if (theta_sq < 1e-10) {
         const double theta_quad = theta_sq * theta_sq;
         imag = 0.5 - 1.0 / 48.0 * theta_sq + 1.0 / 3840.0 * theta_quad;
         real = 1.0 - 1.0 / 8.0 * theta_sq + 1.0 / 384.0 * theta_quad;
-    } else {
-#if PCORE_LANE_PAR
+    } else if (WAVE && PCORE_LANE_PAR) {
         imag = quo[0];
         real = cos_h;
-#else
+    } else {
         const double half_theta = 0.5 * theta;
         imag = dmath::sin_d(half_theta) / theta;
         real = dmath::cos_d(half_theta);
-#endif
     }
     const double qw = real, qx = imag * w0, qy = imag * w1, qz = imag * w2;
     const double tx = 2.0 * qx, ty = 2.0 * qy, tz = 2.0 * qz;
@@ -439,14 +454,15 @@ PCORE_UNROLL
         for (int r = 0; r < 3; r++)
 PCORE_UNROLL
             for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
-#if PCORE_LANE_PAR
-        const double c1 = quo[1];
-        const double c2 = quo[2];
-#else
-        const double th2 = theta * theta;
-        const double c1 = (1.0 - dmath::cos_d(theta)) / th2;
-        const double c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
-#endif
+        double c1, c2;
+        if (WAVE && PCORE_LANE_PAR) {
+            c1 = quo[1];
+            c2 = quo[2];
+        } else {
+            const double th2 = theta * theta;
+            c1 = (1.0 - dmath::cos_d(theta)) / th2;
+            c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
+        }
 PCORE_UNROLL
         for (int r = 0; r < 3; r++)
 PCORE_UNROLL

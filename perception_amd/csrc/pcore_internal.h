@@ -169,7 +169,16 @@ struct GicpArgs {
     // -2 t'z [4], |t'|^2 [4]; padding 0, 0, 0, +inf; pcore_gicp_math.h)
     const float* tgt_quads;
     const int32_t* seg_qoff;
+    // correspondence history (gicp_kernel): per pose kCorrHist sets of corr_hist_cap correspondences, the sets of the
+    // last searched iterations, keyed by the float transform T_f each was searched at.  An iteration whose T_f equals
+    // a kept one bit for bit has the same float queries and so the same correspondences: it reuses the set instead
+    // of searching.  Poses with more than corr_hist_cap source points search every iteration (into corr).
+    int32_t* corr_hist;       // nullable: no history
+    int32_t corr_hist_cap;
 };
+
+constexpr int kCorrHist = 16;      // history sets per pose: lanes 4e .. 4e + 3 of three VGPRs hold set e's 12 floats
+constexpr int kCorrHistCap = 512;  // source points per history set (poses with more search every iteration)
 
 // segments above this many points use the exact shell search of their neighbour grid (GICP
 // correspondences and target covariances); smaller ones the brute-force scans

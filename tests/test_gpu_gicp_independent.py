@@ -30,7 +30,7 @@ def c3_case():
     dev = torch.device("cuda", 0)
     mask = torch.from_numpy(sc.mask).to(dev)
     xyz, lab = core.observed_cloud(torch.from_numpy(sc.depth_raw).to(dev), mask, case.stride, sc.depth_factor)
-    assert np.array_equal(xyz.cpu().numpy(), case.obs_xyz)  # the label-sorted target both sides use
+    assert np.array_equal(xyz.cpu().numpy(), case.obs_xyz_raw)  # set_observation label-sorts it: case.obs_xyz
     core.set_observation(torch.from_numpy(sc.src_depth_cm).to(dev), mask, xyz, lab, 0.01)
     # the independent chain
     depth = oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, case.poses, case.pose_model, case.pose_label,
@@ -50,7 +50,7 @@ def c3_case():
     return case, core, dev, ref
 
 
-@pytest.mark.parametrize("kernel", ["narrow", "wide"])
+@pytest.mark.parametrize("kernel", ["narrow", "wide", "batch"])
 def test_gpu_gicp_matches_independent_numpy_chain(c3_case, kernel, monkeypatch):
     """120 C3 candidates (about half run all 150 iterations): GPU iteration counts equal the numpy chain's, and the
     GPU's adjusted float mat4x4 (cm-scaled rows) is within 1e-4 of the chain's composed pose per unit of the transform

@@ -27,7 +27,7 @@ def main():
     lib = _native.load()
     fn = lib.pcore_debug_gicp_profile
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 9)()
     w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
     torch.cuda.synchronize()
     fn(buf, 1)
@@ -42,6 +42,7 @@ def main():
     print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())
     for k in range(8):
         print(f"{names[k]:14s} {buf[k] / max(total, 1):10.0f} clk per pose-iteration")
+    print(f"correspondence history reuse: {buf[8]} of {total} pose-iterations ({buf[8] / max(total, 1):.3f})")
 
 
 if __name__ == "__main__":

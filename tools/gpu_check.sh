@@ -14,4 +14,4 @@ timeout -k 10 400 python bench.py ${BENCH_ARGS} > $OUT/${TAG}_bench.json 2> $OUT
 python -c "import json; d=json.load(open('$OUT/${TAG}_bench.json')); print('C2 %.4gM poses/s kernel %.4f ms; C3 %.4gM gicp %.2f ms' % (d['value']/1e6, d['roofline']['kernel_ms'], d['c3']['value']/1e6, d['c3']['gicp']['gicp_ms_per_step']))"
 PCORE_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --no-cpu --c3-steps 1 > $OUT/${TAG}_bench_gpus2.json 2> $OUT/${TAG}_bench_gpus2.err \
   || { tail -20 $OUT/${TAG}_bench_gpus2.err; exit 1; }
-python -c "import json; d=json.load(open('$OUT/${TAG}_bench_gpus2.json')); print('gpus2 n_gpus', d['n_gpus'], 'value %.4gM' % (d['value']/1e6), d['config'])"
+python -c "import json; d=json.loads([l for l in open('$OUT/${TAG}_bench_gpus2.json') if l.startswith('{')][-1]); print('gpus2 n_gpus', d['n_gpus'], 'value %.4gM' % (d['value']/1e6), d['config'])"
