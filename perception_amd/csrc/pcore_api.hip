@@ -90,8 +90,7 @@ struct pcore_ctx {
     DevBuf<float4> tri_lab;       // Lab per original triangle
     DevBuf<float4> obs_lab;       // Lab per observed point, label-sorted
     DevBuf<int32_t> colour_id;    // N x nsamp scratch of the fused kernel's colour id pass
-    DevBuf<int32_t> ovf_list;     // poses deferred to the fused overflow launch
-    DevBuf<int32_t> ovf_ctr;      // FusedArgs::ovf_ctr
+    DevBuf<int32_t> fb_ctr;       // FusedArgs::fb_ctr
     DevBuf<int32_t> win_hist;     // FusedArgs::win_hist
     int32_t* fb_host = nullptr;   // mapped host memory (FusedArgs::fb_host), host view
     int32_t* fb_dev = nullptr;    // the same, device view
@@ -99,7 +98,6 @@ struct pcore_ctx {
     int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
     long long tile_key = -1;      // ws, hs, bitmap words, colour of the current tile configuration
     int tile_tier = kDefaultTier;
-    double ovf_frac = 1.0;        // fraction of the poses the chosen tier defers (last histogram)
     std::vector<int> obs_order;   // label-sorted position -> caller's observed index
     bool have_obs_colours = false;
     DevBuf<double> metric_part;  // ADD / ADD-S per-block partial sums
@@ -305,7 +303,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->tris); (void)dev_free(c->tri_lo); (void)dev_free(c->tri_hi);
     (void)dev_free(c->sverts); (void)dev_free(c->stris); (void)dev_free(c->streams);
     (void)dev_free(c->model_st_lo); (void)dev_free(c->model_st_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
-    (void)dev_free(c->ovf_list); (void)dev_free(c->ovf_ctr); (void)dev_free(c->win_hist);
+    (void)dev_free(c->fb_ctr); (void)dev_free(c->win_hist);
     if (c->fb_host) (void)hipHostFree(c->fb_host);
     (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
     (void)dev_free(c->grids); (void)dev_free(c->cell_start); (void)dev_free(c->grid_pts);
@@ -658,12 +656,11 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
         std::memset(c->fb_host, 0, 16 * sizeof(int32_t));
         c->fb_host[kTileTiers + 2] = -1;
         if ((e = hipHostGetDevicePointer((void**)&c->fb_dev, c->fb_host, 0)) != hipSuccess) return e;
-        if ((e = dev_reserve(c->ovf_ctr, 2)) != hipSuccess) return e;
+        if ((e = dev_reserve(c->fb_ctr, 2)) != hipSuccess) return e;
         if ((e = dev_reserve(c->win_hist, kTileTiers + 1)) != hipSuccess) return e;
-        if ((e = hipMemset(c->ovf_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
+        if ((e = hipMemset(c->fb_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
         if ((e = hipMemset(c->win_hist.p, 0, (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
     }
-    if ((e = reserve_gen(c, c->ovf_list, (size_t)num_poses)) != hipSuccess) return e;
     int edge[kTileTiers];
     for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, c->dinfo);
     const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);
@@ -671,7 +668,6 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
         c->tile_key = key;
         c->tile_key_seq = c->fb_seq + 1;
         c->tile_tier = kDefaultTier;
-        c->ovf_frac = 1.0;
     } else {
         volatile int32_t* fb = c->fb_host;
         const int32_t seq = fb[kTileTiers + 2];
@@ -687,24 +683,18 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
                     if (edge[t] > 0 && over * 100 <= tot) { tier = t; break; }
                 }
                 c->tile_tier = tier;
-                c->ovf_frac = (double)over / (double)tot;
             }
         }
     }
     if (const char* env = getenv("PCORE_FUSED_TIER")) {  // A/B + test knob; >= kTileTiers: whole image
         c->tile_tier = std::min(std::max(atoi(env), 0), kTileTiers);
-        c->ovf_frac = 1.0;
     }
-    // overflow launch: twice the predicted deferred poses + 16 workgroups (any count is still covered by the
-    // grid-stride loop); the whole 1024 until a histogram is known
-    a.ovf_grid = (int)std::min<double>(kOvfGrid, 2.0 * c->ovf_frac * num_poses + 16.0);
     // tier kTileTiers (A/B knob only): the whole image
     a.tcap = c->tile_tier < kTileTiers && edge[c->tile_tier] > 0 ? edge[c->tile_tier] : nsamp;
     if (const char* env = getenv("PCORE_FUSED_TCAP"))  // test knob: a tile of this many samples (most poses overflow)
         a.tcap = std::min(std::max(atoi(env), 1), nsamp);
     for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
-    a.ovf_list = c->ovf_list.p;
-    a.ovf_ctr = c->ovf_ctr.p;
+    a.fb_ctr = c->fb_ctr.p;
     a.win_hist = c->win_hist.p;
     a.fb_host = c->fb_dev;
     a.fb_seq = ++c->fb_seq;

@@ -108,20 +108,17 @@ struct FusedArgs {
     const float4* obs_lab;      // Lab of every observed point, label-sorted order
     int32_t* cid;               // N x nsamp scratch: original triangle of each sample's nearest fragment
     float colour_thr;           // color_distance_threshold
-    // sample windows ("Pose windows"): the z-sample tile in LDS holds `tcap` samples; a pose
-    // whose window is larger is appended to ovf_list and scored by the overflow launch (tile = ws * hs).
-    // ovf_ctr[0] counts the list, ovf_ctr[1] the finished overflow workgroups; the overflow launch returns
-    // both to 0
+    // sample windows ("Pose windows"): the z-sample tile in LDS holds `tcap` samples; a pose whose window
+    // is larger is processed in chunks of the tile.  fb_ctr[0] counts those poses, fb_ctr[1] the finished
+    // workgroups; the last workgroup publishes and returns both to 0
     int32_t tcap;
-    int32_t* ovf_list;
-    int32_t* ovf_ctr;
+    int32_t* fb_ctr;
     // window-size histogram (bin b: windows of at most hist_edge[b] samples, the last bin the rest),
-    // published by the overflow launch to fb_host (mapped host memory) and reset there
+    // published by the launch's last workgroup to fb_host (mapped host memory) and reset there
     int32_t hist_edge[kTileTiers];
     int32_t* win_hist;  // kTileTiers + 1 bins
-    int32_t* fb_host;   // kTileTiers + 1 bins + 1 overflow count + 1 sequence number
+    int32_t* fb_host;   // kTileTiers + 1 bins + 1 chunked-pose count + 1 sequence number
     int32_t fb_seq;
-    int32_t ovf_grid;   // workgroups of the overflow launch (from the predicted overflow count)
     // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
     // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
     int32_t dbg_skip;
@@ -234,7 +231,6 @@ size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour = false);
 // tile capacity (samples) of tier t: the largest tile that leaves room for tier_wgs(t) workgroups per CU
 // (capped at the whole sampled image)
 int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, const DeviceInfo& d);
-constexpr int kOvfGrid = 1024;  // most workgroups of the overflow launch (grid-stride over the list)
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
                               const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
                               const float* proj, int32_t* depth, hipStream_t s);

@@ -796,16 +796,20 @@ __device__ __forceinline__ int64_t select_key(float rc, float oc, int m, int num
     return (int64_t)((hi << 31) | ((uint64_t)gidx & 0x7fffffffull));
 }
 
+// The window is processed in chunks of at most `cap` samples (the LDS tile): one chunk -- the window -- for every
+// pose the tile holds; otherwise row bands of whole window rows (blocks of columns when one row exceeds the tile),
+// each rasterised over the full stream walk with triangle windows clipped to the chunk.  The costs are functions of
+// the chunks' integer counts and of the explained bitmap, which accumulate across chunks, so they do not depend on
+// the chunking (the overflow launch that scored such poses before round 4 took a whole-image tile instead).
 template <int STRIDE, bool COLOUR>
-__device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw) {
+__device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& pw,
+                                           int cap) {
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int ws = a.ws, nsamp = a.ws * a.hs;
-    const int tn = sw.nx * sw.ny;  // samples of the window (tile)
 
-    for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
     for (int i = tid; i < a.bitmap_words; i += kThreads) sm.bitmap[i] = 0u;
     if (tid < 4) sm.counters[tid] = 0;
     if (a.dbg_zs)  // debug z-samples: the samples outside the window stay 0
@@ -814,14 +818,19 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
     FProf fp;
+    // counts accumulated over the chunks (wave-uniform)
+    int wave_bad = 0, wave_pts = 0;
+    int32_t* cid = nullptr;
+    if constexpr (COLOUR) cid = a.cid + (size_t)pose * nsamp;
+    auto chunk = [&](const SampleWin& sw) __attribute__((always_inline)) {
+    const int tn = sw.nx * sw.ny;  // samples of the chunk (tile)
+    for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
     raster_phase<STRIDE>(a, sm, pose, sw, nullptr, fp);
     fp.mark(2);
     __syncthreads();
     fp.mark(4);
-    int32_t* cid = nullptr;
     if constexpr (COLOUR) {
         // colour id pass (cost_type 1): which triangle left each sample's minimum depth (tile-local index)
-        cid = a.cid + (size_t)pose * nsamp;
         for (int i = tid; i < tn; i += kThreads) cid[i] = INT_MAX;
         __syncthreads();
         raster_phase<STRIDE, true>(a, sm, pose, sw, cid, fp);
@@ -922,7 +931,6 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
         wave_sync();
     };
 
-    int wave_pts = 0;  // wave-uniform
     // tile index k -> (ix, iy) without an integer division: (k + 0.5) / nx in float is within 1e-3 of the
     // quotient (k < 2^14), so one correction step gives the exact row
     const float inv_nx = tn > 0 ? 1.0f / (float)sw.nx : 0.0f;
@@ -960,9 +968,20 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
     }
     if (qcount > 0) process_points(qcount);
     fp.mark(5);
+    for (int off = 32; off > 0; off >>= 1) my_bad += __shfl_xor(my_bad, off);
+    wave_bad += __builtin_amdgcn_readfirstlane(my_bad);
+    };
+    if (pw.nx * pw.ny <= cap) {
+        chunk(pw);  // the window fits the tile (the common case: its own copy of the code, no loop state)
+    } else {
+        const int cw = min(pw.nx, cap), ch = max(1, cap / max(cw, 1));  // chunk columns / rows
+        for (int r0 = 0; r0 < pw.ny; r0 += ch)
+            for (int c0 = 0; c0 < pw.nx; c0 += cw) {
+                if (r0 > 0 || c0 > 0) __syncthreads();  // the previous chunk's points are processed
+                chunk(SampleWin{pw.x0 + c0, pw.y0 + r0, min(cw, pw.nx - c0), min(ch, pw.ny - r0), pw.fastdiv});
+            }
+    }
     // per-wave totals
-    int wave_bad = my_bad;
-    for (int off = 32; off > 0; off >>= 1) wave_bad += __shfl_xor(wave_bad, off);
     __syncthreads();  // all points counted / marked
     if (lane == 0) atomicAdd(&sm.counters[0], wave_bad);
     // number of points = number of valid samples (counted per wave above)
@@ -1012,8 +1031,8 @@ __device__ __forceinline__ void load_pose_rows(const float* poses, int pose, flo
     for (int i = 0; i < 12; i++) m[i] = P[i];
 }
 
-// Window launch: one workgroup per pose, LDS tile of a.tcap samples.  A pose whose window exceeds the tile
-// goes to the overflow list (its outputs are written by fused_cost_ovf_kernel, launched next).
+// Window launch: one workgroup per pose, LDS tile of a.tcap samples.  A pose whose window exceeds the tile is
+// processed in chunks of the tile (fused_pose).
 #ifdef PCORE_WG_TIMING
 // measurement build only (tools/wg_timeline.py): wall clock (100 MHz) at the start and end of every
 // fused_cost_kernel workgroup, indexed by pose
@@ -1072,49 +1091,21 @@ fused_cost_kernel(FusedArgs a) {
 #pragma unroll
         for (int t = 0; t < kTileTiers; t++) b += tn > a.hist_edge[t] ? 1 : 0;
         atomicAdd(&a.win_hist[b], 1);
-        if (tn > a.tcap) {
-            const int at = atomicAdd(&a.ovf_ctr[0], 1);
-            if (at < a.num_poses) a.ovf_list[at] = pose;
-        }
+        if (tn > a.tcap) atomicAdd(&a.fb_ctr[0], 1);
     }
-    if (tn > a.tcap) return;
-    fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
-}
-
-// Overflow launch: the poses fused_cost_kernel deferred, grid-stride over the list, LDS tile of the whole
-// sampled image.  Workgroup 0 also publishes the window histogram to the host and resets it; the last
-// workgroup to finish returns the list counter to 0 (every workgroup has read it by then), so consecutive
-// launches -- and replays of a captured graph -- start from an empty list.
-template <int STRIDE, bool COLOUR = false>
-__global__ void __launch_bounds__(kThreads) fused_cost_ovf_kernel(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const FusedSmem sm = carve_smem(smem_raw, a.ws * a.hs, a.bitmap_words, COLOUR);
-    const int n = min(__builtin_amdgcn_readfirstlane(a.ovf_ctr[0]), a.num_poses);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        for (int b = 0; b <= kTileTiers; b++) {
-            a.fb_host[b] = a.win_hist[b];
-            a.win_hist[b] = 0;
-        }
-        a.fb_host[kTileTiers + 1] = n;
-        // no system fence: the host may read a torn set, which only steers the next tile choice
-        a.fb_host[kTileTiers + 2] = a.fb_seq;
-    }
-    for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int pose = __builtin_amdgcn_readfirstlane(a.ovf_list[i]);
-        if (pose < 0 || pose >= a.num_poses) continue;
-        const int model = a.pose_model[pose];
-        float m[12];
-        load_pose_rows(a.poses, pose, m);
-        const SampleWin sw = (model >= 0 && model < a.num_models) ? pose_window(a, model, m, STRIDE > 0 ? STRIDE : a.stride)
-                                                                  : SampleWin{0, 0, 0, 0, 0};
-        fused_pose<STRIDE, COLOUR>(a, sm, pose, sw);
-        __syncthreads();  // the next pose re-initialises the LDS
-    }
+    fused_pose<STRIDE, COLOUR>(a, sm, pose, sw, a.tcap);
+    // The last workgroup to finish publishes the window histogram and the chunked-pose count to the host (mapped
+    // memory, read by the next call's tile choice) and returns the counters to zero, so consecutive launches -- and
+    // replays of a captured graph -- start from zero.  Every workgroup's counter updates precede its fenced
+    // arrival, so the last one to arrive sees them all.
     if (threadIdx.x == 0) {
         __threadfence();
-        if (atomicAdd(&a.ovf_ctr[1], 1) == (int)gridDim.x - 1) {
-            a.ovf_ctr[0] = 0;
-            a.ovf_ctr[1] = 0;
+        if (atomicAdd(&a.fb_ctr[1], 1) == (int)gridDim.x - 1) {
+            for (int b = 0; b <= kTileTiers; b++) a.fb_host[b] = atomicExch(&a.win_hist[b], 0);
+            a.fb_host[kTileTiers + 1] = atomicExch(&a.fb_ctr[0], 0);
+            // no system fence: the host may read a torn set, which only steers the next tile choice
+            a.fb_host[kTileTiers + 2] = a.fb_seq;
+            atomicExch(&a.fb_ctr[1], 0);
         }
     }
 }
@@ -1220,17 +1211,6 @@ hipError_t launch_fused_cost(const FusedArgs& a0, hipStream_t s) {
         hipLaunchKernelGGL(fused_cost_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
     else
         hipLaunchKernelGGL(fused_cost_kernel<0>, dim3(a.num_poses), dim3(kThreads), lds, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    // one workgroup (the feedback) when no pose can overflow a whole-image tile
-    const size_t lds_full = fused_lds_bytes(nsamp, a.bitmap_words, colour);
-    const dim3 grid(a.tcap == nsamp ? 1 : std::max(1, std::min({a.num_poses, kOvfGrid, a.ovf_grid})));
-    if (colour)
-        hipLaunchKernelGGL((fused_cost_ovf_kernel<0, true>), grid, dim3(kThreads), lds_full, s, a);
-    else if (a.stride == 8)
-        hipLaunchKernelGGL(fused_cost_ovf_kernel<8>, grid, dim3(kThreads), lds_full, s, a);
-    else
-        hipLaunchKernelGGL(fused_cost_ovf_kernel<0>, grid, dim3(kThreads), lds_full, s, a);
     return hipGetLastError();
 }
 

@@ -152,8 +152,8 @@ def test_c4_21_models_selection_bit_exact_vs_oracle():
 
 @pytest.mark.parametrize("tier", ["auto", "tcap64"])
 def test_evaluate_select_keys_equal_evaluate_then_select(tier, monkeypatch):
-    """pcore_evaluate_select folds every pose's key in the launch that scores it (the window launch or, with a
-    64-sample tile, the overflow launch): the keys and costs equal pcore_evaluate + pcore_select's, 21 models."""
+    """pcore_evaluate_select folds every pose's key in the launch that scores it (with a 64-sample tile nearly every
+    pose is scored in chunks of the tile): the keys and costs equal pcore_evaluate + pcore_select's, 21 models."""
     if tier == "tcap64":
         monkeypatch.setenv("PCORE_FUSED_TCAP", "64")
     w = workloads.build(names=list(syn.YCB_PROXIES), poses_per_model=120)
@@ -174,12 +174,12 @@ def test_evaluate_select_keys_equal_evaluate_then_select(tier, monkeypatch):
 def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, monkeypatch):
     """3,000 random poses of three models (random rotations; behind, across and near the camera plane, off
     screen, far): every pose's costs bit-exact against the oracle with the tile tier chosen from the window
-    histogram, forced to the smallest tier, to a 64-sample tile (nearly every pose overflows to the
-    whole-image launch) and to the whole image -- the conservative pose windows never drop a fragment; at 640x480 and at C5's 1280x720.
+    histogram, forced to the smallest tier, to a 64-sample tile (nearly every pose is scored in chunks of the
+    tile, each a full raster clipped to the chunk) and to the whole image -- the conservative pose windows never drop a fragment; at 640x480 and at C5's 1280x720.
     For 200 of them the sampled z-buffers equal the full-frame render."""
     from perception_amd.model import init_from_eigen_batch
     if tier == "tcap64":
-        monkeypatch.setenv("PCORE_FUSED_TCAP", "64")  # nearly every pose takes the overflow launch
+        monkeypatch.setenv("PCORE_FUSED_TCAP", "64")  # nearly every pose is scored in chunks of the tile
     elif tier != "auto":
         monkeypatch.setenv("PCORE_FUSED_TIER", tier)
     w = workloads.build(names=["003_cracker_box", "005_tomato_soup_can", "024_bowl"], poses_per_model=10,

@@ -66,8 +66,8 @@ def test_tabletop_localization_matches_oracle(cylinder):
 @pytest.mark.parametrize("tile", ["auto", "tcap64"])
 def test_tabletop_colour_cost_matches_oracle(tile, monkeypatch):
     """cost_type 1: the colour id pass (nearest fragment's triangle) and the CIEDE2000 gate, bit-exact -- with
-    the chosen LDS tile and with a 64-sample tile that sends nearly every pose through the overflow launch
-    (the colour ids are indexed within the pose's tile)."""
+    the chosen LDS tile and with a 64-sample tile that scores nearly every pose in chunks of the tile (the colour
+    ids are indexed within the chunk)."""
     if tile == "tcap64":
         monkeypatch.setenv("PCORE_FUSED_TCAP", "64")
     names, placements, sc = _scene(colors=[(200, 40, 30), (30, 60, 190)])
