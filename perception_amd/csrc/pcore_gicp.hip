@@ -1200,6 +1200,174 @@ __device__ __forceinline__ bool batch_lm_step(const GicpArgs& g, BatchSlot<HE>& 
     return done;
 }
 
+// Split variant (PCORE_GICP_BATCH_SPLIT): the trial error is a pass of its own instead of riding on the next
+// linearisation -- a slot alternates a linearisation pass (at x, after an accepted trial) and trial-error passes (at
+// x_i with x's correspondences and M, which no pass overwrites before the trial is decided), so no restore is needed.
+#ifndef PCORE_GICP_BATCH_SPLIT
+#define PCORE_GICP_BATCH_SPLIT 0
+#endif
+enum : int { kSlotLin = 4, kSlotErr = 5 };
+
+template <int HE>
+__device__ __forceinline__ void batch_pass_split(const GicpArgs& g, BatchSlot<HE>& S, double* sRed, int lane) {
+    const int pose = __builtin_amdgcn_readfirstlane(S.pose);
+    const int phase = __builtin_amdgcn_readfirstlane(S.phase);
+    const GicpPose P = gicp_pose(g, pose);
+    const bool hist = g.corr_hist != nullptr && P.ns <= g.corr_hist_cap;
+    int32_t* const hbase = hist ? g.corr_hist + (size_t)pose * kCorrHist * g.corr_hist_cap : nullptr;
+    if (phase == kSlotErr) {
+        // the trial error at x_i with the current iteration's correspondences and M (lm_iteration's error loop)
+        Xform xi;
+        xform_load(S.xi, xi);
+        const int32_t* cur = hist ? hbase + (size_t)__builtin_amdgcn_readfirstlane(S.eset) * g.corr_hist_cap : P.corr;
+        double ea = 0.0;
+        for (int i0 = 0; i0 < P.ns; i0 += 64) {
+            const int i = i0 + lane;
+            const int j = i < P.ns ? cur[i] : -1;
+            if (j >= 0) {
+                const float4 sp = P.src[i], tj = P.tgt[j];
+                const double2* m2 = reinterpret_cast<const double2*>(P.mah + (size_t)6 * i);
+                const double2 a = m2[0], b = m2[1], c = m2[2];
+                const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+                double e[3];
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
+                    e[r] = (double)(r == 0 ? tj.x : r == 1 ? tj.y : tj.z) - q;
+                }
+                ea += gicpm::mahal_err(M6, e);
+            }
+        }
+        const double yt = wave_sum_lane0(ea);
+        if (lane == 0) S.ytrial = yt;
+        wave_lds_sync();
+        return;
+    }
+    // linearisation at x (kSlotFirst / kSlotLin)
+    LabelGrid G{};
+    if (P.use_grid) G = g.grids[P.seg];
+    Xform x;
+    xform_load(S.x, x);
+    float Rf[3][3], tf[3];
+    xform_float(x, Rf, tf);
+    int32_t* lin = P.corr;
+    bool reuse = false;
+    if (hist) {
+        const int e = hist_lookup(S, Rf, tf, lane, reuse);
+        lin = hbase + (size_t)e * g.corr_hist_cap;
+        if (lane == 0) S.elast = e;
+    }
+    double acc[gicpm::kTerms];
+#pragma unroll
+    for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
+    for (int i0 = 0; i0 < P.ns; i0 += 64) {
+        const int i = i0 + lane;
+        const bool act = i < P.ns;
+        const float4 sp = act ? P.src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        int j = -1;
+        if (reuse) {
+            j = act ? lin[i] : -1;
+        } else {
+            float qf[3], best = INFINITY;
+            gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
+            if (P.use_grid) {
+                if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
+            } else {
+                scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, j);
+            }
+            if (act) lin[i] = j;
+        }
+        if (act && j >= 0) {
+            const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
+            double q[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) q[r] = x.R[r][0] * s0 + x.R[r][1] * s1 + x.R[r][2] * s2 + x.t[r];
+            double cs[6], ct[6], M6[6];
+            load_cov(P.scov, i, cs);
+            load_cov(P.tcov, j, ct);
+            const float4 tj = P.tgt[j];
+            const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
+            gicpm::contrib(x.R, q, cs, t3, ct, acc, M6);
+            double2* m2 = reinterpret_cast<double2*>(P.mah + (size_t)6 * i);
+            m2[0] = make_double2(M6[0], M6[1]);
+            m2[1] = make_double2(M6[2], M6[3]);
+            m2[2] = make_double2(M6[4], M6[5]);
+        }
+    }
+    const double* sys = lds_tree_sum(acc, sRed, lane);
+    if (lane < gicpm::kTerms) S.spec[lane] = sys[lane];
+    wave_lds_sync();
+}
+
+template <int HE>
+__device__ __forceinline__ bool batch_lm_step_split(const GicpArgs& g, BatchSlot<HE>& S) {
+    int phase = S.phase;
+    double lambda = S.lambda;
+    bool done = false, solve = false;
+    if (phase == kSlotFirst || phase == kSlotLin) {  // a new iteration's system at x
+#pragma unroll
+        for (int v = 0; v < gicpm::kTerms; v++) S.sys[v] = S.spec[v];
+        S.eset = S.elast;
+        if (lambda < 0.0) lambda = gicpm::lm_init_lambda(S.sys);
+        S.nu = 2.0;
+        S.trials = 0;
+        solve = true;
+    } else {  // kSlotErr: decide the trial
+        double d[6];
+#pragma unroll
+        for (int a = 0; a < 6; a++) d[a] = S.d[a];
+        const double rho = gicpm::lm_rho(S.sys, lambda, d, S.sys[gicpm::kErr], S.ytrial);
+        if (rho < 0.0) {
+            if (S.conv) {
+                done = true;
+            } else {
+                lambda = S.nu * lambda;
+                S.nu = 2.0 * S.nu;
+                S.trials = S.trials + 1;
+                if (S.trials == gicpm::kLmMaxTrials) done = true;
+                else solve = true;
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < 12; v++) S.x[v] = S.xi[v];
+            lambda = gicpm::lm_accept_lambda(lambda, rho);
+            if (S.conv || S.iters >= g.max_iter) {
+                done = true;
+            } else {
+                S.iters = S.iters + 1;
+                phase = kSlotLin;
+            }
+        }
+    }
+    Xform x;
+    xform_get(S.x, x);
+    if (solve) {
+        double d[6];
+        gicpm::lm_solve<false>(S.sys, lambda, d);
+        if (!gicpm::all_finite6(d)) {
+            done = true;
+        } else {
+            double Rd[3][3], td[3];
+            gicpm::se3_exp<false>(d, Rd, td);
+            Xform xi;
+            gicpm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
+            xform_put(S.xi, xi);
+#pragma unroll
+            for (int a = 0; a < 6; a++) S.d[a] = d[a];
+            S.conv = gicpm::is_converged(Rd, td, g.rot_eps, g.trans_eps) ? 1 : 0;
+            phase = kSlotErr;
+        }
+    }
+    S.lambda = lambda;
+    S.phase = phase;
+    if (done) {
+        write_pose(g, g.pose_base + S.pose, x, S.iters);
+        S.phase = kSlotEmpty;
+    }
+    return done;
+}
+
 // lane p < B: pull poses into an empty slot p until one needs iterating (poses without source points, target points
 // or iterations are written at once) or the queue is empty
 template <int HE>
@@ -1256,10 +1424,20 @@ gicp_batch_kernel(GicpArgs g, int num_poses) {
         GPROF_T(t0);
 #pragma unroll 1
         for (int p = 0; p < B; p++)
-            if ((live >> p) & 1ull) batch_pass(g, sSlot[p], sRed, lane GPROF_ARG);
+            if ((live >> p) & 1ull) {
+#if PCORE_GICP_BATCH_SPLIT
+                batch_pass_split(g, sSlot[p], sRed, lane);
+#else
+                batch_pass(g, sSlot[p], sRed, lane GPROF_ARG);
+#endif
+            }
         GPROF_TD(t1, sRed[0]);
         if (lane < B && ((live >> lane) & 1ull)) {
+#if PCORE_GICP_BATCH_SPLIT
+            if (batch_lm_step_split(g, sSlot[lane])) batch_refill(g, sSlot[lane], num_poses);
+#else
             if (batch_lm_step(g, sSlot[lane])) batch_refill(g, sSlot[lane], num_poses);
+#endif
         }
         wave_lds_sync();
         GPROF_TD(t2, sSlot[0].phase);
@@ -1276,6 +1454,7 @@ gicp_batch_kernel(GicpArgs g, int num_poses) {
 #ifndef PCORE_GICP_SLOTS
 #define PCORE_GICP_SLOTS 3
 #endif
+
 #ifndef PCORE_GICP_SLOT_HIST
 #define PCORE_GICP_SLOT_HIST 16
 #endif
