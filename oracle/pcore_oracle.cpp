@@ -892,6 +892,12 @@ void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d) {
     pcore::gicpm::lm_solve(sys, lambda, d);
     for (int a = 0; a < 6; a++) out_d[a] = d[a];
 }
+// Eigen's in-place LDLT with its row / column swaps (the restatement lm_solve is held to)
+void orc_gicp_lm_solve_swaps(const double* sys, double lambda, double* out_d) {
+    double d[6];
+    pcore::gicpm::lm_solve_swaps(sys, lambda, d);
+    for (int a = 0; a < 6; a++) out_d[a] = d[a];
+}
 
 double orc_sin_d(double x) { return pcore::dmath::sin_d(x); }
 double orc_cos_d(double x) { return pcore::dmath::cos_d(x); }

@@ -135,6 +135,7 @@ void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, con
  * system; the double sin / cos of pcore_dmath.h; the spec's correspondences of n float queries. */
 void orc_gicp_se3_exp(const double* a6, double* out_T);
 void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d);
+void orc_gicp_lm_solve_swaps(const double* sys, double lambda, double* out_d);
 double orc_sin_d(double x);
 double orc_cos_d(double x);
 double orc_cube_rn(double u);   // step_lm's std::pow(u, 3), rounded once

@@ -938,8 +938,30 @@ struct BatchSlot {
     int conv;               // the pending trial's delta is converged
     int ring;               // next history entry to replace
     int eset, elast;        // history set of x's linearisation / of the last pass's
+    int ns, nt, seg, lo, qoff;  // the pose's source points, target segment (index, first target, first key quad)
     unsigned hist[HE][12];  // float transform bits of the history entries
 };
+
+// gicp_pose's fields from the slot's cached pose data (filled at refill: no dependent global loads per pass)
+template <int HE>
+__device__ __forceinline__ GicpPose slot_pose(const GicpArgs& g, const BatchSlot<HE>& S) {
+    GicpPose p;
+    p.pose = __builtin_amdgcn_readfirstlane(S.pose);
+    p.gp = g.pose_base + p.pose;
+    p.ns = __builtin_amdgcn_readfirstlane(S.ns);
+    p.nt = __builtin_amdgcn_readfirstlane(S.nt);
+    p.seg = __builtin_amdgcn_readfirstlane(S.seg);
+    const int lo = __builtin_amdgcn_readfirstlane(S.lo), qoff = __builtin_amdgcn_readfirstlane(S.qoff);
+    p.src = g.src + (size_t)p.pose * g.src_cap;
+    p.scov = g.src_cov + (size_t)6 * p.pose * g.src_cap;
+    p.corr = g.corr + (size_t)p.pose * g.src_cap;
+    p.mah = g.mahal + (size_t)6 * p.pose * g.src_cap;
+    p.tcov = g.tgt_cov + (size_t)6 * lo;
+    p.tgt = g.tgt + lo;
+    p.tquads = g.tgt_quads + (size_t)16 * qoff;
+    p.use_grid = p.nt > kGridNNMin && g.grids != nullptr && p.seg >= 0;
+    return p;
+}
 
 __device__ __forceinline__ void xform_load(const double* v, Xform& x) {
 #pragma unroll
@@ -1210,9 +1232,9 @@ enum : int { kSlotLin = 4, kSlotErr = 5 };
 
 template <int HE>
 __device__ __forceinline__ void batch_pass_split(const GicpArgs& g, BatchSlot<HE>& S, double* sRed, int lane) {
-    const int pose = __builtin_amdgcn_readfirstlane(S.pose);
     const int phase = __builtin_amdgcn_readfirstlane(S.phase);
-    const GicpPose P = gicp_pose(g, pose);
+    const GicpPose P = slot_pose(g, S);
+    const int pose = P.pose;
     const bool hist = g.corr_hist != nullptr && P.ns <= g.corr_hist_cap;
     int32_t* const hbase = hist ? g.corr_hist + (size_t)pose * kCorrHist * g.corr_hist_cap : nullptr;
     if (phase == kSlotErr) {
@@ -1394,6 +1416,11 @@ __device__ __forceinline__ void batch_refill(const GicpArgs& g, BatchSlot<HE>& S
             continue;
         }
         S.pose = pose;
+        S.ns = ns;
+        S.nt = nt;
+        S.seg = seg;
+        S.lo = seg >= 0 ? g.seg_lo[seg] : 0;
+        S.qoff = seg >= 0 ? g.seg_qoff[seg] : 0;
         xform_put(S.x, x);
         S.lambda = -1.0;
         S.iters = 1;

@@ -260,7 +260,7 @@ PCORE_UNROLL
 // WAVE: every lane of the wave solves the same system (the pivots move to SGPRs, the independent divisions run
 // lane-parallel); WAVE = false: each lane solves its own system (gicp_batch_kernel's per-slot LM step, the host).
 template <bool WAVE = (PCORE_LANE_PAR != 0)>
-PCORE_GHD void lm_solve(const double* sys, double lambda, double (&d)[6]) {
+PCORE_GHD void lm_solve_swaps(const double* sys, double lambda, double (&d)[6]) {
     double A[6][6];
     {
         int h = 0;
@@ -388,6 +388,144 @@ PCORE_UNROLL
             if (tr[k] == c) { const double v = x[k]; x[k] = x[c]; x[c] = v; }
 PCORE_UNROLL
     for (int i = 0; i < 6; i++) d[i] = x[i];
+}
+
+// The same solve, bit for bit, with the pivot order found first (the one the kernels run).  Eigen's LDLT is left-
+// looking: when step k searches the diagonal of the unfactored corner for its pivot, those entries are still the
+// original ones (each is updated only at its own step), and every earlier swap only moves values.  So the whole pivot
+// sequence is a selection on |diag(H + lambda I)| -- at step k the first maximum of positions k..5, then the swap --
+// and the factorisation is that of P (H + lambda I) P^T without pivoting: entry (i, j) of the swapped lower triangle
+// is the symmetric matrix's (perm[i], perm[j]), and row perm[i]'s L entries are computed from the same values in the
+// same order wherever the row sat meanwhile.  That replaces the swaps of 21 stored entries per step by a gather of the
+// permuted matrix (one read of sys per entry: from LDS in the kernels) and permutes the right-hand side and the
+// result instead.  tests/test_gicp_spec.py holds this to lm_solve_swaps on random, tied, zero and non-finite systems.
+PCORE_GHD constexpr int hidx(int a, int b) { return a <= b ? hdiag(a) + (b - a) : hdiag(b) + (a - b); }
+
+template <bool WAVE = (PCORE_LANE_PAR != 0)>
+PCORE_GHD void lm_solve(const double* sys, double lambda, double (&d)[6]) {
+    int perm[6];
+    {
+        double mag[6];
+PCORE_UNROLL
+        for (int a = 0; a < 6; a++) {
+            mag[a] = __builtin_fabs(sys[hdiag(a)] + lambda);
+            perm[a] = a;
+        }
+PCORE_UNROLL
+        for (int k = 0; k < 5; k++) {
+            int p = k;
+            double big = mag[k];
+PCORE_UNROLL
+            for (int i = k + 1; i < 6; i++) {
+                const double v = mag[i];
+                if (v > big) { big = v; p = i; }
+            }
+            if constexpr (WAVE) p = uniform_i(p);  // identical on every lane
+PCORE_UNROLL
+            for (int c = k + 1; c < 6; c++)
+                if (p == c) {
+                    const double m = mag[k]; mag[k] = mag[c]; mag[c] = m;
+                    const int q = perm[k]; perm[k] = perm[c]; perm[c] = q;
+                }
+        }
+    }
+    // the permuted lower triangle of H + lambda I
+    double A[6][6];
+PCORE_UNROLL
+    for (int i = 0; i < 6; i++)
+PCORE_UNROLL
+        for (int j = 0; j <= i; j++) A[i][j] = i == j ? sys[hdiag(perm[i])] + lambda : sys[hidx(perm[i], perm[j])];
+    bool zero = false;
+PCORE_UNROLL
+    for (int k = 0; k < 6; k++) {
+        if (k > 0) {
+            double temp[6];
+PCORE_UNROLL
+            for (int j = 0; j < k; j++) temp[j] = A[j][j] * A[k][j];
+            double s = A[k][0] * temp[0];
+PCORE_UNROLL
+            for (int j = 1; j < k; j++) s = s + A[k][j] * temp[j];
+            A[k][k] = A[k][k] - s;
+PCORE_UNROLL
+            for (int i = k + 1; i < 6; i++) {
+                double w = A[i][0] * temp[0];
+PCORE_UNROLL
+                for (int j = 1; j < k; j++) w = w + A[i][j] * temp[j];
+                A[i][k] = A[i][k] - w;
+            }
+        }
+        const double akk = A[k][k];
+        const bool valid = WAVE ? uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0 : __builtin_fabs(akk) > 0.0;
+        if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
+            zero = true;
+            break;
+        }
+        if (valid) {
+#if PCORE_LANE_PAR
+            if (WAVE && k < 5) {
+                constexpr int MAXN = 5;
+                double num[MAXN], den[MAXN], q[MAXN];
+PCORE_UNROLL
+                for (int i = 0; i < MAXN; i++) {
+                    num[i] = k + 1 + i < 6 ? A[k + 1 + i < 6 ? k + 1 + i : 5][k] : 0.0;
+                    den[i] = akk;
+                }
+                lane_div<MAXN>(num, den, q);
+PCORE_UNROLL
+                for (int i = k + 1; i < 6; i++) A[i][k] = q[i - k - 1];
+            } else if (!WAVE)
+#endif
+            {
+PCORE_UNROLL
+                for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
+            }
+        }
+    }
+    if (zero) {
+        // D = the (zero) diagonal: every row is set to zero by the pseudo-inverse
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) d[i] = 0.0;
+        return;
+    }
+    double x[6];
+PCORE_UNROLL
+    for (int i = 0; i < 6; i++) x[i] = -sys[21 + perm[i]];  // P (-b)
+PCORE_UNROLL
+    for (int j = 0; j < 6; j++)
+PCORE_UNROLL
+        for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
+#if PCORE_LANE_PAR
+    if constexpr (WAVE) {
+        double Dd[6], q[6];
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) Dd[i] = A[i][i];
+        lane_div<6>(x, Dd, q);
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) x[i] = __builtin_fabs(Dd[i]) > 2.2250738585072014e-308 ? q[i] : 0.0;
+    } else
+#endif
+    {
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) {
+            const double Di = A[i][i];
+            x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
+        }
+    }
+PCORE_UNROLL
+    for (int i = 4; i >= 0; i--) {
+        double s = A[i + 1][i] * x[i + 1];
+PCORE_UNROLL
+        for (int j = i + 2; j < 6; j++) s = s + A[j][i] * x[j];
+        x[i] = x[i] - s;
+    }
+    // P^T x: d[perm[i]] = x[i]
+PCORE_UNROLL
+    for (int a = 0; a < 6; a++) {
+        double v = x[0];
+PCORE_UNROLL
+        for (int i = 1; i < 6; i++) v = perm[i] == a ? x[i] : v;
+        d[a] = v;
+    }
 }
 
 // se3_exp (fast_gicp so3.hpp): so3_exp quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and

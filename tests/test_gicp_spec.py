@@ -284,3 +284,40 @@ def test_gicp_whole_scene_targets_independent_chain():
         assert np.abs(T1 - T2).max() < 1e-9
         iters.append(it1)
     assert max(iters) == 150
+
+
+def test_lm_solve_pivot_order_first_equals_eigen_swaps():
+    """The kernels' LDLT (pivot sequence found first as a selection on |diag|, then the permuted matrix factored
+    without swaps) is bit-identical to the restatement of Eigen's in-place LDLT with its row / column swaps, on random
+    SPD and indefinite systems, tied and zero diagonals, a zero system, huge / tiny scales and non-finite entries."""
+    rng = np.random.default_rng(31)
+    iu = np.triu_indices(6)
+    cases = []
+    for t in range(4000):
+        A = rng.normal(size=(6, 6)) * rng.choice([1e-6, 1.0, 1e3, 1e12])
+        H = A @ A.T if t % 3 else A + A.T  # SPD or indefinite
+        if t % 7 == 0:  # ties in the diagonal magnitudes
+            v = H[0, 0]
+            for i in rng.choice(6, 3, replace=False):
+                H[i, i] = v if rng.random() < 0.5 else -v
+        if t % 11 == 0:
+            H[rng.integers(6), :] = 0.0
+            H = (H + H.T) * 0.5
+        b = rng.normal(size=6)
+        cases.append((np.concatenate([H[iu], b, [0.0]]), float(rng.choice([0.0, 1e-9, 1e-3, 10.0]))))
+    cases.append((np.zeros(28), 0.0))
+    cases.append((np.zeros(28), 1e-9))
+    z = np.zeros(28)
+    z[[0, 6, 11]] = 5.0
+    cases.append((z.copy(), 0.0))
+    for bad in (np.nan, np.inf, -np.inf):
+        for pos in (0, 3, 6, 20, 22):
+            sysb = cases[5][0].copy()
+            sysb[pos] = bad
+            cases.append((sysb, 1e-9))
+    for sysv, lam in cases:
+        a = oracle.gicp_lm_solve_sys(sysv, lam)
+        b = oracle.gicp_lm_solve_sys(sysv, lam, swaps=True)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)) or (np.isnan(a) == np.isnan(b)).all() and \
+            np.array_equal(np.where(np.isnan(a), 0, a).view(np.uint64), np.where(np.isnan(b), 0, b).view(np.uint64)), \
+            (sysv, lam, a, b)

@@ -114,3 +114,39 @@ def test_localize_objects_greedy_render_matches_oracle_pipeline(tmp_path, icp):
     auc_gpu = metrics.compute_pose_metrics(np.array(g_err))["auc"]
     auc_orc = metrics.compute_pose_metrics(np.array(o_err))["auc"]
     assert abs(auc_gpu - auc_orc) <= 0.1, (auc_gpu, auc_orc)
+
+
+def test_device_state_path_equals_host_state_path():
+    """the 6-DoF search builds its per-state inputs on the device (_successor_states_device,
+    _state_poses_dev, _pose_labels_dev, _obs_totals_dev); they equal the host path's (generate_successor_states,
+    _pose_in_cam / _poses_device, _pose_labels, _obs_totals) element for element -- including a model that is not
+    among the segmented objects (required object id = len(segmented), observed total 0), kept here by a zero
+    neighbour threshold."""
+    names = ["003_cracker_box", "005_tomato_soup_can", "061_foam_brick"]
+    extra = "024_bowl"
+    rng = np.random.default_rng(21)
+    gts = np.stack([syn.default_gt_pose(rng, c) for c in [(-0.12, 0.0, 0.8), (0.0, 0.05, 0.85), (0.13, -0.03, 0.75)]])
+    sc = syn.make_scene(names, gts, oracle_render_fn, rng=rng)
+    bank = {n: ModelMetaData(n, model=sc.bank.models[i]) for i, n in enumerate(names)}
+    bank[extra] = ModelMetaData(extra, model=syn.ycb_proxy(extra))
+    cam = CameraIntrinsics(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy)
+    rec = ObjectRecognizer(bank, cam, PerchParams(icp_type=0, min_neighbor_points_for_valid_pose=0))
+    rec.set_static_input(names + [extra])
+    lists = {}
+    for k, name in enumerate(names + [extra]):
+        P = syn.candidate_poses(gts[min(k, 2)][:3, 3], 40, rng, num_viewpoints=10, inplane=4)
+        lists[name] = np.array([np.concatenate([T[:3, 3], matrix_to_quat_xyzw(T[:3, :3])]) for T in P])
+    inp = RecognitionInput(names, sc.depth_raw, sc.mask, depth_factor=sc.depth_factor, pose_lists=lists)
+    rec.set_input(inp)  # segmented objects: the three scene names; the bowl has no label
+    model_d, req_d, pose_d = rec._successor_states_device(inp)
+    host = rec.generate_successor_states(inp)
+    assert np.array_equal(model_d.cpu().numpy(), host.model) and np.array_equal(req_d.cpu().numpy(), host.req)
+    assert np.array_equal(pose_d.cpu().numpy(), host.pose)
+    assert (host.model == 3).sum() == 40 and (host.req[host.model == 3] == 3).all()  # the unsegmented model's states
+    poses_dev = rec._state_poses_dev(pose_d, model_d).cpu().numpy()
+    assert np.array_equal(poses_dev.view(np.uint32), rec._poses_device(host).cpu().numpy().view(np.uint32))
+    assert np.array_equal(poses_dev.view(np.uint32), rec._pose_in_cam(host).view(np.uint32))
+    assert np.array_equal(rec._pose_labels_dev(req_d).cpu().numpy(), rec._pose_labels(host).cpu().numpy())
+    tot_dev, tot_host = rec._obs_totals_dev(req_d).cpu().numpy(), rec._obs_totals(host)
+    assert np.array_equal(tot_dev.view(np.uint32), tot_host.view(np.uint32))
+    assert (tot_host[host.model == 3] == 0).all()
