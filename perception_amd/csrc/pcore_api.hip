@@ -93,6 +93,7 @@ struct pcore_ctx {
     DevBuf<int32_t> fb_ctr;       // FusedArgs::fb_ctr
     DevBuf<int32_t> win_hist;     // FusedArgs::win_hist
     int32_t* fb_host = nullptr;   // mapped host memory (FusedArgs::fb_host), host view
+    bool fb_dirty = false;        // a captured launch ran: clear the feedback counters before the next eager one
     int32_t* fb_dev = nullptr;    // the same, device view
     int32_t fb_seq = 0;           // sequence number of the last fused launch
     int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
@@ -647,7 +648,7 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
 // Tile of the fused window launch ("Pose windows"): the tier with the most workgroups per CU
 // whose tile holds the windows of >= 99 % of the poses of the last finished call with the same sampled
 // image; kDefaultTier until one is known.  Only the speed depends on the choice, never the results.
-static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
+static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hipStream_t s) {
     const bool colour = a.cid != nullptr;
     const int nsamp = a.ws * a.hs;
     hipError_t e;
@@ -657,10 +658,21 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
         c->fb_host[kTileTiers + 2] = -1;
         if ((e = hipHostGetDevicePointer((void**)&c->fb_dev, c->fb_host, 0)) != hipSuccess) return e;
         if ((e = dev_reserve(c->fb_ctr, 2)) != hipSuccess) return e;
-        if ((e = dev_reserve(c->win_hist, kTileTiers + 1)) != hipSuccess) return e;
+        if ((e = dev_reserve(c->win_hist, 2 * (kTileTiers + 1))) != hipSuccess) return e;
         if ((e = hipMemset(c->fb_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
-        if ((e = hipMemset(c->win_hist.p, 0, (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
+        if ((e = hipMemset(c->win_hist.p, 0, 2 * (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
     }
+    // a captured launch keeps one parity and never publishes: its replays leave counts behind, cleared (on the
+    // stream) before the next eager launch
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if ((e = hipStreamIsCapturing(s, &cap)) != hipSuccess) return e;
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    if (!capturing && c->fb_dirty) {
+        if ((e = hipMemsetAsync(c->fb_ctr.p, 0, 2 * sizeof(int32_t), s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(c->win_hist.p, 0, 2 * (kTileTiers + 1) * sizeof(int32_t), s)) != hipSuccess) return e;
+        c->fb_dirty = false;
+    }
+    if (capturing) c->fb_dirty = true;
     int edge[kTileTiers];
     for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, c->dinfo);
     const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);
@@ -696,8 +708,9 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a) {
     for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
     a.fb_ctr = c->fb_ctr.p;
     a.win_hist = c->win_hist.p;
-    a.fb_host = c->fb_dev;
+    a.fb_host = capturing ? nullptr : c->fb_dev;
     a.fb_seq = ++c->fb_seq;
+    a.fb_par = a.fb_seq & 1;
     return hipSuccess;
 }
 
@@ -814,7 +827,7 @@ static int evaluate_impl(pcore_ctx* c, const float* d_poses, const int32_t* d_po
     a.sel_keys = d_keys;
     a.sel_base = index_base;
     a.sel_models = num_models;
-    HIPC(c, set_fused_tiles(c, num_poses, a));
+    HIPC(c, set_fused_tiles(c, num_poses, a, s));
     HIPC(c, launch_fused_cost(a, s));
     return PCORE_OK;
 }

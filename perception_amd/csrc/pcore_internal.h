@@ -109,15 +109,16 @@ struct FusedArgs {
     int32_t* cid;               // N x nsamp scratch: original triangle of each sample's nearest fragment
     float colour_thr;           // color_distance_threshold
     // sample windows ("Pose windows"): the z-sample tile in LDS holds `tcap` samples; a pose whose window
-    // is larger is processed in chunks of the tile.  fb_ctr[0] counts those poses, fb_ctr[1] the finished
-    // workgroups; the last workgroup publishes and returns both to 0
+    // is larger is processed in chunks of the tile.  fb_ctr[par] counts those poses (two buffers by launch parity)
     int32_t tcap;
     int32_t* fb_ctr;
-    // window-size histogram (bin b: windows of at most hist_edge[b] samples, the last bin the rest),
-    // published by the launch's last workgroup to fb_host (mapped host memory) and reset there
+    // window-size histogram (bin b: windows of at most hist_edge[b] samples, the last bin the rest), two sets by
+    // launch parity fb_par: each launch counts into its own and its workgroup 0 publishes the other (the previous
+    // launch's) to fb_host (mapped host memory, nullable: not in a captured graph) and clears it
     int32_t hist_edge[kTileTiers];
-    int32_t* win_hist;  // kTileTiers + 1 bins
+    int32_t* win_hist;  // 2 x (kTileTiers + 1) bins
     int32_t* fb_host;   // kTileTiers + 1 bins + 1 chunked-pose count + 1 sequence number
+    int32_t fb_par;
     int32_t fb_seq;
     // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
     // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
