@@ -903,591 +903,6 @@ gicp_kernel(GicpArgs g, int num_poses) {
 }
 
 
-// ------------------------------------------------------------------------------------------------
-// gicp_batch_kernel: B poses per wave, their LM steps lane-parallel
-// ------------------------------------------------------------------------------------------------
-// gicp_kernel runs a pose's whole iteration on one wave, and the LM step (the pivoted LDLT of H + lambda I,
-// se3_exp, the compose and the accept / reject logic) is uniform arithmetic every lane repeats: ~40 % of a pose-
-// iteration's wave time (profiles/r04b_phase_hist.txt).  Here a wave holds B poses ("slots"): each round it makes
-// one point pass per slot with all 64 lanes, then ONE LM step in which lane p advances slot p -- B poses' steps for
-// the price of one.  Every pose still follows step_lm's sequence exactly; only the interleaving
-// with other poses differs, so the results equal gicp_kernel's and the oracle's bit for bit.
-//
-// A point pass linearises the slot's pose at its trial transform x_i (the step the LM lane just took) and, in the
-// same pass over the points, sums the trial error at x_i with the current iteration's correspondences and
-// Mahalanobis matrices (read before the pass overwrites them with x_i's): on an accepted trial -- every trial on C3 --
-// that linearisation is the next iteration's.  After a rejected trial the current iteration's correspondences and M
-// are gone, so the next pass recomputes them at x (search + M) for its trial error ("restore").  The first pass of a
-// pose only linearises at the identity.
-//   - per slot in LDS: the pose, x, x_i, the current system (at x), the last pass's system, the pending step d, lambda,
-//     nu, the trial error, counters, and the correspondence history (HE float transforms; the sets in HBM scratch)
-//   - the point pass: the same per-point arithmetic, point order, per-lane sums and reduction trees as gicp_kernel
-//   - the LM lane step: gicpm::lm_solve / se3_exp with WAVE = false (each lane its own system), same operations
-enum : int { kSlotEmpty = 0, kSlotFirst = 1, kSlotTrial = 2, kSlotRestore = 3 };
-
-template <int HE>
-struct BatchSlot {
-    double x[12];           // R (row-major), t: the pose's current transform
-    double xi[12];          // the pending trial transform
-    double sys[gicpm::kTerms];   // the current iteration's system (at x)
-    double spec[gicpm::kTerms];  // the last pass's system (at its linearisation transform)
-    double d[6];            // the pending trial's step
-    double lambda, nu, ytrial;
-    unsigned long long kept;  // bit 4e: history entry e is filled
-    int pose, iters, trials, phase;
-    int conv;               // the pending trial's delta is converged
-    int ring;               // next history entry to replace
-    int eset, elast;        // history set of x's linearisation / of the last pass's
-    int ns, nt, seg, lo, qoff;  // the pose's source points, target segment (index, first target, first key quad)
-    unsigned hist[HE][12];  // float transform bits of the history entries
-};
-
-// gicp_pose's fields from the slot's cached pose data (filled at refill: no dependent global loads per pass)
-template <int HE>
-__device__ __forceinline__ GicpPose slot_pose(const GicpArgs& g, const BatchSlot<HE>& S) {
-    GicpPose p;
-    p.pose = __builtin_amdgcn_readfirstlane(S.pose);
-    p.gp = g.pose_base + p.pose;
-    p.ns = __builtin_amdgcn_readfirstlane(S.ns);
-    p.nt = __builtin_amdgcn_readfirstlane(S.nt);
-    p.seg = __builtin_amdgcn_readfirstlane(S.seg);
-    const int lo = __builtin_amdgcn_readfirstlane(S.lo), qoff = __builtin_amdgcn_readfirstlane(S.qoff);
-    p.src = g.src + (size_t)p.pose * g.src_cap;
-    p.scov = g.src_cov + (size_t)6 * p.pose * g.src_cap;
-    p.corr = g.corr + (size_t)p.pose * g.src_cap;
-    p.mah = g.mahal + (size_t)6 * p.pose * g.src_cap;
-    p.tcov = g.tgt_cov + (size_t)6 * lo;
-    p.tgt = g.tgt + lo;
-    p.tquads = g.tgt_quads + (size_t)16 * qoff;
-    p.use_grid = p.nt > kGridNNMin && g.grids != nullptr && p.seg >= 0;
-    return p;
-}
-
-__device__ __forceinline__ void xform_load(const double* v, Xform& x) {
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-#pragma unroll
-        for (int c = 0; c < 3; c++) x.R[r][c] = uniform_d(v[3 * r + c]);
-        x.t[r] = uniform_d(v[9 + r]);
-    }
-}
-__device__ __forceinline__ void xform_get(const double* v, Xform& x) {  // per-lane (the LM lane step)
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-#pragma unroll
-        for (int c = 0; c < 3; c++) x.R[r][c] = v[3 * r + c];
-        x.t[r] = v[9 + r];
-    }
-}
-__device__ __forceinline__ void xform_put(double* v, const Xform& x) {
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-#pragma unroll
-        for (int c = 0; c < 3; c++) v[3 * r + c] = x.R[r][c];
-        v[9 + r] = x.t[r];
-    }
-}
-
-// history lookup of the float transform (Rf, tf) in slot S: the entry holding the same 12 float bit patterns, or -- on
-// a miss -- a fresh entry (the ring's next) recorded for it.  Returns the entry; `hit` says whether its set holds the
-// correspondences already.  Lane l compares components 3 (l & 3) + v of entry l >> 2.
-template <int HE>
-__device__ __forceinline__ int hist_lookup(BatchSlot<HE>& S, const float (&Rf)[3][3], const float (&tf)[3], int lane,
-                                           bool& hit) {
-    const int sub = lane & 3, ent = lane >> 2;
-    const float c0 = sub == 0 ? Rf[0][0] : sub == 1 ? Rf[1][0] : sub == 2 ? Rf[2][0] : tf[0];
-    const float c1 = sub == 0 ? Rf[0][1] : sub == 1 ? Rf[1][1] : sub == 2 ? Rf[2][1] : tf[1];
-    const float c2 = sub == 0 ? Rf[0][2] : sub == 1 ? Rf[1][2] : sub == 2 ? Rf[2][2] : tf[2];
-    const unsigned b0 = __builtin_bit_cast(unsigned, c0), b1 = __builtin_bit_cast(unsigned, c1),
-                   b2 = __builtin_bit_cast(unsigned, c2);
-    bool m = false;
-    if (ent < HE) m = S.hist[ent][3 * sub] == b0 && S.hist[ent][3 * sub + 1] == b1 && S.hist[ent][3 * sub + 2] == b2;
-    const unsigned long long eq = __ballot(m);
-    const unsigned long long kept = __builtin_amdgcn_readfirstlane((unsigned)S.kept) |
-                                    ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(S.kept >> 32)) << 32);
-    const unsigned long long full = eq & (eq >> 1) & (eq >> 2) & (eq >> 3) & kept;
-    if (full != 0ull) {
-        hit = true;
-        return __builtin_ctzll(full) >> 2;
-    }
-    hit = false;
-    const int e = __builtin_amdgcn_readfirstlane(S.ring);
-    wave_lds_sync();  // every lane has read S.ring / S.kept / the entries
-    if (ent == e) {
-        S.hist[e][3 * sub] = b0;
-        S.hist[e][3 * sub + 1] = b1;
-        S.hist[e][3 * sub + 2] = b2;
-    }
-    if (lane == 0) {
-        S.ring = e + 1 == HE ? 0 : e + 1;
-        S.kept = kept | (1ull << (4 * e));
-    }
-    wave_lds_sync();
-    return e;
-}
-
-// One slot's point pass (all 64 lanes; the slot's fields are wave-uniform).  Writes the linearisation at the pass's
-// transform to S.spec (28 terms) and the trial error to S.ytrial.
-template <int HE>
-__device__ __forceinline__ void batch_pass(const GicpArgs& g, BatchSlot<HE>& S, double* sRed, int lane GPROF_PARAM) {
-    GPROF_T(tp0);
-    const int pose = __builtin_amdgcn_readfirstlane(S.pose);
-    const int phase = __builtin_amdgcn_readfirstlane(S.phase);
-    const GicpPose P = gicp_pose(g, pose);
-    LabelGrid G{};
-    if (P.use_grid) G = g.grids[P.seg];
-    const bool trial = phase != kSlotFirst, restore = phase == kSlotRestore;
-    Xform xl;  // the linearisation transform: x on the first pass, else the trial transform x_i
-    xform_load(phase == kSlotFirst ? S.x : S.xi, xl);
-    float Rf[3][3], tf[3];
-    xform_float(xl, Rf, tf);
-    const bool hist = g.corr_hist != nullptr && P.ns <= g.corr_hist_cap;
-    int32_t* cur = P.corr;  // the current iteration's correspondences (trial error)
-    int32_t* lin = P.corr;  // the pass's correspondences
-    bool reuse = false;
-    if (hist) {
-        int32_t* const hbase = g.corr_hist + (size_t)pose * kCorrHist * g.corr_hist_cap;
-        cur = hbase + (size_t)__builtin_amdgcn_readfirstlane(S.eset) * g.corr_hist_cap;
-        const int e = hist_lookup(S, Rf, tf, lane, reuse);
-        lin = hbase + (size_t)e * g.corr_hist_cap;
-        if (lane == 0) S.elast = e;
-    }
-    Xform xc;  // restore: the current transform x, for its correspondences and M
-    float Rcf[3][3], tcf[3];
-    if (restore) {
-        xform_load(S.x, xc);
-        xform_float(xc, Rcf, tcf);
-    }
-    double acc[gicpm::kTerms];
-#pragma unroll
-    for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-    double ea = 0.0;
-    GPROF_TD(tp1, Rf[0][0]);
-    GPROF_ADD(4, tp0, tp1);
-    for (int i0 = 0; i0 < P.ns; i0 += 64) {
-        GPROF_T(tr0);
-        const int i = i0 + lane;
-        const bool act = i < P.ns;
-        const float4 sp = act ? P.src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-        double q[3];  // x_l s: the trial error's transformed point and the linearisation's
-#pragma unroll
-        for (int r = 0; r < 3; r++) q[r] = xl.R[r][0] * s0 + xl.R[r][1] * s1 + xl.R[r][2] * s2 + xl.t[r];
-        if (trial) {
-            // the current iteration's correspondence and M of this point (read before this pass overwrites them)
-            int jo = -1;
-            double Mo[6];
-            if (restore) {
-                float qf[3], best = INFINITY;
-                gicpm::query_f(Rcf, tcf, sp.x, sp.y, sp.z, qf);
-                if (P.use_grid) {
-                    if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, jo);
-                } else {
-                    scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, jo);
-                }
-                if (act && jo >= 0) {
-                    double cs[6], ct[6];
-                    load_cov(P.scov, i, cs);
-                    load_cov(P.tcov, jo, ct);
-                    gicpm::mahal_matrix(xc.R, cs, ct, Mo);
-                }
-            } else if (act) {
-                jo = cur[i];
-                if (jo >= 0) {
-                    const double2* m2 = reinterpret_cast<const double2*>(P.mah + (size_t)6 * i);
-                    const double2 a = m2[0], b = m2[1], c = m2[2];
-                    Mo[0] = a.x; Mo[1] = a.y; Mo[2] = b.x; Mo[3] = b.y; Mo[4] = c.x; Mo[5] = c.y;
-                }
-            }
-            if (act && jo >= 0) {
-                const float4 tj = P.tgt[jo];
-                const double e[3] = {(double)tj.x - q[0], (double)tj.y - q[1], (double)tj.z - q[2]};
-                ea += gicpm::mahal_err(Mo, e);
-            }
-        }
-        GPROF_TD(tr1, ea);
-        GPROF_ADD(5, tr0, tr1);
-        // linearisation at x_l: the correspondence from the history set or the search, then the contribution
-        int j = -1;
-        if (reuse) {
-            j = act ? lin[i] : -1;
-        } else {
-            float qf[3], best = INFINITY;
-            gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
-            if (P.use_grid) {
-                if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
-            } else {
-                scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, j);
-            }
-            if (act) lin[i] = j;
-        }
-        GPROF_TD(tr2, j);
-        GPROF_ADD(6, tr1, tr2);
-        if (act && j >= 0) {
-            double cs[6], ct[6], M6[6];
-            load_cov(P.scov, i, cs);
-            load_cov(P.tcov, j, ct);
-            const float4 tj = P.tgt[j];
-            const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
-            gicpm::contrib(xl.R, q, cs, t3, ct, acc, M6);
-            double2* m2 = reinterpret_cast<double2*>(P.mah + (size_t)6 * i);
-            m2[0] = make_double2(M6[0], M6[1]);
-            m2[1] = make_double2(M6[2], M6[3]);
-            m2[2] = make_double2(M6[4], M6[5]);
-        }
-        GPROF_TD(tr3, acc[gicpm::kErr]);
-        GPROF_ADD(7, tr2, tr3);
-    }
-    GPROF_T(tp2);
-    const double* sys = lds_tree_sum(acc, sRed, lane);
-    if (lane < gicpm::kTerms) S.spec[lane] = sys[lane];
-    const double yt = wave_sum_lane0(ea);  // lane 0: the tree's sum (gicp_kernel's trial error order)
-    if (lane == 0) S.ytrial = yt;
-    wave_lds_sync();
-    GPROF_TD(tp3, S.ytrial);
-    GPROF_ADD(8, tp2, tp3);
-}
-
-// The LM lane step of one slot (lane p, per-lane values): step_lm's decisions after the slot's pass, then the next
-// trial's solve.  Returns true when the pose is finished (its adjusted pose is written).
-template <int HE>
-__device__ __forceinline__ bool batch_lm_step(const GicpArgs& g, BatchSlot<HE>& S) {
-    int phase = S.phase;
-    Xform x;
-    xform_get(S.x, x);
-    double lambda = S.lambda;
-    bool done = false;
-    if (phase == kSlotFirst) {
-#pragma unroll
-        for (int v = 0; v < gicpm::kTerms; v++) S.sys[v] = S.spec[v];
-        S.eset = S.elast;
-        if (lambda < 0.0) lambda = gicpm::lm_init_lambda(S.sys);
-        S.nu = 2.0;
-        S.trials = 0;
-    } else {
-        double d[6];
-#pragma unroll
-        for (int a = 0; a < 6; a++) d[a] = S.d[a];
-        const double rho = gicpm::lm_rho(S.sys, lambda, d, S.sys[gicpm::kErr], S.ytrial);
-        if (rho < 0.0) {
-            if (S.conv) {
-                done = true;  // converged on a rejected trial: x unchanged
-            } else {
-                lambda = S.nu * lambda;
-                S.nu = 2.0 * S.nu;
-                S.trials = S.trials + 1;
-                if (S.trials == gicpm::kLmMaxTrials) done = true;  // "lm not converged"
-                phase = kSlotRestore;
-            }
-        } else {
-            xform_get(S.xi, x);
-            xform_put(S.x, x);
-            lambda = gicpm::lm_accept_lambda(lambda, rho);
-            if (S.conv || S.iters >= g.max_iter) {
-                done = true;
-            } else {
-                S.iters = S.iters + 1;  // the pass's linearisation at x_i is the next iteration's
-#pragma unroll
-                for (int v = 0; v < gicpm::kTerms; v++) S.sys[v] = S.spec[v];
-                S.eset = S.elast;
-                S.nu = 2.0;
-                S.trials = 0;
-                phase = kSlotTrial;
-            }
-        }
-    }
-    if (!done) {
-        double d[6];
-        gicpm::lm_solve<false>(S.sys, lambda, d);
-        if (!gicpm::all_finite6(d)) {
-            done = true;  // guard: a non-finite system
-        } else {
-            double Rd[3][3], td[3];
-            gicpm::se3_exp<false>(d, Rd, td);
-            Xform xi;
-            gicpm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
-            xform_put(S.xi, xi);
-#pragma unroll
-            for (int a = 0; a < 6; a++) S.d[a] = d[a];
-            S.conv = gicpm::is_converged(Rd, td, g.rot_eps, g.trans_eps) ? 1 : 0;
-            if (phase == kSlotFirst) phase = kSlotTrial;
-        }
-    }
-    S.lambda = lambda;
-    S.phase = phase;
-    if (done) {
-        write_pose(g, g.pose_base + S.pose, x, S.iters);
-        S.phase = kSlotEmpty;
-    }
-    return done;
-}
-
-// Split variant (PCORE_GICP_BATCH_SPLIT): the trial error is a pass of its own instead of riding on the next
-// linearisation -- a slot alternates a linearisation pass (at x, after an accepted trial) and trial-error passes (at
-// x_i with x's correspondences and M, which no pass overwrites before the trial is decided), so no restore is needed.
-#ifndef PCORE_GICP_BATCH_SPLIT
-#define PCORE_GICP_BATCH_SPLIT 0
-#endif
-enum : int { kSlotLin = 4, kSlotErr = 5 };
-
-template <int HE>
-__device__ __forceinline__ void batch_pass_split(const GicpArgs& g, BatchSlot<HE>& S, double* sRed, int lane) {
-    const int phase = __builtin_amdgcn_readfirstlane(S.phase);
-    const GicpPose P = slot_pose(g, S);
-    const int pose = P.pose;
-    const bool hist = g.corr_hist != nullptr && P.ns <= g.corr_hist_cap;
-    int32_t* const hbase = hist ? g.corr_hist + (size_t)pose * kCorrHist * g.corr_hist_cap : nullptr;
-    if (phase == kSlotErr) {
-        // the trial error at x_i with the current iteration's correspondences and M (lm_iteration's error loop)
-        Xform xi;
-        xform_load(S.xi, xi);
-        const int32_t* cur = hist ? hbase + (size_t)__builtin_amdgcn_readfirstlane(S.eset) * g.corr_hist_cap : P.corr;
-        double ea = 0.0;
-        for (int i0 = 0; i0 < P.ns; i0 += 64) {
-            const int i = i0 + lane;
-            const int j = i < P.ns ? cur[i] : -1;
-            if (j >= 0) {
-                const float4 sp = P.src[i], tj = P.tgt[j];
-                const double2* m2 = reinterpret_cast<const double2*>(P.mah + (size_t)6 * i);
-                const double2 a = m2[0], b = m2[1], c = m2[2];
-                const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-                const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-                double e[3];
-#pragma unroll
-                for (int r = 0; r < 3; r++) {
-                    const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
-                    e[r] = (double)(r == 0 ? tj.x : r == 1 ? tj.y : tj.z) - q;
-                }
-                ea += gicpm::mahal_err(M6, e);
-            }
-        }
-        const double yt = wave_sum_lane0(ea);
-        if (lane == 0) S.ytrial = yt;
-        wave_lds_sync();
-        return;
-    }
-    // linearisation at x (kSlotFirst / kSlotLin)
-    LabelGrid G{};
-    if (P.use_grid) G = g.grids[P.seg];
-    Xform x;
-    xform_load(S.x, x);
-    float Rf[3][3], tf[3];
-    xform_float(x, Rf, tf);
-    int32_t* lin = P.corr;
-    bool reuse = false;
-    if (hist) {
-        const int e = hist_lookup(S, Rf, tf, lane, reuse);
-        lin = hbase + (size_t)e * g.corr_hist_cap;
-        if (lane == 0) S.elast = e;
-    }
-    double acc[gicpm::kTerms];
-#pragma unroll
-    for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-    for (int i0 = 0; i0 < P.ns; i0 += 64) {
-        const int i = i0 + lane;
-        const bool act = i < P.ns;
-        const float4 sp = act ? P.src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        int j = -1;
-        if (reuse) {
-            j = act ? lin[i] : -1;
-        } else {
-            float qf[3], best = INFINITY;
-            gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
-            if (P.use_grid) {
-                if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
-            } else {
-                scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, j);
-            }
-            if (act) lin[i] = j;
-        }
-        if (act && j >= 0) {
-            const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-            double q[3];
-#pragma unroll
-            for (int r = 0; r < 3; r++) q[r] = x.R[r][0] * s0 + x.R[r][1] * s1 + x.R[r][2] * s2 + x.t[r];
-            double cs[6], ct[6], M6[6];
-            load_cov(P.scov, i, cs);
-            load_cov(P.tcov, j, ct);
-            const float4 tj = P.tgt[j];
-            const double t3[3] = {(double)tj.x, (double)tj.y, (double)tj.z};
-            gicpm::contrib(x.R, q, cs, t3, ct, acc, M6);
-            double2* m2 = reinterpret_cast<double2*>(P.mah + (size_t)6 * i);
-            m2[0] = make_double2(M6[0], M6[1]);
-            m2[1] = make_double2(M6[2], M6[3]);
-            m2[2] = make_double2(M6[4], M6[5]);
-        }
-    }
-    const double* sys = lds_tree_sum(acc, sRed, lane);
-    if (lane < gicpm::kTerms) S.spec[lane] = sys[lane];
-    wave_lds_sync();
-}
-
-template <int HE>
-__device__ __forceinline__ bool batch_lm_step_split(const GicpArgs& g, BatchSlot<HE>& S) {
-    int phase = S.phase;
-    double lambda = S.lambda;
-    bool done = false, solve = false;
-    if (phase == kSlotFirst || phase == kSlotLin) {  // a new iteration's system at x
-#pragma unroll
-        for (int v = 0; v < gicpm::kTerms; v++) S.sys[v] = S.spec[v];
-        S.eset = S.elast;
-        if (lambda < 0.0) lambda = gicpm::lm_init_lambda(S.sys);
-        S.nu = 2.0;
-        S.trials = 0;
-        solve = true;
-    } else {  // kSlotErr: decide the trial
-        double d[6];
-#pragma unroll
-        for (int a = 0; a < 6; a++) d[a] = S.d[a];
-        const double rho = gicpm::lm_rho(S.sys, lambda, d, S.sys[gicpm::kErr], S.ytrial);
-        if (rho < 0.0) {
-            if (S.conv) {
-                done = true;
-            } else {
-                lambda = S.nu * lambda;
-                S.nu = 2.0 * S.nu;
-                S.trials = S.trials + 1;
-                if (S.trials == gicpm::kLmMaxTrials) done = true;
-                else solve = true;
-            }
-        } else {
-#pragma unroll
-            for (int v = 0; v < 12; v++) S.x[v] = S.xi[v];
-            lambda = gicpm::lm_accept_lambda(lambda, rho);
-            if (S.conv || S.iters >= g.max_iter) {
-                done = true;
-            } else {
-                S.iters = S.iters + 1;
-                phase = kSlotLin;
-            }
-        }
-    }
-    Xform x;
-    xform_get(S.x, x);
-    if (solve) {
-        double d[6];
-        gicpm::lm_solve<false>(S.sys, lambda, d);
-        if (!gicpm::all_finite6(d)) {
-            done = true;
-        } else {
-            double Rd[3][3], td[3];
-            gicpm::se3_exp<false>(d, Rd, td);
-            Xform xi;
-            gicpm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
-            xform_put(S.xi, xi);
-#pragma unroll
-            for (int a = 0; a < 6; a++) S.d[a] = d[a];
-            S.conv = gicpm::is_converged(Rd, td, g.rot_eps, g.trans_eps) ? 1 : 0;
-            phase = kSlotErr;
-        }
-    }
-    S.lambda = lambda;
-    S.phase = phase;
-    if (done) {
-        write_pose(g, g.pose_base + S.pose, x, S.iters);
-        S.phase = kSlotEmpty;
-    }
-    return done;
-}
-
-// lane p < B: pull poses into an empty slot p until one needs iterating (poses without source points, target points
-// or iterations are written at once) or the queue is empty
-template <int HE>
-__device__ __forceinline__ void batch_refill(const GicpArgs& g, BatchSlot<HE>& S, int num_poses) {
-    while (S.phase == kSlotEmpty) {
-        const int q = atomicAdd(g.work_counter, 1);
-        if (q >= num_poses) {
-            S.pose = -1;
-            return;
-        }
-        const int pose = g.pose_order ? g.pose_order[q] : q;
-        const int gp = g.pose_base + pose;
-        const int ns = g.src_count[pose];
-        int seg = g.whole_seg;
-        if (g.pose_label) {
-            const int pl = g.pose_label[gp];
-            seg = (pl >= 0 && pl < g.num_segs) ? pl : -1;
-        }
-        const int nt = seg >= 0 ? g.seg_hi[seg] - g.seg_lo[seg] : 0;
-        Xform x;
-        xform_identity(x);
-        if (ns <= 0 || nt <= 0 || g.max_iter <= 0) {
-            write_pose(g, gp, x, 0);
-            continue;
-        }
-        S.pose = pose;
-        S.ns = ns;
-        S.nt = nt;
-        S.seg = seg;
-        S.lo = seg >= 0 ? g.seg_lo[seg] : 0;
-        S.qoff = seg >= 0 ? g.seg_qoff[seg] : 0;
-        xform_put(S.x, x);
-        S.lambda = -1.0;
-        S.iters = 1;
-        S.kept = 0ull;
-        S.ring = 0;
-        S.eset = 0;
-        S.elast = 0;
-        S.phase = kSlotFirst;
-    }
-}
-
-template <int B, int HE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
-gicp_batch_kernel(GicpArgs g, int num_poses) {
-    static_assert(B >= 1 && B <= 64 && 4 * HE <= 64 && HE <= kCorrHist, "slots / history entries");
-    __shared__ double sRed[kRedDoubles];
-    __shared__ BatchSlot<HE> sSlot[B];
-    const int lane = threadIdx.x;
-    if (lane < B) {
-        sSlot[lane].phase = kSlotEmpty;
-        batch_refill(g, sSlot[lane], num_poses);
-    }
-    wave_lds_sync();
-    GPROF_DECL;  // [0] point passes, [1] LM lane steps + refills (wave clocks), [2] rounds, [3] passes
-    for (;;) {
-        const unsigned long long live = __ballot(lane < B && sSlot[lane < B ? lane : 0].phase != kSlotEmpty);
-        if (live == 0ull) break;
-        GPROF_T(t0);
-#pragma unroll 1
-        for (int p = 0; p < B; p++)
-            if ((live >> p) & 1ull) {
-#if PCORE_GICP_BATCH_SPLIT
-                batch_pass_split(g, sSlot[p], sRed, lane);
-#else
-                batch_pass(g, sSlot[p], sRed, lane GPROF_ARG);
-#endif
-            }
-        GPROF_TD(t1, sRed[0]);
-        if (lane < B && ((live >> lane) & 1ull)) {
-#if PCORE_GICP_BATCH_SPLIT
-            if (batch_lm_step_split(g, sSlot[lane])) batch_refill(g, sSlot[lane], num_poses);
-#else
-            if (batch_lm_step(g, sSlot[lane])) batch_refill(g, sSlot[lane], num_poses);
-#endif
-        }
-        wave_lds_sync();
-        GPROF_TD(t2, sSlot[0].phase);
-        GPROF_ADD(0, t0, t1);
-        GPROF_ADD(1, t1, t2);
-#ifdef PCORE_GICP_PROFILE
-        gp_acc[2] += 1ull;
-        gp_acc[3] += (unsigned long long)__builtin_popcountll(live);
-#endif
-    }
-    GPROF_FLUSH;
-}
-
-#ifndef PCORE_GICP_SLOTS
-#define PCORE_GICP_SLOTS 3
-#endif
-
-#ifndef PCORE_GICP_SLOT_HIST
-#define PCORE_GICP_SLOT_HIST 16
-#endif
-constexpr int kGicpSlots = PCORE_GICP_SLOTS;
-constexpr int kGicpSlotHist = PCORE_GICP_SLOT_HIST;
-
 // Small batches (C1: 128 poses fill 128 of 1024 SIMDs) with large target segments: WPP waves per pose.
 // All waves search the correspondences of the iteration's source points (round r -> wave r % WPP), the
 // indices go to LDS, and wave 0 then adds the contributions and runs the LM iteration exactly as gicp_kernel
@@ -1656,12 +1071,6 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hi
         const int wgs = std::min(num_poses, num_cus * 2);
         hipLaunchKernelGGL(gicp_wide_kernel<kGicpWideWpp>, dim3(wgs), dim3(64 * kGicpWideWpp), wide_lds, s, g,
                            num_poses);
-        return hipGetLastError();
-    }
-    const char* kn = getenv("PCORE_GICP_KERNEL");
-    if (kn && kn[0] == 'b') {  // A/B knob: gicp_batch_kernel (B poses per wave; same results)
-        const int wgs = std::min(resident_wgs, (num_poses + kGicpSlots - 1) / kGicpSlots);
-        hipLaunchKernelGGL((gicp_batch_kernel<kGicpSlots, kGicpSlotHist>), dim3(wgs), dim3(64), 0, s, g, num_poses);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(gicp_kernel, dim3(std::min(resident_wgs, num_poses)), dim3(64), 0, s, g, num_poses);

@@ -258,7 +258,7 @@ PCORE_UNROLL
 // permutes, runs the unit-lower forward substitution, divides by D (|D_i| <= DBL_MIN gives 0), runs the unit-upper
 // back substitution and permutes back.  Sums run in index order.  sys: 28 terms (upper H row-major, b).
 // WAVE: every lane of the wave solves the same system (the pivots move to SGPRs, the independent divisions run
-// lane-parallel); WAVE = false: each lane solves its own system (gicp_batch_kernel's per-slot LM step, the host).
+// lane-parallel); WAVE = false: each lane (or the host) solves its own system.
 template <bool WAVE = (PCORE_LANE_PAR != 0)>
 PCORE_GHD void lm_solve_swaps(const double* sys, double lambda, double (&d)[6]) {
     double A[6][6];

@@ -416,7 +416,7 @@ def _label_covs(case, six=True):
     return cov
 
 
-@pytest.mark.parametrize("kernel", ["narrow", "wide", "batch"])
+@pytest.mark.parametrize("kernel", ["narrow", "wide"])
 @pytest.mark.parametrize("fixture", ["one_object", "three_objects"])
 def test_evaluate_icp_matches_oracle(fixture, kernel, request, monkeypatch):
     """Both GICP kernels -- one wave per pose (large batches) and eight waves per pose (small batches) --
