@@ -1,11 +1,12 @@
 #!/bin/bash
 # Full GPU session: parity tests, smoke, the counter passes that the bench line's roofline reads (two PMC
 # passes FETCH_SIZE / WRITE_SIZE -> profiles/pmc_traffic.json, three SQ passes -> profiles/sq_counters.json,
-# both tagged with the kernel-source digest), the bench itself, and the rocprofv3 kernel-trace summary of the
+# both tagged with the kernel-source digest; four SQ passes over gicp_kernel on C3 -> profiles/sq_counters_gicp.json,
+# tagged with the GICP-source digest), the bench itself, and the rocprofv3 kernel-trace summary of the
 # same bench command.  The folded json files are copied to $OUT (gpurun_out/ comes back; profiles/ on the box
 # does not).  Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
-OUT=${OUT:-gpurun_out}; TAG=${TAG:-r02}
+OUT=${OUT:-gpurun_out}; TAG=${TAG:-r04}
 mkdir -p $OUT; export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
   echo "== pytest"
@@ -26,6 +27,10 @@ if [ -z "$SKIP_PMC" ]; then
   OUT=$OUT TAG=sq_$TAG bash tools/sq_counters.sh || exit 1
   python tools/sq_json.py $OUT sq_$TAG 10000 || exit 1
   cp profiles/sq_counters.json $OUT/sq_counters.json
+  echo "== sq counters, GICP (C3)"
+  OUT=$OUT TAG=sqg_$TAG bash tools/sq_gicp.sh || exit 1
+  python tools/sq_gicp_json.py $OUT sqg_$TAG || exit 1
+  cp profiles/sq_counters_gicp.json $OUT/sq_counters_gicp.json
 fi
 echo "== bench"
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -20 $OUT/bench_$TAG.err; exit 1; }
