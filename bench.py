@@ -418,7 +418,7 @@ def main():
         "unit": "Gwave-instr/s",
         "frac": valu_achieved / valu_peak if valu_achieved else None,
         "traffic": traffic,
-        "kernel": "fused_cost_kernel (+ fused_cost_ovf_kernel: stage COST)",
+        "kernel": "fused_cost_kernel (stage COST, one launch per batch)",
         "kernel_ms": busy_ms,
         "timing": {"launch_span_ms": kern_ms, "gpu_ms_per_launch": busy_ms, "launches_in_flight": L,
                    "definition": "HIP events around every stage-COST call on its lane's stream over the timed region: "

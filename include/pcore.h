@@ -202,6 +202,25 @@ typedef struct pcore_gpu_stats {
 } pcore_gpu_stats;
 int pcore_get_stats(pcore_ctx* ctx, pcore_gpu_stats* out, int32_t reset);
 
+/* LDS tile of the fused window launch (no reference counterpart: the reference renders whole frames; DESIGN.md
+ * "Pose windows").  tier = the tier the next call starts from (wgs_per_cu[tier] workgroups per CU, a tile of
+ * edge[tier] samples), tcap = the tile of the last launch; hist[b] = the poses of launch seq whose window held
+ * more than edge[b-1] and at most edge[b] samples (hist[num_tiers]: more than edge[num_tiers-1]); chunked = its
+ * poses scored in chunks of the tile.  seq numbers the context's launches from 1 (each launch publishes the counts
+ * of the one before it); seq < 1: no counts yet.  Diagnostics only: the results never depend on the tile. */
+#define PCORE_MAX_TILE_TIERS 8
+typedef struct pcore_tile_info {
+    int32_t num_tiers;
+    int32_t tier;
+    int32_t tcap;
+    int32_t seq;
+    int32_t edge[PCORE_MAX_TILE_TIERS];
+    int32_t wgs_per_cu[PCORE_MAX_TILE_TIERS];
+    int32_t hist[PCORE_MAX_TILE_TIERS + 1];
+    int32_t chunked;
+} pcore_tile_info;
+int pcore_get_tile_info(pcore_ctx* ctx, pcore_tile_info* out);
+
 /* GenerateSuccessorStates / GetStateImagesUnifiedGPU host work on the device (search_env.cpp:7056-7254,
  * 1535-1576), for the drop-in recognizer's states:
  *

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "pcore_render",
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
     "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation", "pcore_get_stats",
-    "pcore_count_within", "pcore_state_poses", "pcore_evaluate_select",
+    "pcore_count_within", "pcore_state_poses", "pcore_evaluate_select", "pcore_get_tile_info",
 )
 
 
@@ -56,6 +56,17 @@ class GpuStats(ctypes.Structure):
     """pcore_gpu_stats (include/pcore.h; the reference's gpu_stats, model.h:24-27)."""
     _fields_ = [("icp_runtime", ctypes.c_float), ("peak_memory_usage", ctypes.c_double), ("gicp_ms", ctypes.c_float),
                 ("icp_chunks", ctypes.c_int32)]
+
+
+MAX_TILE_TIERS = 8
+
+
+class TileInfo(ctypes.Structure):
+    """pcore_tile_info (include/pcore.h): the fused window launch's LDS tile and its window histogram."""
+    _fields_ = [("num_tiers", ctypes.c_int32), ("tier", ctypes.c_int32), ("tcap", ctypes.c_int32),
+                ("seq", ctypes.c_int32), ("edge", ctypes.c_int32 * MAX_TILE_TIERS),
+                ("wgs_per_cu", ctypes.c_int32 * MAX_TILE_TIERS), ("hist", ctypes.c_int32 * (MAX_TILE_TIERS + 1)),
+                ("chunked", ctypes.c_int32)]
 
 
 class IcpParams(ctypes.Structure):
@@ -112,6 +123,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
                                      vp, vp, vp, vp, vp, vp]
     L.pcore_render.argtypes = [vp, vp, vp, vp, i32, f32, vp, vp, vp]
     L.pcore_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats), i32]
+    L.pcore_get_tile_info.argtypes = [vp, ctypes.POINTER(TileInfo)]
     L.pcore_depth_to_cloud.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, i32,
                                        ctypes.POINTER(i32), vp]
     L.pcore_select.argtypes = [vp, vp, vp, vp, i32, i64, i32, vp, vp]

@@ -264,6 +264,14 @@ class PoseCore:
         return {"icp_runtime": st.icp_runtime, "peak_memory_usage": st.peak_memory_usage, "gicp_ms": st.gicp_ms,
                 "icp_chunks": st.icp_chunks}
 
+    def tile_info(self) -> dict:
+        """pcore_get_tile_info: the fused window launch's tile tier and the last published window histogram."""
+        ti = _native.TileInfo()
+        self._check(self.lib.pcore_get_tile_info(self._h, ctypes.byref(ti)))
+        n = ti.num_tiers
+        return {"tier": ti.tier, "tcap": ti.tcap, "seq": ti.seq, "edge": list(ti.edge[:n]),
+                "wgs_per_cu": list(ti.wgs_per_cu[:n]), "hist": list(ti.hist[:n + 1]), "chunked": ti.chunked}
+
     def depth_to_cloud(self, depth: torch.Tensor, stride: int, depth_factor: float,
                        label_mask: Optional[torch.Tensor] = None, pose_label: Optional[torch.Tensor] = None,
                        stream=None):

@@ -99,6 +99,10 @@ struct pcore_ctx {
     int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
     long long tile_key = -1;      // ws, hs, bitmap words, colour of the current tile configuration
     int tile_tier = kDefaultTier;
+    int32_t tile_tcap = 0;        // tile (samples) of the last window launch
+    bool tile_probed = false;     // the window probe has chosen a tier for the current tile key
+    DevBuf<int32_t> win_probe;    // its histogram
+    int32_t tile_edge[kTileTiers] = {};
     std::vector<int> obs_order;   // label-sorted position -> caller's observed index
     bool have_obs_colours = false;
     DevBuf<double> metric_part;  // ADD / ADD-S per-block partial sums
@@ -645,9 +649,24 @@ int pcore_set_observation(pcore_ctx* c, const int32_t* d_src_depth_cm, const uin
     return PCORE_OK;
 }
 
-// Tile of the fused window launch ("Pose windows"): the tier with the most workgroups per CU
-// whose tile holds the windows of >= 99 % of the poses of the last finished call with the same sampled
-// image; kDefaultTier until one is known.  Only the speed depends on the choice, never the results.
+// the tier with the most workgroups per CU whose tile holds the windows of >= 99 % of the histogram's poses
+static int choose_tier(const int32_t* h, const int* edge, int fallback) {
+    long long tot = 0;
+    for (int b = 0; b <= kTileTiers; b++) tot += h[b];
+    if (tot <= 0) return fallback;
+    long long over = tot;  // windows above edge[t]
+    for (int t = 0; t < kTileTiers; t++) {
+        over -= h[t];
+        if (edge[t] > 0 && over * 100 <= tot) return t;
+    }
+    return kTileTiers - 1;
+}
+
+// Tile of the fused window launch ("Pose windows"): choose_tier over the window histogram of the
+// last launch that has published one with the same sampled image.  Until one has (the first call with a new
+// image, or every call of a host that runs ahead of the GPU), the tier comes from a window probe of the
+// first such batch: one small launch and a wait, once per sampled image.  Only the speed depends on the choice,
+// never the results.
 static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hipStream_t s) {
     const bool colour = a.cid != nullptr;
     const int nsamp = a.ws * a.hs;
@@ -676,36 +695,41 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hip
     int edge[kTileTiers];
     for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, c->dinfo);
     const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);
+    bool published = false;
     if (key != c->tile_key) {
         c->tile_key = key;
         c->tile_key_seq = c->fb_seq + 1;
         c->tile_tier = kDefaultTier;
+        c->tile_probed = false;
     } else {
         volatile int32_t* fb = c->fb_host;
         const int32_t seq = fb[kTileTiers + 2];
         if (seq >= c->tile_key_seq && seq <= c->fb_seq) {
             int32_t h[kTileTiers + 1];
-            long long tot = 0;
-            for (int b = 0; b <= kTileTiers; b++) tot += (h[b] = fb[b]);
-            if (tot > 0) {
-                int tier = kTileTiers - 1;
-                long long over = tot;  // windows above edge[t]
-                for (int t = 0; t < kTileTiers; t++) {
-                    over -= h[t];
-                    if (edge[t] > 0 && over * 100 <= tot) { tier = t; break; }
-                }
-                c->tile_tier = tier;
-            }
+            for (int b = 0; b <= kTileTiers; b++) h[b] = fb[b];
+            c->tile_tier = choose_tier(h, edge, c->tile_tier);
+            published = true;
         }
     }
-    if (const char* env = getenv("PCORE_FUSED_TIER")) {  // A/B + test knob; >= kTileTiers: whole image
-        c->tile_tier = std::min(std::max(atoi(env), 0), kTileTiers);
+    const char* env_tier = getenv("PCORE_FUSED_TIER");  // A/B + test knob; >= kTileTiers: whole image
+    if (!published && !c->tile_probed && !capturing && !env_tier && !getenv("PCORE_NO_WINDOW_PROBE")) {
+        if ((e = dev_reserve(c->win_probe, kTileTiers + 1)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(c->win_probe.p, 0, (kTileTiers + 1) * sizeof(int32_t), s)) != hipSuccess) return e;
+        for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
+        if ((e = launch_window_probe(a, c->win_probe.p, s)) != hipSuccess) return e;
+        int32_t h[kTileTiers + 1];
+        if ((e = hipMemcpyAsync(h, c->win_probe.p, sizeof(h), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        c->tile_tier = choose_tier(h, edge, c->tile_tier);
+        c->tile_probed = true;
     }
+    if (env_tier) c->tile_tier = std::min(std::max(atoi(env_tier), 0), kTileTiers);
     // tier kTileTiers (A/B knob only): the whole image
     a.tcap = c->tile_tier < kTileTiers && edge[c->tile_tier] > 0 ? edge[c->tile_tier] : nsamp;
     if (const char* env = getenv("PCORE_FUSED_TCAP"))  // test knob: a tile of this many samples (most poses overflow)
         a.tcap = std::min(std::max(atoi(env), 1), nsamp);
-    for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = edge[t];
+    for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = c->tile_edge[t] = edge[t];
+    c->tile_tcap = a.tcap;
     a.fb_ctr = c->fb_ctr.p;
     a.win_hist = c->win_hist.p;
     a.fb_host = capturing ? nullptr : c->fb_dev;
@@ -1083,6 +1107,27 @@ int pcore_get_stats(pcore_ctx* c, pcore_gpu_stats* out, int32_t reset) {
     out->gicp_ms = (float)gicp_ms;
     out->icp_chunks = c->icp_ev_used;
     if (reset) c->peak_mem_mb = 0.0;
+    return PCORE_OK;
+}
+
+int pcore_get_tile_info(pcore_ctx* c, pcore_tile_info* out) {
+    if (!c || !out) return PCORE_E_INVALID_ARG;
+    static_assert(kTileTiers <= PCORE_MAX_TILE_TIERS, "pcore_tile_info holds the tiers");
+    std::memset(out, 0, sizeof(*out));
+    out->num_tiers = kTileTiers;
+    out->tier = c->tile_tier;
+    out->tcap = c->tile_tcap;
+    out->seq = -1;
+    for (int t = 0; t < kTileTiers; t++) {
+        out->edge[t] = c->tile_edge[t];
+        out->wgs_per_cu[t] = tier_wgs(t);
+    }
+    if (c->fb_host) {
+        const volatile int32_t* fb = c->fb_host;
+        for (int b = 0; b <= kTileTiers; b++) out->hist[b] = fb[b];
+        out->chunked = fb[kTileTiers + 1];
+        out->seq = fb[kTileTiers + 2];
+    }
     return PCORE_OK;
 }
 

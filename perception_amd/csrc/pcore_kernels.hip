@@ -1109,6 +1109,34 @@ fused_cost_kernel(FusedArgs a) {
     fused_pose<STRIDE, COLOUR>(a, sm, pose, sw, a.tcap);
 }
 
+// Window probe: the tier histogram of a batch's pose windows, for the tile choice of a context that has no
+// published feedback yet (set_fused_tiles).  One wave per pose (pose_window's corner lanes), nothing else.
+__global__ void __launch_bounds__(kThreads) window_probe_kernel(FusedArgs a, int32_t* hist) {
+    const int pose = blockIdx.x * (kThreads / kWave) + (int)(threadIdx.x / kWave);
+    if (pose >= a.num_poses) return;  // wave-uniform
+    const int model = a.pose_model[pose];
+    int tn = 0;
+    if (model >= 0 && model < a.num_models) {
+        float m[12];
+        load_pose_rows(a.poses, pose, m);
+        const SampleWin w = pose_window(a, model, m, a.stride);
+        tn = w.nx * w.ny;
+    }
+    if (lane_id() == 0) {
+        int b = 0;
+#pragma unroll
+        for (int t = 0; t < kTileTiers; t++) b += tn > a.hist_edge[t] ? 1 : 0;
+        atomicAdd(&hist[b], 1);
+    }
+}
+
+hipError_t launch_window_probe(const FusedArgs& a, int32_t* hist, hipStream_t s) {
+    if (a.num_poses <= 0) return hipSuccess;
+    const int per_wg = kThreads / kWave;
+    hipLaunchKernelGGL(window_probe_kernel, dim3((a.num_poses + per_wg - 1) / per_wg), dim3(kThreads), 0, s, a, hist);
+    return hipGetLastError();
+}
+
 // Stage CLOUD into per-pose scratch slots (the GICP source clouds): sampled raster, source occlusion,
 // then the reference's compaction order (row-major samples, compute_point_clouds.cuh:290-346).
 template <int STRIDE>

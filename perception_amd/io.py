@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import time
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -210,21 +211,57 @@ def _parse_poses_text(text: str) -> np.ndarray:
     return np.asarray(rows, np.float64).reshape(-1, 7)
 
 
+try:
+    import xxhash as _xxhash
+
+    def _content_digest(data: bytes) -> bytes:
+        return _xxhash.xxh3_128_digest(data)
+except ImportError:  # pragma: no cover - xxhash ships with the image
+    def _content_digest(data: bytes) -> bytes:
+        return hashlib.blake2b(data, digest_size=16).digest()
+
+
 _POSES_CACHE: "OrderedDict[tuple, np.ndarray]" = OrderedDict()
 _POSES_CACHE_MAX = 64
+_POSES_STAT: "OrderedDict[str, tuple]" = OrderedDict()  # abspath -> (stat signature, content digest)
+_SETTLED_NS = 2_000_000_000
+
+
+def _stat_signature(st: os.stat_result) -> tuple:
+    return st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns
 
 
 def read_poses_txt_cached(path: str, use_cache: bool = True) -> np.ndarray:
-    """read_poses_txt, parsed once per file CONTENT: keyed by (path, BLAKE2b digest of the bytes), so a poses.txt
-    rewritten in place -- whatever its size and timestamps -- is parsed again, and an unchanged one is only read and
-    hashed (the reference re-reads and re-parses it every GenerateSuccessorStates; the content, and so the result, is
-    the same).  Least-recently-used eviction past 64 files.  use_cache=False (or PCORE_POSES_CACHE=0) parses
-    every time.  Returns a read-only array."""
+    """read_poses_txt, parsed once per file CONTENT: keyed by (path, 128-bit digest of the bytes), so a poses.txt
+    rewritten in place -- whatever its size and timestamps -- is parsed again (the reference re-reads and re-parses it
+    every GenerateSuccessorStates; the content, and so the result, is the same).  The digest is XXH3-128 (BLAKE2b
+    when xxhash is not importable; BLAKE2b took 1.3-4.7 ms per 10k-pose file).
+
+    A file whose status change time was already 2 s old when it was read is not read again while its (device,
+    inode, size, mtime, ctime) stay the same: any write after that read sets ctime to the current time, which no
+    utime call can set back, so an unchanged signature means unchanged bytes.  A file changed within the last 2 s
+    (the kernel's timestamp clock is coarse) is read and hashed every time.  Least-recently-used eviction past 64
+    files.  use_cache=False (or PCORE_POSES_CACHE=0) parses every time.  Returns a read-only array."""
     if not use_cache or os.environ.get("PCORE_POSES_CACHE", "1") == "0":
         return read_poses_txt(path)
-    with open(path, "rb") as f:
+    apath = os.path.abspath(path)
+    sig = _stat_signature(os.stat(apath))
+    known = _POSES_STAT.get(apath)
+    if known is not None and known[0] == sig and (apath, known[1]) in _POSES_CACHE:
+        key = (apath, known[1])
+        _POSES_CACHE.move_to_end(key)
+        _POSES_STAT.move_to_end(apath)
+        return _POSES_CACHE[key]
+    with open(apath, "rb") as f:
+        sig_open = _stat_signature(os.fstat(f.fileno()))
         data = f.read()
-    key = (os.path.abspath(path), hashlib.blake2b(data, digest_size=16).digest())
+        sig_read = _stat_signature(os.fstat(f.fileno()))
+    key = (apath, _content_digest(data))
+    _POSES_STAT.pop(apath, None)
+    if sig_open == sig_read and time.time_ns() - sig_read[4] > _SETTLED_NS:
+        _POSES_STAT[apath] = (sig_read, key[1])
+        while len(_POSES_STAT) > _POSES_CACHE_MAX:
+            _POSES_STAT.popitem(last=False)
     hit = _POSES_CACHE.get(key)
     if hit is None:
         hit = _parse_poses_text(data.decode())

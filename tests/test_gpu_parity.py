@@ -237,10 +237,57 @@ def test_window_tiles_any_tier(one_object, tier, monkeypatch):
     assert np.array_equal(dbg.cpu().numpy(), full[:, ::s, ::s])
 
 
+def _choose_tier(hist, edge):
+    """set_fused_tiles' choose_tier (pcore_api.hip): the first tier whose tile holds >= 99 % of the windows."""
+    tot = sum(hist)
+    over = tot
+    for t, e in enumerate(edge):
+        over -= hist[t]
+        if e > 0 and over * 100 <= tot:
+            return t
+    return len(edge) - 1
+
+
+def test_window_probe_picks_the_feedback_tier_on_the_first_call():
+    """A fresh context has no published window histogram: its first call probes the batch's windows and starts from
+    the tier that the launch's own histogram picks once published (a host running ahead of the GPU never waits for
+    that feedback).  Poses pulled to half their distance (4x the window) need a tile above tier 0's; the costs are
+    the oracle's whatever the tier."""
+    case = SceneCase(("003_cracker_box",), n_poses=64)
+    core, t = _setup(case)
+    sc = case.scene
+    s = case.stride
+    near = case.poses.copy()
+    near[:, [3, 7, 11]] *= np.float32(0.5)
+    n = len(near)
+    dev = t["poses"].device
+    poses = torch.from_numpy(near).to(dev)
+    pm = torch.zeros(n, dtype=torch.int32, device=dev)
+    pl = torch.zeros(n, dtype=torch.int32, device=dev)
+    tot = torch.full((n,), float(case.pose_obs_total[0]), device=dev)
+    assert core.tile_info()["seq"] == -1
+    rc, oc, df = core.evaluate(poses, pm, pl, tot, cost_type=2, stride=s)
+    torch.cuda.synchronize()
+    first = core.tile_info()
+    assert first["seq"] < 1 and first["tcap"] == first["edge"][first["tier"]]  # launch 1 publishes no launch's counts
+    core.evaluate(poses, pm, pl, tot, cost_type=2, stride=s)  # its workgroup 0 publishes the first launch's counts
+    torch.cuda.synchronize()
+    fb = core.tile_info()
+    assert fb["seq"] >= 0 and sum(fb["hist"]) == n
+    assert _choose_tier(fb["hist"], fb["edge"]) == first["tier"] >= 1
+    orc, ooc, odf = oracle.evaluate(sc.bank.tris, sc.bank.tris_model_count, near, np.zeros(n, np.int32),
+                                    np.zeros(n, np.int32), sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask,
+                                    1.0, s, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz, case.label_start,
+                                    case.label_end, np.full(n, case.pose_obs_total[0], np.float32), 2, True, 0.01)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+
+
 def test_graph_replay_matches_oracle(one_object):
     """PoseCore.capture_evaluate: the captured window launch (HIP graph) re-scores new poses written in place into
-    the captured tensor, with the oracle's costs, replay after replay (the launch's feedback counters return to 0
-    inside the graph)."""
+    the captured tensor, with the oracle's costs, replay after replay (a captured launch publishes no tier feedback;
+    the next eager call clears the counters it left)."""
     case, core, t = one_object
     sc = case.scene
     s = case.stride

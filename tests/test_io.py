@@ -152,3 +152,28 @@ def test_read_poses_txt_cached_same_size_same_mtime_rewrite(tmp_path):
         pio.write_poses_txt(q, rows * (i + 1))
         pio.read_poses_txt_cached(q)
     assert len(pio._POSES_CACHE) <= pio._POSES_CACHE_MAX
+
+
+def test_read_poses_txt_cached_settled_file_skips_the_read(tmp_path, monkeypatch):
+    """A file whose ctime was settled when it was read is served from its stat signature without reading the bytes
+    again; rewriting it afterwards (same size, mtime put back) changes ctime, and the new content is parsed."""
+    from perception_amd import io as pio
+    import os
+    import time
+    p = str(tmp_path / "poses.txt")
+    rows = np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]])
+    pio.write_poses_txt(p, rows)
+    st = os.stat(p)
+    real_ns = time.time_ns
+    monkeypatch.setattr(pio.time, "time_ns", lambda: real_ns() + 10 * pio._SETTLED_NS)  # pretend the file is old
+    a = pio.read_poses_txt_cached(p)
+    digests = []
+    monkeypatch.setattr(pio, "_content_digest", lambda d: digests.append(1) or b"x" * 16)
+    assert pio.read_poses_txt_cached(p) is a and not digests  # stat hit: nothing read or hashed
+    time.sleep(0.05)  # past the coarse timestamp clock's tick
+    pio.write_poses_txt(p, rows[:, [1, 0, 2, 3, 4, 5, 6]])
+    os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert os.stat(p).st_ctime_ns != st.st_ctime_ns
+    monkeypatch.undo()
+    b = pio.read_poses_txt_cached(p)
+    assert b[0, 0] == 0.2 and a[0, 0] == 0.1
