@@ -341,6 +341,8 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
     streams::Built sb;
     int chunks = kStreamChunks;
     if (const char* e = getenv("PCORE_STREAM_CHUNKS")) chunks = std::max(1, atoi(e));  // A/B knob
+    int model_streams = kFusedWaves;
+    if (const char* e = getenv("PCORE_MODEL_STREAMS")) model_streams = std::max(1, atoi(e));  // A/B knob
     std::vector<float4> box;
     std::vector<int32_t> slo(num_models), shi(num_models), tlo(num_models), thi(num_models);
     int t0 = 0;
@@ -385,7 +387,7 @@ int pcore_upload_meshes(pcore_ctx* c, const float* tri_xyz, const uint8_t* tri_r
         box.push_back(bmin);
         box.push_back(bmax);
         slo[m] = (int)sb.streams.size();
-        streams::build_model(tv, vxyz, t0, kFusedWaves, kVRing, kRefPasses, sb, chunks);
+        streams::build_model(tv, vxyz, t0, model_streams, kVRing, kRefPasses, sb, chunks);
         shi[m] = (int)sb.streams.size();
         t0 += T;
     }

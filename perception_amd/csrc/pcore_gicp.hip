@@ -505,30 +505,66 @@ __device__ __forceinline__ float uniform_f(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, x)));
 }
 
-// The wave shuffle-down tree through LDS, a transposed layout instead of 6 x 28 ds_bpermute rounds: every lane
-// stores its partial sums (14 values, then the other 14), lane k adds up value k's 64 entries in the tree's own
-// order -- node(l, off) = node(l, 2 off) + node(l + off, 2 off), leaves node(l, 64) = lane l's entry, so lane 0's
-// level-by-level sums ((x0 + x32) + (x16 + x48)) + ... come out bit-identical -- and the 28 sums land in
-// red[kRedHalf * 64 ...], where every lane reads them.  ~7.4 KB of LDS per wave.
-constexpr int kRedHalf = gicpm::kTerms / 2;
-constexpr int kRedDoubles = kRedHalf * 64 + gicpm::kTerms;
-template <int L, int OFF, int NV>
-__device__ __forceinline__ double tree_node(const double* col) {
-    if constexpr (OFF == 64) return col[L * NV];
-    else return tree_node<L, 2 * OFF, NV>(col) + tree_node<L + OFF, 2 * OFF, NV>(col);
+// The wave shuffle-down tree of the 28 normal-equation sums (the oracle's order: node(l, off) = node(l, 2 off) +
+// node(l + off, 2 off) for off = 32 ... 1, node(l, 64) = lane l's entry, so lane 0's sums ((x0 + x32) + (x16 + x48))
+// + ... ), computed in registers with the values split between the halves at every level: at offset o the lanes of
+// each 2o-block pair two registers A, B; the lower half adds its partner's A and keeps value A, the upper half adds
+// its partner's B and keeps value B.  Lane l then holds node(l mod o, o) of half as many values, so the wave does
+// 16 + 8 + 4 + 2 + 1 + 1 adds instead of 28 x 6.  The sums are the tree's own (IEEE addition commutes), whichever lane
+// forms them: value v ends on lane 2 v.  Offsets 32 and 16 swap halves with v_permlane32_swap / v_permlane16_swap,
+// 8 and 4 use DPP row shifts written bank by bank, 2 and 1 quad permutations.  (Round 3 transposed the partial sums
+// through 7.4 KB of LDS per wave and summed them on 14 lanes: 5.6 k of ~36 k clocks per pose-iteration.)
+template <int CTRL, int ROWS, int BANKS>
+__device__ __forceinline__ double dpp_d(double old, double src) {
+    const unsigned long long o = __builtin_bit_cast(unsigned long long, old);
+    const unsigned long long v = __builtin_bit_cast(unsigned long long, src);
+    const unsigned lo = __builtin_amdgcn_update_dpp((unsigned)o, (unsigned)v, CTRL, ROWS, BANKS, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp((unsigned)(o >> 32), (unsigned)(v >> 32), CTRL, ROWS, BANKS, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ const double* lds_tree_sum(const double (&acc)[gicpm::kTerms], double* red, int lane) {
-    constexpr int NA = kRedHalf, NB = gicpm::kTerms - kRedHalf;
-    double* out = red + kRedHalf * 64;
+template <bool ROWS16>
+__device__ __forceinline__ double swap_add(double a, double b) {  // offsets 32 (ROWS16 false) and 16
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a);
+    const unsigned long long ub = __builtin_bit_cast(unsigned long long, b);
+    unsigned alo = (unsigned)ua, ahi = (unsigned)(ua >> 32), blo = (unsigned)ub, bhi = (unsigned)(ub >> 32);
+    if constexpr (ROWS16) {
+        const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+        alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+    } else {
+        const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+        alo = l[0]; blo = l[1]; ahi = h[0]; bhi = h[1];
+    }
+    return __builtin_bit_cast(double, ((unsigned long long)ahi << 32) | alo) +
+           __builtin_bit_cast(double, ((unsigned long long)bhi << 32) | blo);
+}
+template <int OFF>
+__device__ __forceinline__ double bank_add(double a, double b) {  // offsets 8 (banks 0-1 | 2-3) and 4 (0, 2 | 1, 3)
+    constexpr int LOW = OFF == 8 ? 0x3 : 0x5;
+    const double t = dpp_d<0x110 + OFF, 0xf, 0xf ^ LOW>(dpp_d<0x100 + OFF, 0xf, LOW>(0.0, a), b);  // row_shl / row_shr
+    const double u = dpp_d<0xE4, 0xf, 0xf ^ LOW>(a, b);                                            // own value
+    return u + t;
+}
+__device__ __forceinline__ const double* wave_tree_sums(const double (&acc)[gicpm::kTerms], double* out, int lane) {
+    constexpr int K = gicpm::kTerms;
+    static_assert(K > 16 && K <= 32, "28 sums: 16 register pairs at offset 32");
+    double r[16];
 #pragma unroll
-    for (int v = 0; v < NA; v++) red[lane * NA + v] = acc[v];
-    wave_lds_sync();
-    if (lane < NA) out[lane] = tree_node<0, 1, NA>(red + lane);
-    wave_lds_sync();
+    for (int k = 0; k < 16; k++) r[k] = swap_add<false>(acc[k], k + 16 < K ? acc[k + 16] : 0.0);
 #pragma unroll
-    for (int v = 0; v < NB; v++) red[lane * NB + v] = acc[NA + v];
-    wave_lds_sync();
-    if (lane < NB) out[NA + lane] = tree_node<0, 1, NB>(red + lane);
+    for (int k = 0; k < 8; k++) r[k] = swap_add<true>(r[k], r[k + 8]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] = bank_add<8>(r[k], r[k + 4]);
+#pragma unroll
+    for (int k = 0; k < 2; k++) r[k] = bank_add<4>(r[k], r[k + 2]);
+    {  // offset 2: lanes 0-1 of a quad keep r0, lanes 2-3 r1
+        const bool up = lane & 2;
+        const double sel = up ? r[0] : r[1], own = up ? r[1] : r[0];
+        r[0] = own + dpp_d<0x4E, 0xf, 0xf>(0.0, sel);  // quad_perm [2, 3, 0, 1]
+    }
+    r[0] = r[0] + dpp_d<0xB1, 0xf, 0xf>(0.0, r[0]);    // offset 1: quad_perm [1, 0, 3, 2]
+    if (!(lane & 1) && (lane >> 1) < K) out[lane >> 1] = r[0];
     wave_lds_sync();
     return out;
 }
@@ -813,7 +849,7 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
 gicp_kernel(GicpArgs g, int num_poses) {
-    __shared__ double sRed[kRedDoubles];
+    __shared__ double sRed[gicpm::kTerms];
     __shared__ double2 sM0[3][64];
     __shared__ float4 sS0[64], sT0[64];
     __shared__ int sPose;
@@ -887,7 +923,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
                     linearize_round<true>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
                                           P.tquads, P.nt, -1, cset, P.mah, r0, acc, !reuse GPROF_ARG);
                 GPROF_T(t_b);
-                const double* sys = lds_tree_sum(acc, sRed, lane);
+                const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
                 const int st = lm_iteration(sys, x, lambda, P.src, cset, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
                                             g.trans_eps GPROF_ARG);
@@ -912,7 +948,7 @@ template <int WPP>
 __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num_poses) {
     constexpr int NT = 64 * WPP;
     extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
-    __shared__ double sRed[kRedDoubles];
+    __shared__ double sRed[gicpm::kTerms];
     __shared__ double2 sM0[3][64];
     __shared__ float4 sS0[64], sT0[64];
     __shared__ double sX[12];
@@ -971,7 +1007,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                                            P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, r0, acc, false GPROF_ARG);
                 }
                 GPROF_TD(t_w2, acc[0]);
-                const double* sys = lds_tree_sum(acc, sRed, lane);
+                const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_w3, sys[0]);
                 const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
                                             g.trans_eps GPROF_ARG);

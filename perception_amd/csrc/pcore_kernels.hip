@@ -1110,30 +1110,46 @@ fused_cost_kernel(FusedArgs a) {
 }
 
 // Window probe: the tier histogram of a batch's pose windows, for the tile choice of a context that has no
-// published feedback yet (set_fused_tiles).  One wave per pose (pose_window's corner lanes), nothing else.
+// published feedback yet (set_fused_tiles).  One wave per pose at a time (pose_window's corner lanes), poses strided
+// over a bounded grid; waves count in registers, workgroups in LDS, and each workgroup adds its bins once (one
+// address per bin: a per-pose atomic serialised, 270 us for 50 k poses).
+constexpr int kProbeBlocks = 2048;
 __global__ void __launch_bounds__(kThreads) window_probe_kernel(FusedArgs a, int32_t* hist) {
-    const int pose = blockIdx.x * (kThreads / kWave) + (int)(threadIdx.x / kWave);
-    if (pose >= a.num_poses) return;  // wave-uniform
-    const int model = a.pose_model[pose];
-    int tn = 0;
-    if (model >= 0 && model < a.num_models) {
-        float m[12];
-        load_pose_rows(a.poses, pose, m);
-        const SampleWin w = pose_window(a, model, m, a.stride);
-        tn = w.nx * w.ny;
-    }
-    if (lane_id() == 0) {
+    constexpr int kWaves = kThreads / kWave;
+    int cnt[kTileTiers + 1] = {};
+    for (int pose = blockIdx.x * kWaves + (int)(threadIdx.x / kWave); pose < a.num_poses;
+         pose += gridDim.x * kWaves) {  // wave-uniform
+        const int model = a.pose_model[pose];
+        int tn = 0;
+        if (model >= 0 && model < a.num_models) {
+            float m[12];
+            load_pose_rows(a.poses, pose, m);
+            const SampleWin w = pose_window(a, model, m, a.stride);
+            tn = w.nx * w.ny;
+        }
         int b = 0;
 #pragma unroll
         for (int t = 0; t < kTileTiers; t++) b += tn > a.hist_edge[t] ? 1 : 0;
-        atomicAdd(&hist[b], 1);
+#pragma unroll
+        for (int k = 0; k <= kTileTiers; k++) cnt[k] += b == k ? 1 : 0;
     }
+    __shared__ int32_t wg_cnt[kTileTiers + 1];
+    if (threadIdx.x <= kTileTiers) wg_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k <= kTileTiers; k++)
+            if (cnt[k]) atomicAdd(&wg_cnt[k], cnt[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x <= kTileTiers && wg_cnt[threadIdx.x]) atomicAdd(&hist[threadIdx.x], wg_cnt[threadIdx.x]);
 }
 
 hipError_t launch_window_probe(const FusedArgs& a, int32_t* hist, hipStream_t s) {
     if (a.num_poses <= 0) return hipSuccess;
     const int per_wg = kThreads / kWave;
-    hipLaunchKernelGGL(window_probe_kernel, dim3((a.num_poses + per_wg - 1) / per_wg), dim3(kThreads), 0, s, a, hist);
+    const int blocks = std::min(kProbeBlocks, (a.num_poses + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL(window_probe_kernel, dim3(blocks), dim3(kThreads), 0, s, a, hist);
     return hipGetLastError();
 }
 
