@@ -221,6 +221,11 @@ typedef struct pcore_tile_info {
 } pcore_tile_info;
 int pcore_get_tile_info(pcore_ctx* ctx, pcore_tile_info* out);
 
+/* Test hook (no reference counterpart): the GICP kernels' damped LM solve (H + lambda I) d = -b of n raw 28-term
+ * systems (upper H row-major, b, error; d_sys n x 28, d_lambda n, d_out n x 6 doubles), one wave each, for the
+ * parity test against the oracle's restatement of Eigen's pivoted LDLT. */
+int pcore_debug_lm_solve(const double* d_sys, const double* d_lambda, double* d_out, int32_t n, pcore_stream stream);
+
 /* GenerateSuccessorStates / GetStateImagesUnifiedGPU host work on the device (search_env.cpp:7056-7254,
  * 1535-1576), for the drop-in recognizer's states:
  *

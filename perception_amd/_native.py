@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "pcore_render",
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
     "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation", "pcore_get_stats",
-    "pcore_count_within", "pcore_state_poses", "pcore_evaluate_select", "pcore_get_tile_info",
+    "pcore_count_within", "pcore_state_poses", "pcore_evaluate_select", "pcore_get_tile_info", "pcore_debug_lm_solve",
 )
 
 
@@ -123,7 +123,10 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
                                      vp, vp, vp, vp, vp, vp]
     L.pcore_render.argtypes = [vp, vp, vp, vp, i32, f32, vp, vp, vp]
     L.pcore_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats), i32]
-    L.pcore_get_tile_info.argtypes = [vp, ctypes.POINTER(TileInfo)]
+    if hasattr(L, "pcore_get_tile_info"):  # diagnostics / test hooks: absent from older A/B builds (PCORE_LIB)
+        L.pcore_get_tile_info.argtypes = [vp, ctypes.POINTER(TileInfo)]
+    if hasattr(L, "pcore_debug_lm_solve"):
+        L.pcore_debug_lm_solve.argtypes = [vp, vp, vp, i32, vp]
     L.pcore_depth_to_cloud.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, i32,
                                        ctypes.POINTER(i32), vp]
     L.pcore_select.argtypes = [vp, vp, vp, vp, i32, i64, i32, vp, vp]
@@ -137,7 +140,7 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
     L.pcore_count_within.argtypes = [vp, vp, vp, vp, i32, vp, vp]
     L.pcore_state_poses.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_double), vp, i32, i32, vp, vp]
     for name in EXPORTED_SYMBOLS:
-        if name not in ("pcore_destroy", "pcore_last_error", "pcore_generation"):
+        if name not in ("pcore_destroy", "pcore_last_error", "pcore_generation") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
     L.pcore_generation.restype = ctypes.c_uint64
     _lib = L

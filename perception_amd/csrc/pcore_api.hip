@@ -1133,6 +1133,11 @@ int pcore_get_tile_info(pcore_ctx* c, pcore_tile_info* out) {
     return PCORE_OK;
 }
 
+int pcore_debug_lm_solve(const double* d_sys, const double* d_lambda, double* d_out, int32_t n, pcore_stream stream) {
+    if (n < 0 || (n > 0 && (!d_sys || !d_lambda || !d_out))) return PCORE_E_INVALID_ARG;
+    return launch_lm_solve_test(d_sys, d_lambda, d_out, n, (hipStream_t)stream) == hipSuccess ? PCORE_OK : PCORE_E_HIP;
+}
+
 int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,
                          int32_t stride, float depth_factor, const uint8_t* d_label_mask, const int32_t* d_pose_label,
                          float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label, int32_t cap, int32_t* out_count,

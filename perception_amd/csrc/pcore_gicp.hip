@@ -706,7 +706,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
     for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
         GPROF_T(p0);
         double d[6];
-        gicpm::lm_solve(sys, lambda, d);
+        gicpm::lm_solve_rows(sys, lambda, d);
 #pragma unroll
         for (int a = 0; a < 6; a++) d[a] = uniform_d(d[a]);
         GPROF_TD(p1, d[5]);
@@ -1053,6 +1053,22 @@ extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
     return e == hipSuccess ? 0 : 1;
 }
 #endif
+
+// Test hook of the kernels' damped solve (gicpm::lm_solve_rows): one wave per 28-term system.
+__global__ void __launch_bounds__(64) lm_solve_test_kernel(const double* sys, const double* lambda, double* out, int n) {
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    double d[6];
+    gicpm::lm_solve_rows(sys + (size_t)gicpm::kTerms * i, lambda[i], d);
+    if (threadIdx.x == 0)
+        for (int a = 0; a < 6; a++) out[(size_t)6 * i + a] = d[a];
+}
+
+hipError_t launch_lm_solve_test(const double* sys, const double* lambda, double* out, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lm_solve_test_kernel, dim3(n), dim3(64), 0, s, sys, lambda, out, n);
+    return hipGetLastError();
+}
 
 // predicted cost of one GICP iteration of a pose: source points x targets of its segment (the scan)
 __global__ void gicp_cost_key_kernel(GicpArgs g, int n, uint32_t* keys, int32_t* idx) {

@@ -528,6 +528,129 @@ PCORE_UNROLL
     }
 }
 
+#if PCORE_LANE_PAR
+// lm_solve with row i of the permuted system on lane i (device only; lanes 6-63 shadow row 5 and are ignored).  Every
+// entry sees the operations of lm_solve in the same order -- row k's L entries and the diagonal D come to every lane by
+// v_readlane where another row needs them, a row's updates run on its own lane instead of on every lane in turn, and
+// each column's divisions are one division sequence -- so the result is lm_solve's bit for bit (the uniform d on every
+// lane).  tests/test_gpu_gicp_solve.py holds it to the oracle's lm_solve on random, tied, zero and non-finite systems.
+__device__ __forceinline__ double read_lane_k(double v, int k) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, k);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), k);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ void lm_solve_rows(const double* sys, double lambda, double (&d)[6]) {
+    const int lane = lane_index();
+    const int r = lane < 6 ? lane : 5;
+    int perm[6];
+    {
+        double mag[6];
+PCORE_UNROLL
+        for (int a = 0; a < 6; a++) {
+            mag[a] = __builtin_fabs(sys[hdiag(a)] + lambda);
+            perm[a] = a;
+        }
+PCORE_UNROLL
+        for (int k = 0; k < 5; k++) {
+            int p = k;
+            double big = mag[k];
+PCORE_UNROLL
+            for (int i = k + 1; i < 6; i++) {
+                const double v = mag[i];
+                if (v > big) { big = v; p = i; }
+            }
+            p = uniform_i(p);
+PCORE_UNROLL
+            for (int c = k + 1; c < 6; c++)
+                if (p == c) {
+                    const double m = mag[k]; mag[k] = mag[c]; mag[c] = m;
+                    const int q = perm[k]; perm[k] = perm[c]; perm[c] = q;
+                }
+        }
+    }
+    int pr = perm[0];
+PCORE_UNROLL
+    for (int i = 1; i < 6; i++) pr = r == i ? perm[i] : pr;
+    // this lane's row of the permuted lower triangle (entries past the diagonal are never read)
+    double A[6];
+PCORE_UNROLL
+    for (int j = 0; j < 6; j++) {
+        const double v = sys[hidx(pr, perm[j])];
+        A[j] = j == r ? v + lambda : v;
+    }
+    double D[6];  // the factored diagonal, uniform
+    bool zero = false;
+PCORE_UNROLL
+    for (int k = 0; k < 6; k++) {
+        double akk;
+        if (k > 0) {
+            double temp[6];
+PCORE_UNROLL
+            for (int j = 0; j < k; j++) temp[j] = D[j] * read_lane_k(A[j], k);
+            // row k's diagonal (uniform) ...
+            double s = read_lane_k(A[0], k) * temp[0];
+PCORE_UNROLL
+            for (int j = 1; j < k; j++) s = s + read_lane_k(A[j], k) * temp[j];
+            akk = read_lane_k(A[k], k) - s;
+            // ... and the rows below it, each on its lane
+            double w = A[0] * temp[0];
+PCORE_UNROLL
+            for (int j = 1; j < k; j++) w = w + A[j] * temp[j];
+            A[k] = r > k ? A[k] - w : (r == k ? akk : A[k]);
+        } else {
+            akk = read_lane_k(A[0], 0);
+        }
+        D[k] = akk;
+        const bool valid = uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0;
+        if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
+            zero = true;
+            break;
+        }
+        if (valid && k < 5) {
+            const double q = A[k] / akk;
+            A[k] = r > k ? q : A[k];
+        }
+    }
+    if (zero) {
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) d[i] = 0.0;
+        return;
+    }
+    double x = -sys[21 + pr];  // P (-b), this lane's entry
+PCORE_UNROLL
+    for (int j = 0; j < 5; j++) {
+        const double xj = read_lane_k(x, j);
+        if (r > j) x = x - xj * A[j];
+    }
+    {
+        const double Di = A[r];  // lane r's diagonal entry
+        x = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x / Di : 0.0;
+    }
+    double xs[6];
+    xs[5] = read_lane_k(x, 5);
+PCORE_UNROLL
+    for (int i = 4; i >= 0; i--) {
+        const double p = A[i] * x;  // lane j > i: A[j][i] x[j]
+        double s = read_lane_k(p, i + 1);
+PCORE_UNROLL
+        for (int j = i + 2; j < 6; j++) s = s + read_lane_k(p, j);
+        xs[i] = read_lane_k(x, i) - s;
+        if (r == i) x = xs[i];
+    }
+PCORE_UNROLL
+    for (int a = 0; a < 6; a++) {
+        double v = xs[0];
+PCORE_UNROLL
+        for (int i = 1; i < 6; i++) v = perm[i] == a ? xs[i] : v;
+        d[a] = v;
+    }
+}
+#else
+// host pass / plain C++ (the oracle): the scalar solve it restates
+PCORE_GHD void lm_solve_rows(const double* sys, double lambda, double (&d)[6]) { lm_solve<false>(sys, lambda, d); }
+#endif
+
 // se3_exp (fast_gicp so3.hpp): so3_exp quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
 // cos(theta/2)), Eigen's Quaternion::toRotationMatrix, translation V rho with
 // V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10)

@@ -234,6 +234,8 @@ size_t fused_lds_bytes(int tile_samples, int bitmap_words, bool colour = false);
 int fused_tier_samples(int t, int ws, int hs, int bitmap_words, bool colour, const DeviceInfo& d);
 // the tier histogram (a.hist_edge) of a batch's pose windows into hist[0..kTileTiers] (added to)
 hipError_t launch_window_probe(const FusedArgs& a, int32_t* hist, hipStream_t s);
+// test hook: gicpm::lm_solve_rows of n raw 28-term systems, one wave each (pcore_debug_lm_solve)
+hipError_t launch_lm_solve_test(const double* sys, const double* lambda, double* out, int n, hipStream_t s);
 hipError_t launch_render_full(const float* tris, int num_tris, const int32_t* tri_lo, const int32_t* tri_hi,
                               const float* poses, const int32_t* pose_model, int num_poses, int width, int height,
                               const float* proj, int32_t* depth, hipStream_t s);

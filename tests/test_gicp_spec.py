@@ -286,10 +286,9 @@ def test_gicp_whole_scene_targets_independent_chain():
     assert max(iters) == 150
 
 
-def test_lm_solve_pivot_order_first_equals_eigen_swaps():
-    """The kernels' LDLT (pivot sequence found first as a selection on |diag|, then the permuted matrix factored
-    without swaps) is bit-identical to the restatement of Eigen's in-place LDLT with its row / column swaps, on random
-    SPD and indefinite systems, tied and zero diagonals, a zero system, huge / tiny scales and non-finite entries."""
+def lm_solve_cases():
+    """Random SPD and indefinite 28-term systems, tied and zero diagonals, a zero system, huge / tiny scales and
+    non-finite entries, with their damping: (sys, lambda) pairs (also the GPU solve's test cases)."""
     rng = np.random.default_rng(31)
     iu = np.triu_indices(6)
     cases = []
@@ -315,6 +314,14 @@ def test_lm_solve_pivot_order_first_equals_eigen_swaps():
             sysb = cases[5][0].copy()
             sysb[pos] = bad
             cases.append((sysb, 1e-9))
+    return cases
+
+
+def test_lm_solve_pivot_order_first_equals_eigen_swaps():
+    """The kernels' LDLT (pivot sequence found first as a selection on |diag|, then the permuted matrix factored
+    without swaps) is bit-identical to the restatement of Eigen's in-place LDLT with its row / column swaps, on random
+    SPD and indefinite systems, tied and zero diagonals, a zero system, huge / tiny scales and non-finite entries."""
+    cases = lm_solve_cases()
     for sysv, lam in cases:
         a = oracle.gicp_lm_solve_sys(sysv, lam)
         b = oracle.gicp_lm_solve_sys(sysv, lam, swaps=True)
