@@ -292,6 +292,29 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
 #pragma unroll
         for (int q = 0; q < KMAX; q++) { nd[q] = 0.0f; nb[q] = 0; }
         int cnt = 0;
+        // the list holds a NaN distance (a non-finite point among the first k candidates): it is no longer sorted,
+        // and only the counting insertion below reproduces orc knn_self's placement
+        bool nan_list = false;
+        // insertion identical to orc knn_self: the new element starts at pos and bubbles down past entries with a
+        // strictly larger distance
+        auto insert_counting = [&](float d, int j) {
+            int pos;
+            if (cnt < k) pos = cnt;
+            else if (d < nd[k - 1]) pos = k - 1;
+            else return;
+            int c = 0;
+#pragma unroll
+            for (int q = 0; q < KMAX; q++) c += (q < pos && nd[q] > d) ? 1 : 0;
+            const int fin = pos - c;
+#pragma unroll
+            for (int q = KMAX - 1; q >= 1; q--)
+                if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
+#pragma unroll
+            for (int q = 0; q < KMAX; q++)
+                if (q == fin) { nd[q] = d; nb[q] = j; }
+            if (cnt < k) cnt++;
+            nan_list = nan_list || d != d;
+        };
         for (int j0 = 0; j0 < n; j0 += kCovLanes) {
             wave_lds_sync();  // the previous tile is read
             if (j0 + lane < n) tile[lane] = P[j0 + lane];
@@ -301,23 +324,29 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
                 const float4 xj = tile[jj];
                 const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
                 const int j = j0 + jj;
-                // insertion identical to orc knn_self: new element starts at pos and bubbles down past
-                // entries with a strictly larger distance
-                int pos;
-                if (cnt < k) pos = cnt;
-                else if (d < nd[k - 1]) pos = k - 1;
-                else continue;
-                int c = 0;
+                if (cnt < k || nan_list) {  // the first k candidates (every lane at once), or a NaN list
+                    insert_counting(d, j);
+                } else if (d < nd[k - 1]) {
+                    // a full, sorted list (no NaN: one could only enter among the first k): the counting insertion's
+                    // result in one pass -- entry q moves right where nd[q] > d, and the first such entry's slot
+                    // takes the new element (d < nd[k - 1], so there is one)
+                    bool gp = false;  // (old) nd[q - 1] > d
+                    float pd = d;     // old nd[q - 1], nb[q - 1]
+                    int pb = j;
 #pragma unroll
-                for (int q = 0; q < KMAX; q++) c += (q < pos && nd[q] > d) ? 1 : 0;
-                const int fin = pos - c;
-#pragma unroll
-                for (int q = KMAX - 1; q >= 1; q--)
-                    if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
-#pragma unroll
-                for (int q = 0; q < KMAX; q++)
-                    if (q == fin) { nd[q] = d; nb[q] = j; }
-                if (cnt < k) cnt++;
+                    for (int q = 0; q < KMAX; q++) {
+                        if (q < k) {
+                            const float od = nd[q];
+                            const int ob = nb[q];
+                            const bool g = od > d;
+                            nd[q] = g ? (gp ? pd : d) : od;
+                            nb[q] = g ? (gp ? pb : j) : ob;
+                            gp = g;
+                            pd = od;
+                            pb = ob;
+                        }
+                    }
+                }
             }
         }
         if (i < n) cov_from_list<KMAX>(P, nb, cnt, C + (size_t)6 * i);
