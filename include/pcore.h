@@ -226,6 +226,13 @@ int pcore_get_tile_info(pcore_ctx* ctx, pcore_tile_info* out);
  * parity test against the oracle's restatement of Eigen's pivoted LDLT. */
 int pcore_debug_lm_solve(const double* d_sys, const double* d_lambda, double* d_out, int32_t n, pcore_stream stream);
 
+/* Test hook (no reference counterpart): the GICP covariances of point segments by covariance_kernel (fast_gicp's
+ * k-nearest-neighbour covariance with PLANE regularisation): d_xyzw = points as x, y, z, w floats;
+ * segment s is points d_seg_off[s] .. + d_seg_cnt[s] (its own neighbour set); d_out_cov6 gets 6 doubles per point
+ * (upper triangle, row-major).  1 <= k <= 16. */
+int pcore_debug_covariances(const float* d_xyzw, const int32_t* d_seg_off, const int32_t* d_seg_cnt, int32_t num_segs,
+                            int32_t k, double* d_out_cov6, pcore_stream stream);
+
 /* GenerateSuccessorStates / GetStateImagesUnifiedGPU host work on the device (search_env.cpp:7056-7254,
  * 1535-1576), for the drop-in recognizer's states:
  *

@@ -1138,6 +1138,14 @@ int pcore_debug_lm_solve(const double* d_sys, const double* d_lambda, double* d_
     return launch_lm_solve_test(d_sys, d_lambda, d_out, n, (hipStream_t)stream) == hipSuccess ? PCORE_OK : PCORE_E_HIP;
 }
 
+int pcore_debug_covariances(const float* d_xyzw, const int32_t* d_seg_off, const int32_t* d_seg_cnt, int32_t num_segs,
+                            int32_t k, double* d_out_cov6, pcore_stream stream) {
+    if (num_segs < 0 || k <= 0 || (num_segs > 0 && (!d_xyzw || !d_seg_off || !d_seg_cnt || !d_out_cov6)))
+        return PCORE_E_INVALID_ARG;
+    return launch_covariances(reinterpret_cast<const float4*>(d_xyzw), d_seg_off, d_seg_cnt, 0, num_segs, k, d_out_cov6,
+                              (hipStream_t)stream, INT_MAX) == hipSuccess ? PCORE_OK : PCORE_E_INVALID_ARG;
+}
+
 int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,
                          int32_t stride, float depth_factor, const uint8_t* d_label_mask, const int32_t* d_pose_label,
                          float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label, int32_t cap, int32_t* out_count,
