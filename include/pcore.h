@@ -261,6 +261,19 @@ int pcore_depth_to_cloud(pcore_ctx* ctx, const int32_t* d_depth, int32_t num_pos
                          const int32_t* d_pose_label, float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label,
                          int32_t cap, int32_t* out_count, pcore_stream stream);
 
+/* Stage "CLOUD" with the reference's two debug outputs as well (renderer.cu:1821-1847): d_color_planes = the
+ * rendered colour planes (red, green, blue planes of N x H x W uint8 each -- pcore_render's d_out_color) and
+ * d_out_color = each point's colour from them as three planes of `cap` bytes (depth_to_2d_cloud,
+ * compute_point_clouds.cuh:163-165; the reference's plane stride is its point count, the same when cap equals it);
+ * d_out_dc_index = result_dc_index (N x H x W int32): for every pixel the number of cloud points before it in pose /
+ * row / column order, the reference's exclusive scan of the stride mask (compute_point_clouds.cuh:267-292).  Both
+ * outputs are nullable; the rest is pcore_depth_to_cloud's. */
+int pcore_depth_to_cloud_ex(pcore_ctx* ctx, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,
+                            int32_t stride, float depth_factor, const uint8_t* d_label_mask, const int32_t* d_pose_label,
+                            const uint8_t* d_color_planes, float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label,
+                            uint8_t* d_out_color, int32_t* d_out_dc_index, int32_t cap, int32_t* out_count,
+                            pcore_stream stream);
+
 /* Host selection of the reference moved on device: cost = (int)(rc + oc) (x86 conversion semantics),
  * skip invalid (-1/-2), keep |(int)rc - (int)oc| < 30, per-model minimum with strict '<' (lowest global
  * index wins ties) -- search_env.cpp:2022-2048, 2554-2566.  Result is folded into d_keys[num_models]

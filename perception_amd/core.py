@@ -274,23 +274,50 @@ class PoseCore:
 
     def depth_to_cloud(self, depth: torch.Tensor, stride: int, depth_factor: float,
                        label_mask: Optional[torch.Tensor] = None, pose_label: Optional[torch.Tensor] = None,
-                       stream=None):
-        """Stage CLOUD (compute_point_clouds): returns (xyz (P,3), pose (P,), label (P,))."""
+                       stream=None, color_planes: Optional[torch.Tensor] = None, dc_index: bool = False):
+        """Stage CLOUD (compute_point_clouds): returns (xyz (P,3), pose (P,), label (P,)); with `color_planes` (the
+        rendered colour planes, uint8 (3, N, H, W): `render(..., color=True)`'s second output) also the points'
+        colours (3, P) -- renderer.cu's result_cloud_color -- and with dc_index=True also result_dc_index (N, H, W)
+        int32 (pcore_depth_to_cloud_ex), appended in that order."""
         if depth.dim() == 2:
             depth = depth.unsqueeze(0)
         n, h, w = depth.shape
         cap = n * ((w + stride - 1) // stride) * ((h + stride - 1) // stride)
-        xyz = torch.empty((max(cap, 1), 3), dtype=torch.float32, device=depth.device)
-        pose = torch.empty((max(cap, 1),), dtype=torch.int32, device=depth.device)
-        lab = torch.empty((max(cap, 1),), dtype=torch.int32, device=depth.device)
+        dev = depth.device
+        xyz = torch.empty((max(cap, 1), 3), dtype=torch.float32, device=dev)
+        pose = torch.empty((max(cap, 1),), dtype=torch.int32, device=dev)
+        lab = torch.empty((max(cap, 1),), dtype=torch.int32, device=dev)
         cnt = ctypes.c_int32(0)
-        self._check(self.lib.pcore_depth_to_cloud(
+        extra = color_planes is not None or dc_index
+        if not extra:
+            self._check(self.lib.pcore_depth_to_cloud(
+                self._h, _ptr(depth.contiguous(), torch.int32, "depth"), n, w, h, stride, float(depth_factor),
+                _ptr(label_mask, torch.uint8, "label_mask"), _ptr(pose_label, torch.int32, "pose_label"),
+                _ptr(xyz, torch.float32, "xyz"), _ptr(pose, torch.int32, "pose"), _ptr(lab, torch.int32, "label"),
+                cap, ctypes.byref(cnt), _stream(stream)))
+            k = cnt.value
+            return xyz[:k], pose[:k], lab[:k]
+        planes = None
+        col = None
+        if color_planes is not None:
+            planes = color_planes.contiguous()
+            if tuple(planes.shape) != (3, n, h, w):
+                raise ValueError(f"color_planes must be (3, {n}, {h}, {w}), got {tuple(planes.shape)}")
+            col = torch.empty((3, max(cap, 1)), dtype=torch.uint8, device=dev)
+        dc = torch.empty((n, h, w), dtype=torch.int32, device=dev) if dc_index else None
+        self._check(self.lib.pcore_depth_to_cloud_ex(
             self._h, _ptr(depth.contiguous(), torch.int32, "depth"), n, w, h, stride, float(depth_factor),
             _ptr(label_mask, torch.uint8, "label_mask"), _ptr(pose_label, torch.int32, "pose_label"),
-            _ptr(xyz, torch.float32, "xyz"), _ptr(pose, torch.int32, "pose"), _ptr(lab, torch.int32, "label"),
-            cap, ctypes.byref(cnt), _stream(stream)))
+            _ptr(planes, torch.uint8, "color_planes"), _ptr(xyz, torch.float32, "xyz"), _ptr(pose, torch.int32, "pose"),
+            _ptr(lab, torch.int32, "label"), _ptr(col, torch.uint8, "color"), _ptr(dc, torch.int32, "dc_index"),
+            max(cap, 1) if col is not None else cap, ctypes.byref(cnt), _stream(stream)))
         k = cnt.value
-        return xyz[:k], pose[:k], lab[:k]
+        out = [xyz[:k], pose[:k], lab[:k]]
+        if col is not None:
+            out.append(col[:, :k])
+        if dc is not None:
+            out.append(dc)
+        return tuple(out)
 
     def select(self, rc: torch.Tensor, oc: torch.Tensor, pose_model: torch.Tensor, num_models: int,
                index_base: int = 0, keys: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:

@@ -79,6 +79,7 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_count;
     DevBuf<double> icp_cov;
     DevBuf<int32_t> icp_corr;   // GicpArgs::corr
+    DevBuf<int32_t> scratch_dc_pre;  // stage CLOUD result_dc_index: per-pose sample prefixes
     DevBuf<int32_t> icp_corr_hist;  // GicpArgs::corr_hist
     DevBuf<double> icp_mahal;   // GicpArgs::mahal
     DevBuf<int32_t> icp_counter;
@@ -315,7 +316,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->scratch_dc_pre); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part); (void)dev_free(c->tri_rgb); (void)dev_free(c->render_tri);
     for (hipEvent_t e : c->icp_ev) (void)hipEventDestroy(e);
@@ -1150,10 +1151,20 @@ int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses
                          int32_t stride, float depth_factor, const uint8_t* d_label_mask, const int32_t* d_pose_label,
                          float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label, int32_t cap, int32_t* out_count,
                          pcore_stream stream) {
+    return pcore_depth_to_cloud_ex(c, d_depth, num_poses, width, height, stride, depth_factor, d_label_mask,
+                                   d_pose_label, nullptr, d_out_xyz, d_out_pose, d_out_label, nullptr, nullptr, cap,
+                                   out_count, stream);
+}
+
+int pcore_depth_to_cloud_ex(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,
+                            int32_t stride, float depth_factor, const uint8_t* d_label_mask, const int32_t* d_pose_label,
+                            const uint8_t* d_color_planes, float* d_out_xyz, int32_t* d_out_pose, int32_t* d_out_label,
+                            uint8_t* d_out_color, int32_t* d_out_dc_index, int32_t cap, int32_t* out_count,
+                            pcore_stream stream) {
     if (!c) return PCORE_E_INVALID_ARG;
     if (!c->have_cam) return fail(c, PCORE_E_STATE, "depth_to_cloud: camera not set");
     if (num_poses < 0 || width <= 0 || height <= 0 || stride <= 0 || !d_depth || cap < 0 ||
-        (cap > 0 && !d_out_xyz) || !out_count)
+        (cap > 0 && !d_out_xyz) || !out_count || (d_out_color && !d_color_planes))
         return fail(c, PCORE_E_INVALID_ARG, "depth_to_cloud: bad arguments");
     if (width % stride != 0) return fail(c, PCORE_E_INVALID_ARG, "depth_to_cloud: width % stride != 0");
     if (d_label_mask && num_poses != 1)
@@ -1171,7 +1182,14 @@ int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses
     HIPC(c, launch_exclusive_scan(c->scratch_counts.p, c->scratch_offsets.p, num_poses, c->scratch_total.p, s));
     HIPC(c, launch_cloud_write(d_depth, num_poses, width, height, stride, c->cam.cx, c->cam.cy, c->cam.fx, c->cam.fy,
                                depth_factor, d_label_mask, d_pose_label, c->scratch_offsets.p, d_out_xyz, d_out_pose,
-                               d_out_label, cap, no_bounds, nullptr, nullptr, s));
+                               d_out_label, cap, no_bounds, nullptr, nullptr, s, d_out_color ? d_color_planes : nullptr,
+                               d_out_color));
+    if (d_out_dc_index) {
+        const size_t samples = (size_t)((width + stride - 1) / stride) * ((height + stride - 1) / stride);
+        HIPC(c, dev_reserve(c->scratch_dc_pre, (size_t)num_poses * (samples + 1)));
+        HIPC(c, launch_cloud_dc_index(d_depth, num_poses, width, height, stride, d_label_mask, c->scratch_offsets.p,
+                                      c->scratch_dc_pre.p, d_out_dc_index, s));
+    }
     int32_t total = 0;
     HIPC(c, hipMemcpyAsync(&total, c->scratch_total.p, 4, hipMemcpyDeviceToHost, s));
     HIPC(c, hipStreamSynchronize(s));

@@ -266,7 +266,12 @@ hipError_t launch_cloud_write(const int32_t* depth, int num_poses, int width, in
                               float cy, float fx, float fy, float depth_factor, const uint8_t* label_mask,
                               const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose,
                               int32_t* label, int cap, const CloudBounds& cb, const uint8_t* rgb_in,
-                              uint8_t* rgb_out, hipStream_t s);
+                              uint8_t* rgb_out, hipStream_t s, const uint8_t* planes_in = nullptr,
+                              uint8_t* planes_out = nullptr);
+// result_dc_index of stage CLOUD into dc (N x H x W int32); pre: N x (samples + 1) int32 scratch
+hipError_t launch_cloud_dc_index(const int32_t* depth, int num_poses, int width, int height, int stride,
+                                 const uint8_t* label_mask, const int32_t* offsets, int32_t* pre, int32_t* dc,
+                                 hipStream_t s);
 hipError_t launch_sample_source(const int32_t* src_depth, const uint8_t* src_mask, int width, int height,
                                 int stride, int32_t* src_s, uint8_t* lab_s, hipStream_t s);
 hipError_t launch_select(const float* rc, const float* oc, const int32_t* pose_model, int num_poses,

@@ -1502,7 +1502,7 @@ __global__ void cloud_write_kernel(const int32_t* depth, int width, int height, 
                                    float fx, float fy, float depth_factor, const uint8_t* label_mask,
                                    const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose_out,
                                    int32_t* label_out, int cap, CloudBounds cb, const uint8_t* rgb_in,
-                                   uint8_t* rgb_out) {
+                                   uint8_t* rgb_out, const uint8_t* planes_in, uint8_t* planes_out, int num_poses) {
     __shared__ int wsum[16];
     __shared__ int carry_s;
     const int n = blockIdx.x;
@@ -1546,6 +1546,12 @@ __global__ void cloud_write_kernel(const int32_t* depth, int width, int height, 
                     rgb_out[3 * (size_t)o + 1] = rgb_in[3 * idx + 1];
                     rgb_out[3 * (size_t)o + 2] = rgb_in[3 * idx + 2];
                 }
+                if (planes_out) {  // depth_to_2d_cloud :163-165: the rendered colour planes into point planes
+                    const size_t plane = npx * (size_t)num_poses;
+                    planes_out[o] = planes_in[idx];
+                    planes_out[(size_t)cap + o] = planes_in[plane + idx];
+                    planes_out[2 * (size_t)cap + o] = planes_in[2 * plane + idx];
+                }
                 if (label_out) {
                     if (label_mask) label_out[o] = (int32_t)label_mask[idx] - 1;
                     else if (pose_label) label_out[o] = pose_label[n];
@@ -1576,11 +1582,79 @@ hipError_t launch_cloud_write(const int32_t* depth, int num_poses, int width, in
                               float cy, float fx, float fy, float depth_factor, const uint8_t* label_mask,
                               const int32_t* pose_label, const int32_t* offsets, float* xyz, int32_t* pose,
                               int32_t* label, int cap, const CloudBounds& cb, const uint8_t* rgb_in,
-                              uint8_t* rgb_out, hipStream_t s) {
+                              uint8_t* rgb_out, hipStream_t s, const uint8_t* planes_in, uint8_t* planes_out) {
     if (num_poses <= 0) return hipSuccess;
     hipLaunchKernelGGL(cloud_write_kernel, dim3(num_poses), dim3(256), 0, s, depth, width, height, stride, cx, cy, fx,
                        fy, depth_factor, label_mask, pose_label, offsets, xyz, pose, label, cap, cb, rgb_in,
-                       rgb_out);
+                       rgb_out, planes_in, planes_out, num_poses);
+    return hipGetLastError();
+}
+
+// result_dc_index (compute_point_clouds.cuh:267-292): the reference scans a 0/1 mask over every pixel of the N
+// z-buffers, so a pixel's entry is the number of cloud points (valid stride samples) before it in pose / row / column
+// order.  Per pose, the exclusive count at every stride sample and at the pose's end (one block per pose) ...
+__global__ void cloud_sample_prefix_kernel(const int32_t* depth, int width, int height, int stride,
+                                           const uint8_t* label_mask, const int32_t* offsets, int32_t* pre) {
+    __shared__ int wsum[16];
+    __shared__ int carry_s;
+    const int n = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
+    const size_t npx = (size_t)width * height;
+    int32_t* P = pre + (size_t)n * (ws * hs + 1);
+    const CloudBounds cb{};
+    if (threadIdx.x == 0) carry_s = offsets[n];
+    __syncthreads();
+    for (int base = 0; base < ws * hs; base += blockDim.x) {
+        const int k = base + threadIdx.x;
+        bool v = false;
+        if (k < ws * hs) {
+            const int ky = k / ws, kx = k - ky * ws;
+            v = cloud_valid(depth, label_mask, npx * n + (size_t)(kx * stride) + (size_t)(ky * stride) * width,
+                            kx * stride, ky * stride, cb);
+        }
+        const uint64_t b = __ballot(v);
+        if (lane == 0) wsum[wave] = __popcll(b);
+        __syncthreads();
+        int woff = 0, tot = 0;
+        for (int w = 0; w < nw; w++) {
+            if (w < wave) woff += wsum[w];
+            tot += wsum[w];
+        }
+        const int carry = carry_s;
+        if (k < ws * hs) P[k] = carry + woff + mbcnt64(b);
+        __syncthreads();
+        if (threadIdx.x == 0) carry_s = carry + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) P[ws * hs] = carry_s;
+}
+
+// ... then every pixel: the samples before pixel (x, y) are the rows of samples above it and, on a sample row, the
+// samples left of it
+__global__ void cloud_dc_index_kernel(int num_poses, int width, int height, int stride, const int32_t* pre,
+                                      int32_t* dc) {
+    const int ws = (width + stride - 1) / stride, hs = (height + stride - 1) / stride;
+    const size_t npx = (size_t)width * height, total = npx * num_poses;
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t)gridDim.x * blockDim.x) {
+        const size_t n = p / npx, r = p - n * npx;
+        const int y = (int)(r / width), x = (int)(r - (size_t)y * width);
+        const int ry = y % stride == 0 ? y / stride : y / stride + 1;
+        const int cx = y % stride == 0 ? (x + stride - 1) / stride : 0;
+        const int k = min(ry * ws + cx, ws * hs);
+        dc[p] = pre[n * (size_t)(ws * hs + 1) + k];
+    }
+}
+
+hipError_t launch_cloud_dc_index(const int32_t* depth, int num_poses, int width, int height, int stride,
+                                 const uint8_t* label_mask, const int32_t* offsets, int32_t* pre, int32_t* dc,
+                                 hipStream_t s) {
+    if (num_poses <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cloud_sample_prefix_kernel, dim3(num_poses), dim3(256), 0, s, depth, width, height, stride,
+                       label_mask, offsets, pre);
+    const size_t total = (size_t)width * height * num_poses;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+    hipLaunchKernelGGL(cloud_dc_index_kernel, dim3(blocks), dim3(256), 0, s, num_poses, width, height, stride, pre, dc);
     return hipGetLastError();
 }
 

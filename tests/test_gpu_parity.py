@@ -140,6 +140,43 @@ def test_depth_to_cloud_matches_oracle(one_object):
     assert np.array_equal(lab.cpu().numpy(), olab)
 
 
+def test_depth_to_cloud_colours_and_dc_index(one_object):
+    """Stage CLOUD's debug outputs (renderer.cu:1821-1847, pcore_depth_to_cloud_ex): result_dc_index is the reference's
+    exclusive scan of the stride mask over every pixel of the N z-buffers (compute_point_clouds.cuh:267-292), and
+    result_cloud_color gathers the colour planes at the points (:163-165); the points themselves are the plain call's.
+    Restated here in numpy on random colour planes, with and without a label mask."""
+    case, core, t = one_object
+    sc = case.scene
+    s = case.stride
+    n = 9
+    zb = core.render(t["poses"][:n], t["pm"][:n], t["pl"][:n])
+    rng = np.random.default_rng(3)
+    planes = rng.integers(0, 256, size=(3, n, sc.height, sc.width), dtype=np.uint8)
+    dev = zb.device
+    for label_mask in (None, t["mask"]):
+        m = n if label_mask is None else 1
+        z = zb[:m]
+        pl = t["pl"][:m]
+        xyz, pose, lab, col, dc = core.depth_to_cloud(z, s, 100.0, label_mask=label_mask, pose_label=pl,
+                                                      color_planes=torch.from_numpy(planes[:, :m].copy()).to(dev),
+                                                      dc_index=True)
+        pxyz, ppose, plab = core.depth_to_cloud(z, s, 100.0, label_mask=label_mask, pose_label=pl)
+        assert _bits_equal(xyz.cpu().numpy(), pxyz.cpu().numpy())
+        assert np.array_equal(pose.cpu().numpy(), ppose.cpu().numpy())
+        assert np.array_equal(lab.cpu().numpy(), plab.cpu().numpy())
+        zn = z.cpu().numpy()
+        mask = np.zeros(zn.shape, bool)
+        mask[:, ::s, ::s] = zn[:, ::s, ::s] > 0
+        if label_mask is not None:
+            mask &= label_mask.cpu().numpy()[None] > 0
+        flat = mask.ravel().astype(np.int64)
+        want_dc = (np.cumsum(flat) - flat).reshape(zn.shape)
+        assert np.array_equal(dc.cpu().numpy(), want_dc)
+        assert len(xyz) == flat.sum() > 0
+        want_col = planes[:, :m].reshape(3, -1)[:, mask.ravel()]
+        assert np.array_equal(col.cpu().numpy(), want_col)
+
+
 def test_select_matches_oracle(three_objects):
     case, core, t = three_objects
     rc, oc, df = core.evaluate(t["poses"], t["pm"], t["pl"], t["tot"], cost_type=2, stride=case.stride)
