@@ -1038,6 +1038,10 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         a.cloud_out = c->icp_cloud.p;
         a.cloud_count = c->icp_count.p;
         a.cloud_cap = nsamp;
+        // the fused launch's most-occupied tile (6 workgroups per CU); larger windows are rastered in chunks of it
+        a.tcap = fused_tier_samples(0, a.ws, a.hs, 0, false, c->dinfo);
+        if (const char* e = getenv("PCORE_FUSED_TCAP")) a.tcap = std::min(std::max(atoi(e), 1), a.ws * a.hs);
+        if (a.tcap <= 0) a.tcap = a.ws * a.hs;
         HIPC(c, launch_render_cloud(a, s));
         hipEvent_t* ev = timed ? c->icp_ev.data() + 3 * c->icp_ev_used : nullptr;
         if (ev) HIPC(c, hipEventRecord(ev[0], s));

@@ -1164,7 +1164,8 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int s = STRIDE > 0 ? STRIDE : a.stride;
     const int ws = a.ws, nsamp = a.ws * a.hs;
-    const FusedSmem sm = carve_smem(smem_raw, nsamp, 0);
+    const int cap = a.tcap > 0 && a.tcap < nsamp ? a.tcap : nsamp;  // the LDS tile (samples)
+    const FusedSmem sm = carve_smem(smem_raw, cap, 0);
     const int model = a.pose_model[pose];
     SampleWin sw = {0, 0, 0, 0, 0};
     if (model >= 0 && model < a.num_models) {
@@ -1172,56 +1173,69 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
         load_pose_rows(a.poses, pose, m);
         sw = pose_window(a, model, m, s);
     }
-    const int tn = sw.nx * sw.ny;  // <= nsamp: the tile is the whole image here
-    for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
     if (tid == 0) carry_s = 0;
     const bool use_seg = a.pose_label != nullptr;
     const int32_t pl = use_seg ? a.pose_label[pose] : 0;
     FProf fp;
-    raster_phase<STRIDE>(a, sm, pose, sw, nullptr, fp);
-    __syncthreads();
     float4* out = a.cloud_out + (size_t)pose * a.cloud_cap;
-    // row-major over the window = the reference's row-major compaction order (no valid sample lies outside)
-    const float inv_nx = tn > 0 ? 1.0f / (float)sw.nx : 0.0f;
-    for (int base = 0; base < tn; base += kThreads) {
-        const int k = base + tid;
-        int32_t zf = 0;
-        int kx = 0, ky = 0;
-        if (k < tn) {
-            int iy = (int)(((float)k + 0.5f) * inv_nx), ix = k - iy * sw.nx;
-            if (ix < 0) { iy--; ix += sw.nx; } else if (ix >= sw.nx) { iy++; ix -= sw.nx; }
-            kx = sw.x0 + ix;
-            ky = sw.y0 + iy;
-            const int gk = ky * ws + kx;
-            zf = occlusion_rule(sm.zbuf[k], a.src_s[gk], use_seg ? (int)a.lab_s[gk] : 0, use_seg, pl,
-                                a.occlusion_threshold);
-        }
-        const bool valid = zf > 0;
-        const uint64_t b = __ballot(valid);
-        if (lane == 0) wsum[wave] = __popcll(b);
+    // one chunk of the window (fused_pose's chunking): raster into the tile, then the chunk's valid samples appended
+    // in row-major order -- row bands of whole window rows (column blocks when a row exceeds the tile) keep the
+    // reference's row-major compaction order (no valid sample lies outside the window)
+    auto chunk = [&](const SampleWin& cw) __attribute__((always_inline)) {
+        const int tn = cw.nx * cw.ny;
+        for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
+        raster_phase<STRIDE>(a, sm, pose, cw, nullptr, fp);
         __syncthreads();
-        int woff = 0, tot = 0;
-        for (int w = 0; w < kWaves; w++) {
-            if (w < wave) woff += wsum[w];
-            tot += wsum[w];
+        const float inv_nx = tn > 0 ? 1.0f / (float)cw.nx : 0.0f;
+        for (int base = 0; base < tn; base += kThreads) {
+            const int k = base + tid;
+            int32_t zf = 0;
+            int kx = 0, ky = 0;
+            if (k < tn) {
+                int iy = (int)(((float)k + 0.5f) * inv_nx), ix = k - iy * cw.nx;
+                if (ix < 0) { iy--; ix += cw.nx; } else if (ix >= cw.nx) { iy++; ix -= cw.nx; }
+                kx = cw.x0 + ix;
+                ky = cw.y0 + iy;
+                const int gk = ky * ws + kx;
+                zf = occlusion_rule(sm.zbuf[k], a.src_s[gk], use_seg ? (int)a.lab_s[gk] : 0, use_seg, pl,
+                                    a.occlusion_threshold);
+            }
+            const bool valid = zf > 0;
+            const uint64_t b = __ballot(valid);
+            if (lane == 0) wsum[wave] = __popcll(b);
+            __syncthreads();
+            int woff = 0, tot = 0;
+            for (int w = 0; w < kWaves; w++) {
+                if (w < wave) woff += wsum[w];
+                tot += wsum[w];
+            }
+            const int carry = carry_s;
+            if (valid) {
+                const int o = carry + woff + mbcnt64(b);
+                const float zp = (float)zf / a.depth_factor;
+                const float xp = ((float)(kx * s) - a.cx) / a.fx * zp;
+                const float yp = ((float)(ky * s) - a.cy) / a.fy * zp;
+                if (o < a.cloud_cap) out[o] = make_float4(xp, yp, zp, 0.0f);
+            }
+            __syncthreads();
+            if (tid == 0) carry_s = carry + tot;
+            __syncthreads();
         }
-        const int carry = carry_s;
-        if (valid) {
-            const int o = carry + woff + mbcnt64(b);
-            const float zp = (float)zf / a.depth_factor;
-            const float xp = ((float)(kx * s) - a.cx) / a.fx * zp;
-            const float yp = ((float)(ky * s) - a.cy) / a.fy * zp;
-            if (o < a.cloud_cap) out[o] = make_float4(xp, yp, zp, 0.0f);
-        }
-        __syncthreads();
-        if (tid == 0) carry_s = carry + tot;
-        __syncthreads();
+    };
+    if (sw.nx * sw.ny <= cap) {
+        chunk(sw);
+    } else {
+        const int cw = min(sw.nx, cap), ch = max(1, cap / max(cw, 1));
+        for (int r0 = 0; r0 < sw.ny; r0 += ch)
+            for (int c0 = 0; c0 < sw.nx; c0 += cw)
+                chunk(SampleWin{sw.x0 + c0, sw.y0 + r0, min(cw, sw.nx - c0), min(ch, sw.ny - r0), sw.fastdiv});
     }
     if (tid == 0) a.cloud_count[pose] = carry_s < a.cloud_cap ? carry_s : a.cloud_cap;
 }
 
 hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
-    const size_t lds = fused_lds_bytes(a.ws * a.hs, 0);
+    const int nsamp = a.ws * a.hs;
+    const size_t lds = fused_lds_bytes(a.tcap > 0 && a.tcap < nsamp ? a.tcap : nsamp, 0);
     if (a.num_poses <= 0) return hipSuccess;
     if (a.stride == 8)
         hipLaunchKernelGGL(render_cloud_kernel<8>, dim3(a.num_poses), dim3(kThreads), lds, s, a);

@@ -526,6 +526,28 @@ def test_evaluate_icp_matches_oracle(fixture, kernel, request, monkeypatch):
     assert _bits_equal(df.cpu().numpy(), odf)
 
 
+def test_evaluate_icp_chunked_cloud_tile_matches_oracle(three_objects, monkeypatch):
+    """With a 64-sample tile the GICP source clouds are rastered in chunks of the tile (render_cloud_kernel's row
+    bands / column blocks) and appended chunk after chunk: the reference's row-major compaction order, so the refined
+    poses and costs stay the oracle's bit for bit."""
+    case, core, t = three_objects
+    sc = case.scene
+    n = min(32, len(case.poses))
+    monkeypatch.setenv("PCORE_FUSED_TCAP", "64")
+    adj, iters, rc, oc, df = core.evaluate_icp(t["poses"][:n], t["pm"][:n], t["pl"][:n], t["tot"][:n],
+                                               cost_type=2, stride=case.stride)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, case.poses[:n], case.pose_model[:n], case.pose_label[:n],
+        sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy,
+        100.0, case.obs_xyz, _label_covs(case), case.label_start, case.label_end, case.pose_obs_total[:n], 2, True,
+        0.01)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+
+
 def test_evaluate_icp_3dof_matches_oracle(one_object):
     case, core, t = one_object
     sc = case.scene
