@@ -13,7 +13,8 @@
 //                      k-NN of every point inside its segment (candidates staged through LDS), double
 //                      mean / covariance, 6-sweep Jacobi, PLANE regularisation.
 //   gicp_kernel        one wave per pose: per-lane sequential partial sums of J^T M J / J^T M e / e^T M e,
-//                      the LDS-transposed shuffle-down tree, the LM iteration on every lane (uniform), then
+//                      the shuffle-down tree in registers (wave_tree_sums), the LM iteration (the damped solve
+//                      with a row per lane, the rest uniform), the correspondence history, then
 //                      concatenate_transforms (renderer.cu:1412-1429).
 //   gicp_wide_kernel   small batches: eight waves search a pose's correspondences, wave 0 as gicp_kernel.
 #include "pcore_internal.h"
@@ -870,7 +871,7 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
 
 // One wave per pose; persistent waves pull poses from a counter.  Each iteration linearises in rounds of 64
 // source points (point i -> lane i % 64, contributions added in point order), reduces the 28 terms by the
-// LDS-transposed shuffle-down tree and runs the LM iteration on every lane.  The per-pose iteration chain is
+// shuffle-down tree in registers and runs the LM iteration on the wave.  The per-pose iteration chain is
 // latency-bound, so the slowest pose sets a chunk's tail (the queue is ordered longest first).
 #ifndef PCORE_GICP_WAVES_PER_EU
 #define PCORE_GICP_WAVES_PER_EU 3
