@@ -301,12 +301,22 @@ def main():
     del dbg
     torch.cuda.synchronize()
 
+    # host timestamps of every timed step (perf_counter, s): step start, around the wait for the lane's previous
+    # exchange, around the launch call, after the exchange is issued -- they attribute a slow step to the host wait
+    # (the exchange), to the launch call itself, or to the GPU (the HIP-event span) without another run
+    host_ts = []
+
     def run_step(i, ev=None):
         b = i % L
         core, st = lanes[b]
-        with torch.cuda.stream(st):
-            if works[b] is not None:
+        t0h = time.perf_counter()
+        # the lane's previous exchange must have completed before its key buffer is rewritten: with RCCL wait() only
+        # orders the lane's stream after the collective; with gloo it blocks the host until the exchange is done
+        if works[b] is not None:
+            with torch.cuda.stream(st):
                 works[b].wait()
+        t1h = time.perf_counter()
+        with torch.cuda.stream(st):
             keys_ring[b].fill_(PCORE_KEY_NONE)
             if ev is not None:
                 ev[0].record(st)
@@ -315,7 +325,10 @@ def main():
                           select=(keys_ring[b], w.index_base, w.num_models))
             if ev is not None:
                 ev[1].record(st)
+            t2h = time.perf_counter()
             works[b] = pdist.allreduce_min_keys_async(keys_ring[b])
+        if ev is not None:
+            host_ts.append((t0h, t1h, t2h, time.perf_counter()))
 
     for i in range(args.warmup + L):  # every lane warmed (tile tier picked from its own first call)
         run_step(i)
@@ -359,6 +372,23 @@ def main():
             cur_hi = max(cur_hi, hi)
     busy += cur_hi - cur_lo
     busy_ms = busy / len(iv)
+
+    ht = np.array(host_ts) - t0
+    wait_ms = (ht[:, 1] - ht[:, 0]) * 1e3
+    launch_ms = (ht[:, 2] - ht[:, 1]) * 1e3
+    issue_ms = (ht[:, 3] - ht[:, 2]) * 1e3
+    spans = np.array([a.elapsed_time(b) for a, b in ev])
+    host_timing = {
+        "wait_prev_exchange_ms": {"mean": float(wait_ms.mean()), "max": float(wait_ms.max())},
+        "launch_call_ms": {"mean": float(launch_ms.mean()), "max": float(launch_ms.max())},
+        "exchange_issue_ms": {"mean": float(issue_ms.mean()), "max": float(issue_ms.max())},
+        "launch_span_ms": {"mean": float(spans.mean()), "max": float(spans.max())},
+        "slowest_step": int(np.argmax(np.diff(np.append(ht[:, 0], elapsed)))),
+        "definition": "per timed step, host perf_counter: wait = works[b].wait() for the lane's previous exchange "
+                      "(gloo: host-blocking; RCCL: a stream dependency), launch_call = fill + evaluate call + "
+                      "event records, exchange_issue = the async all_reduce call; launch_span = HIP events around "
+                      "the fill + stage-COST launch on the lane's stream",
+    }
 
     best_cost, best_idx = decode_keys(keys)
     c3 = None
@@ -456,6 +486,7 @@ def main():
                    "batches_in_flight": L, "ranks": joined, "devices": devices,
                    "dist_backend": torch.distributed.get_backend() if joined > 1 else None},
         "roofline": roofline,
+        "host_timing": host_timing,
         "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},
     }
     if c3 is not None:

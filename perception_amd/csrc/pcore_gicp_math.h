@@ -651,6 +651,76 @@ PCORE_UNROLL
 PCORE_GHD void lm_solve_rows(const double* sys, double lambda, double (&d)[6]) { lm_solve<false>(sys, lambda, d); }
 #endif
 
+// Adjugate (upper: 00 01 02 11 12 22) and determinant of a symmetric 3x3 given by its upper triangle (same order)
+PCORE_GHD void adj_sym3(const double (&m)[6], double (&a)[6], double& det) {
+    a[0] = m[3] * m[5] - m[4] * m[4];
+    a[1] = m[2] * m[4] - m[1] * m[5];
+    a[2] = m[1] * m[4] - m[2] * m[3];
+    a[3] = m[0] * m[5] - m[2] * m[2];
+    a[4] = m[1] * m[2] - m[0] * m[4];
+    a[5] = m[0] * m[3] - m[1] * m[1];
+    det = m[0] * a[0] + m[1] * a[1] + m[2] * a[2];
+}
+PCORE_GHD constexpr int s3(int i, int j) { return i <= j ? (i == 0 ? j : i == 1 ? 2 + j : 5) : s3(j, i); }
+
+// d = (H + lambda I)^-1 (-b) by the 3x3 block elimination of the translation block (the candidate spec of the damped
+// solve): with H = [[A, B], [B^T, C]] (A rotation, C translation, both + lambda I) and r = -b,
+//   adj(C), det(C) = dC;  P = B adj(C);  S~ = dC A - P B^T (= dC times the Schur complement, upper triangle);
+//   u~ = dC r_rot - P r_trans;  x_rot = adj(S~) u~ / det(S~);  x_trans = adj(C) (r_trans - B^T x_rot) / dC,
+// every sum in index order.  H + lambda I is positive definite whenever it is not zero (H is a sum of J^T M J with M
+// positive definite, lambda = 1e-9 max|H_aa| > 0 unless H = 0): a zero diagonal gives d = 0 (Eigen's LDLT of the zero
+// matrix); a non-finite system gives a non-finite d, which stops the pose (lm_iteration's guard).  The dependent
+// chain is two adjugates, two 3-term products and two divisions deep, against the LDLT's six pivot steps.
+PCORE_GHD void lm_solve_schur(const double* sys, double lambda, double (&d)[6]) {
+    double A[6], C[6], B[3][3], r[6];
+PCORE_UNROLL
+    for (int i = 0; i < 3; i++) {
+PCORE_UNROLL
+        for (int j = i; j < 3; j++) {
+            A[s3(i, j)] = i == j ? sys[hdiag(i)] + lambda : sys[hidx(i, j)];
+            C[s3(i, j)] = i == j ? sys[hdiag(3 + i)] + lambda : sys[hidx(3 + i, 3 + j)];
+        }
+PCORE_UNROLL
+        for (int j = 0; j < 3; j++) B[i][j] = sys[hidx(i, 3 + j)];
+    }
+PCORE_UNROLL
+    for (int i = 0; i < 6; i++) r[i] = -sys[21 + i];
+    if (A[0] == 0.0 && A[3] == 0.0 && A[5] == 0.0 && C[0] == 0.0 && C[3] == 0.0 && C[5] == 0.0) {
+PCORE_UNROLL
+        for (int i = 0; i < 6; i++) d[i] = 0.0;  // the zero system
+        return;
+    }
+    double aC[6], dC;
+    adj_sym3(C, aC, dC);
+    double P[3][3];
+PCORE_UNROLL
+    for (int i = 0; i < 3; i++)
+PCORE_UNROLL
+        for (int j = 0; j < 3; j++)
+            P[i][j] = B[i][0] * aC[s3(0, j)] + B[i][1] * aC[s3(1, j)] + B[i][2] * aC[s3(2, j)];
+    double St[6], ut[3];
+PCORE_UNROLL
+    for (int i = 0; i < 3; i++) {
+PCORE_UNROLL
+        for (int j = i; j < 3; j++)
+            St[s3(i, j)] = dC * A[s3(i, j)] - (P[i][0] * B[j][0] + P[i][1] * B[j][1] + P[i][2] * B[j][2]);
+        ut[i] = dC * r[i] - (P[i][0] * r[3] + P[i][1] * r[4] + P[i][2] * r[5]);
+    }
+    double aS[6], dS;
+    adj_sym3(St, aS, dS);
+    double x1[3];
+PCORE_UNROLL
+    for (int i = 0; i < 3; i++) x1[i] = (aS[s3(i, 0)] * ut[0] + aS[s3(i, 1)] * ut[1] + aS[s3(i, 2)] * ut[2]) / dS;
+    double w[3];
+PCORE_UNROLL
+    for (int j = 0; j < 3; j++) w[j] = r[3 + j] - (B[0][j] * x1[0] + B[1][j] * x1[1] + B[2][j] * x1[2]);
+PCORE_UNROLL
+    for (int j = 0; j < 3; j++) {
+        d[j] = x1[j];
+        d[3 + j] = (aC[s3(j, 0)] * w[0] + aC[s3(j, 1)] * w[1] + aC[s3(j, 2)] * w[2]) / dC;
+    }
+}
+
 // se3_exp (fast_gicp so3.hpp): so3_exp quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
 // cos(theta/2)), Eigen's Quaternion::toRotationMatrix, translation V rho with
 // V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10)

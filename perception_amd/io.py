@@ -327,6 +327,26 @@ def write_output_stats(path: str, scenes_rendered: int, scenes_valid: int, expan
         f.write(f"{scenes_rendered} {scenes_valid} {expands} {time_s} {cost} {icp_time} {peak_gpu_mem}\n")
 
 
+def write_cost_dump(path: str, poses: List[dict]):
+    """<debug_dir>/cost_dump.json (search_env.cpp:2463-2464, 2647-2649): {"poses": [...]} as nlohmann::json prints
+    it with std::setw(4) -- keys in sorted order (nlohmann's std::map objects), four-space indent, one array element
+    per line, floats (stored as double) in shortest round-trip form, and a trailing newline (std::endl).  Read by
+    convert_fat_coco.py:1365-1369."""
+    import json
+
+    with open(path, "w") as f:
+        f.write(json.dumps({"poses": poses}, indent=4, sort_keys=True))
+        f.write("\n")
+
+
+def read_cost_dump(path: str) -> List[dict]:
+    """The "poses" list of a cost_dump.json (as convert_fat_coco.py:1368-1369 loads it)."""
+    import json
+
+    with open(path) as f:
+        return json.load(f)["poses"]
+
+
 def read_output_stats(path: str) -> Dict[str, float]:
     """perch.py:220-229."""
     with open(path) as f:

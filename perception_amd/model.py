@@ -101,6 +101,72 @@ def matrix_to_quat_xyzw(R: np.ndarray) -> np.ndarray:
     return np.array([x, y, z, w])
 
 
+def quat_from_matrix_eigen_batch(R: np.ndarray, dtype=np.float32) -> np.ndarray:
+    """Eigen::Quaternion<Scalar>(Matrix3) over (N, 3, 3) rotations in Scalar = dtype arithmetic, Eigen's own algorithm
+    (Geometry/Quaternion.h, quaternionbase_assign_impl<Other, 3, 3>): with t = trace ((m00 + m11) + m22) > 0,
+    t = sqrt(t + 1), w = t / 2, then (x, y, z) = (m21 - m12, m02 - m20, m10 - m01) * (0.5 / t); otherwise i = the
+    first largest diagonal entry (m11 > m00, then m22 > m_ii), j = i + 1, k = j + 1 (mod 3),
+    t = sqrt(((m_ii - m_jj) - m_kk) + 1), q_i = t / 2 and, scaled by 0.5 / t, w = m_kj - m_jk, q_j = m_ji + m_ij,
+    q_k = m_ki + m_ik.  -> (N, 4) (x, y, z, w).  search_env.cpp:2008 builds the adjusted ContPose with
+    Quaternionf of the float matrix, hence float32 by default."""
+    m = np.asarray(R, dtype=dtype).reshape(-1, 3, 3)
+    n = len(m)
+    half = dtype(0.5)
+    one = dtype(1.0)
+    out = np.zeros((n, 4), dtype=dtype)
+    tr = (m[:, 0, 0] + m[:, 1, 1]) + m[:, 2, 2]
+    pos = tr > 0
+    with np.errstate(invalid="ignore", divide="ignore"):
+        t = np.sqrt(tr + one)
+        s = half / t
+        pq = np.stack([(m[:, 2, 1] - m[:, 1, 2]) * s, (m[:, 0, 2] - m[:, 2, 0]) * s, (m[:, 1, 0] - m[:, 0, 1]) * s,
+                       half * t], 1)
+        i = np.where(m[:, 1, 1] > m[:, 0, 0], 1, 0)
+        i = np.where(m[:, 2, 2] > m[np.arange(n), i, i], 2, i)
+        j = (i + 1) % 3
+        k = (j + 1) % 3
+        r = np.arange(n)
+        t2 = np.sqrt(((m[r, i, i] - m[r, j, j]) - m[r, k, k]) + one)
+        s2 = half / t2
+        nq = np.zeros((n, 4), dtype=dtype)
+        nq[r, i] = half * t2
+        nq[:, 3] = (m[r, k, j] - m[r, j, k]) * s2
+        nq[r, j] = (m[r, j, i] + m[r, i, j]) * s2
+        nq[r, k] = (m[r, k, i] + m[r, i, k]) * s2
+    out[:] = np.where(pos[:, None], pq, nq)
+    return out
+
+
+def so3_log_batch(q_xyzw: np.ndarray, dtype=np.float32) -> np.ndarray:
+    """Sophus::SO3<Scalar>::log() of unit quaternions (x, y, z, w) in Scalar = dtype (Sophus so3.hpp logAndTheta,
+    epsilon 1e-5 for float, 1e-10 for double): n^2 = (x x + y y) + z z; below epsilon^2 the factor
+    2 / w - 2/3 n^2 / (w w^2), else with n = sqrt(n^2) +-pi / n when |w| < epsilon, otherwise 2 atan(n / w) / n;
+    the tangent is that factor times (x, y, z).  The reference's Sophus is not vendored (search_env.cpp:2614 is its
+    only use on this path): parity unpinned."""
+    q = np.asarray(q_xyzw, dtype=dtype).reshape(-1, 4)
+    x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    eps = dtype(1e-5) if dtype == np.float32 else dtype(1e-10)
+    two = dtype(2.0)
+    sq = (x * x + y * y) + z * z
+    with np.errstate(invalid="ignore", divide="ignore"):
+        small = two / w - dtype(2.0 / 3.0) * sq / (w * (w * w))
+        nn = np.sqrt(sq)
+        pi = dtype(np.pi)
+        near_pi = np.where(w > 0, pi / nn, -pi / nn)
+        general = two * np.arctan(nn / w) / nn
+        f = np.where(sq < eps * eps, small, np.where(np.abs(w) < eps, near_pi, general))
+    return (f[:, None] * q[:, :3]).astype(dtype)
+
+
+def matmul_lazy(X: np.ndarray, Y: np.ndarray) -> np.ndarray:
+    """Batched 4x4 (or 3x3) products in the operands' own dtype, each entry summed over k in index order as Eigen's
+    lazy fixed-size product does without FMA: ((x0 y0 + x1 y1) + x2 y2) + ..."""
+    acc = X[..., :, 0, None] * Y[..., None, 0, :]
+    for c in range(1, X.shape[-1]):
+        acc = acc + X[..., :, c, None] * Y[..., None, c, :]
+    return acc
+
+
 def quat_xyzw_to_matrix_batch(q: np.ndarray) -> np.ndarray:
     """quat_xyzw_to_matrix over (N, 4) quaternions: the same float64 operations per element."""
     q = np.asarray(q, dtype=np.float64).reshape(-1, 4)

@@ -204,6 +204,7 @@ def run(output_dir_name: str, ps: ParamServer, device: Optional[int] = None) -> 
     t0 = time.perf_counter()
     if use_external_pose_list == 1:  # 6-DoF: 16-bit depth, label mask, poses.txt lists
         rec = ObjectRecognizer(bank, cam, params, device)
+        rec.debug_dir = experiment_dir  # SetDebugDir (perch_fat.cpp:116): cost_dump.json goes there
         inp = RecognitionInput(names, str(ps.get("/input_depth_image")), str(ps.get("/predicted_mask_image")),
                                depth_factor=depth_factor, camera_pose=camera_pose,
                                rendered_root_dir=ps.get("/rendered_root_dir"),
@@ -217,6 +218,7 @@ def run(output_dir_name: str, ps: ParamServer, device: Optional[int] = None) -> 
                             res=float(ps.get("/search_resolution_translation", 0.04)),
                             theta_res=float(ps.get("/search_resolution_yaw", 0.3926991)))
         rec = TabletopRecognizer(bank, cam, table, params, device)
+        rec.debug_dir = experiment_dir
         depth = _read_image(str(ps.get("/input_depth_image")))
         rgb = None
         colour = ps.get("/input_color_image")

@@ -28,8 +28,8 @@ from . import io as pio
 from ._native import COST_DEPTH_6DOF, ICP_K, ICP_MAX_ITER, ICP_ROT_EPS, ICP_TRANS_EPS, PCORE_KEY_NONE
 from .core import PoseCore, decode_keys
 from .distributed import allreduce_min_keys, shard_range
-from .model import (Model, chain_matmul_batch, compute_proj, init_from_eigen_batch, matrix_to_quat_xyzw, pose_matrix,
-                    pose_matrix_batch, to_eigen)
+from .model import (Model, chain_matmul_batch, compute_proj, init_from_eigen_batch, matmul_lazy, pose_matrix_batch,
+                    quat_from_matrix_eigen_batch, so3_log_batch)
 
 # cam_to_body (search_env.cpp:1536-1539)
 CAM_TO_BODY = np.array([[0, 0, 1, 0], [-1, 0, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1]], np.float64)
@@ -214,6 +214,14 @@ def valid_pose_mask(translations: np.ndarray, seg_points: np.ndarray, search_rad
     return radius_counts(translations, seg, search_rad, device) >= need
 
 
+def cvtt_i32(x) -> np.ndarray:
+    """C++ (int) of floats on x86 (cvttss2si): truncation toward zero; NaN and out-of-range values give INT_MIN."""
+    x = np.asarray(x, np.float32)
+    with np.errstate(invalid="ignore"):
+        ok = np.isfinite(x) & (x > -2147483649.0) & (x < 2147483648.0)
+        return np.where(ok, np.trunc(np.where(ok, x, 0.0)), -2147483648).astype(np.int64)
+
+
 def _dims(model: Model):
     """Bounding-box extents of the model's vertices (min / max over the triangle corners: the same as over
     the unique vertices, without sorting them)."""
@@ -244,6 +252,9 @@ class ObjectRecognizer:
         self.preprocess: List[np.ndarray] = []
         self.last_stats = EnvStats()
         self.last_timing: dict = {}
+        # EnvObjectRecognition::debug_dir_: when set, compute_greedy_render_poses writes <debug_dir>/cost_dump.json
+        # (search_env.cpp:2463-2464, 2600-2619, 2647-2649); perch_fat sets it to the experiment directory
+        self.debug_dir: Optional[str] = None
 
     # -- ObjectRecognizer::SetStaticInput -> LoadObjFiles (search_env.cpp:253-307) -----------------
     def set_static_input(self, model_names: Sequence[str], six_dof: bool = True):
@@ -530,17 +541,11 @@ class ObjectRecognizer:
             torch.distributed.all_reduce(st, op=torch.distributed.ReduceOp.MAX)
             icp_time, peak_mb = float(st[0]), float(st[1])
         win = win.cpu().numpy()
-        results = []
-        for m in range(K):
-            if idx[m] < 0:
-                continue
-            # search_env.cpp:1996-2019: GPU-adjusted mat4x4 -> to_eigen(100) -> ContPose (6-DoF keeps the frame)
-            Tm = to_eigen(win[m], 100).astype(np.float64)
-            if inp.use_external_pose_list != 1:
-                Tm = (self.camera_pose @ CAM_TO_BODY) @ Tm @ np.linalg.inv(self.preprocess[m])
-            q = matrix_to_quat_xyzw(Tm[:3, :3])
-            cont = np.concatenate([Tm[:3, 3], q])
-            results.append((m, int(cost[m]), int(idx[m]), cont))
+        found = [m for m in range(K) if idx[m] >= 0]
+        conts = self.adjusted_cont_poses(win[found], np.array(found, np.int32), inp.use_external_pose_list)
+        results = [(m, int(cost[m]), int(idx[m]), conts[r]) for r, m in enumerate(found)]
+        if self.debug_dir is not None:
+            self._write_cost_dump(inp, n_total, lo, n, adj_all if n > 0 else None, pm if n > 0 else None, world, rank)
         t_end = time.perf_counter()
         # host-side breakdown of the last search (seconds): successor states (poses.txt + IsValidPose), per-state
         # inputs of the GPU call, the GPU search (launch .. synchronise, incl. the exchange), results
@@ -549,6 +554,69 @@ class ObjectRecognizer:
         self.last_stats = EnvStats(scenes_rendered=n_total, scenes_valid=0, time=time.perf_counter() - t0,
                                    icp_time=icp_time, peak_gpu_mem=peak_mb)
         return results
+
+    def adjusted_cont_poses(self, adj16: np.ndarray, model: np.ndarray, use_external_pose_list: int) -> np.ndarray:
+        """ComputeGreedyCostsInParallelGPU's adjusted ContPose of each state (search_env.cpp:1996-2019): the GPU-adjusted
+        mat4x4 -> to_eigen(100) (a Matrix4f); in 3-DoF cam_z_front * T * preprocess^-1 as float products; then
+        (T(0,3), T(1,3), T(2,3)) and Quaternionf of the float rotation block.  -> (N, 7) x y z qx qy qz qw."""
+        A = np.asarray(adj16, np.float32).reshape(-1, 4, 4).copy()
+        A[:, :3, :] = A[:, :3, :] / np.float32(100.0)
+        if use_external_pose_list != 1 and len(A):
+            cz = (self.camera_pose @ CAM_TO_BODY).astype(np.float32)
+            pinv = np.stack([np.linalg.inv(P).astype(np.float32) for P in self.preprocess])[np.asarray(model)]
+            A = matmul_lazy(matmul_lazy(np.broadcast_to(cz, A.shape), A), pinv)
+        q = quat_from_matrix_eigen_batch(A[:, :3, :3], np.float32)
+        return np.concatenate([A[:, :3, 3], q], 1).astype(np.float64)
+
+    def raw_model_to_scene(self, cont: np.ndarray, model: np.ndarray) -> np.ndarray:
+        """ObjectModel::GetRawModelToSceneTransform (object_model.cpp:502-510) of ContPoses (N, 7): GetTransform() (double:
+        translation * normalised quaternion) cast to float, times the float preprocessing transform.  -> (N, 4, 4)
+        float32."""
+        c = np.asarray(cont, np.float64).reshape(-1, 7)
+        if not len(c):
+            return np.zeros((0, 4, 4), np.float32)
+        T = pose_matrix_batch(c[:, :3], c[:, 3:7]).astype(np.float32)
+        pre = np.stack([P.astype(np.float32) for P in self.preprocess])[np.asarray(model)]
+        return matmul_lazy(T, pre)
+
+    def _write_cost_dump(self, inp, n_total, lo, n, adj, pm, world, rank):
+        """<debug_dir>/cost_dump.json as ComputeGreedyRenderPoses writes it (search_env.cpp:2540-2649): one entry per
+        candidate state whose cost is not -1 / -2, in candidate order -- id (the state's index), target_cost = (int) rc,
+        source_cost = (int) oc, total_cost = (int) (rc + oc), transform (GetRawModelToSceneTransform of the adjusted
+        pose, column-major), translation, quaternion (x y z w) and lie_rotation (Sophus SO3f log).  The costs are the
+        ones this search's argmin used, read back from the device outputs it already holds (no extra launch); with
+        several ranks the shards are gathered on rank 0, which writes the file."""
+        if n > 0:
+            rc, oc, _ = self._last_costs
+            adj_h, pm_h = adj.cpu().numpy(), pm.cpu().numpy()
+        else:
+            rc = oc = np.zeros(0, np.float32)
+            adj_h, pm_h = np.zeros((0, 16), np.float32), np.zeros(0, np.int32)
+        part = (lo, rc, oc, adj_h, pm_h)
+        if world > 1:
+            parts = [None] * world
+            torch.distributed.all_gather_object(parts, part)
+            if rank != 0:
+                return
+            parts.sort(key=lambda p: p[0])
+            lo, rc, oc, adj_h, pm_h = 0, *(np.concatenate([p[k] for p in parts]) for k in range(1, 5))
+        target, source = cvtt_i32(rc), cvtt_i32(oc)
+        total = cvtt_i32(np.asarray(rc, np.float32) + np.asarray(oc, np.float32))
+        cost = np.where(target < 0, -1, total)
+        keep = np.nonzero((cost != -1) & (cost != -2))[0]
+        cont = self.adjusted_cont_poses(adj_h[keep], pm_h[keep], inp.use_external_pose_list)
+        T = self.raw_model_to_scene(cont, pm_h[keep])
+        lie = so3_log_batch(quat_from_matrix_eigen_batch(T[:, :3, :3], np.float32), np.float32)
+        c32 = cont.astype(np.float32)
+        poses = []
+        for r, i in enumerate(keep):
+            poses.append({"id": int(lo + i), "target_cost": int(target[i]), "source_cost": int(source[i]),
+                          "total_cost": int(cost[i]),
+                          "transform": [float(v) for v in T[r].T.reshape(-1)],  # Eigen's column-major data()
+                          "translation": [float(v) for v in c32[r, :3]],
+                          "quaternion": [float(v) for v in c32[r, 3:7]],
+                          "lie_rotation": [float(v) for v in lie[r]]})
+        pio.write_cost_dump(os.path.join(self.debug_dir, "cost_dump.json"), poses)
 
     @property
     def _last_costs(self):
@@ -571,10 +639,10 @@ class ObjectRecognizer:
         LocalizeObjectsGreedyRender (object_recognizer.cpp:318-337): per detected object the raw-model-to-scene
         transform, the preprocessing transform, the pose and the model name."""
         out = LocalizationResult([], [], [], [], [], [], self.last_stats)
-        for m, cost, idx, cont in res:
+        raw = self.raw_model_to_scene(np.array([r[3] for r in res]).reshape(-1, 7), np.array([r[0] for r in res], np.int32))
+        for (m, cost, idx, cont), T in zip(res, raw):
             # GetRawModelToSceneTransform (object_model.cpp:502-510): ContPose transform * preprocessing
-            T = pose_matrix(cont[:3], cont[3:7]).astype(np.float32).astype(np.float64) @ self.preprocess[m]
-            out.object_transforms.append(T)
+            out.object_transforms.append(T.astype(np.float64))
             out.preprocessing_transforms.append(self.preprocess[m])
             out.detected_poses.append(cont)
             out.model_names.append(self.model_names[m])

@@ -6,9 +6,10 @@ covariances are numpy's (covariances: lexsort k-NN, eigh normal), the per-point 
 the solve is numpy.linalg.solve, the SE(3) exponential is scipy's matrix exponential of the twist, and the
 Levenberg-Marquardt control is LsqRegistration::step_lm / computeTransformation as published (lm_init_lambda_factor
 1e-9, lm_max_iterations 10, lambda *= max(1/3, 1 - (2 rho - 1)^3) on acceptance, nu doubling on rejection,
-is_converged on max(|dR - I| / rot_eps, |dt| / trans_eps) < 1).  Only the correspondence rule -- the spec's
-nearest target of the float query, which is a tie / rounding rule rather than algebra -- comes from the oracle
-(oracle.gicp_nn).
+is_converged on max(|dR - I| / rot_eps, |dt| / trans_eps) < 1).  The correspondence is its own too (nearest_exact:
+the float32 squared distance (dx dx + dy dy) + dz dz of every target, first strict minimum, as fast_gicp's brute-force
+k = 1 search ranks them), not the spec's centred FMA key; oracle.gicp_nn (the key rule the kernels run) is only used
+when a caller asks for it to measure how far the two rules lead apart (tools/nn_rule_divergence.py).
 """
 from __future__ import annotations
 
@@ -16,6 +17,25 @@ import numpy as np
 import scipy.linalg as sla
 
 import oracle
+
+
+def nearest_exact(q, tgt):
+    """Nearest target of every float query by the exact float32 squared distance ((dx dx + dy dy) + dz dz, no FMA),
+    the first (lowest-index) strict minimum; -1 for a non-finite query or when no target has a finite distance."""
+    q = np.asarray(q, np.float32).reshape(-1, 3)
+    t = np.asarray(tgt, np.float32).reshape(-1, 3)
+    out = np.full(len(q), -1, np.int32)
+    if len(t) == 0:
+        return out
+    with np.errstate(invalid="ignore", over="ignore"):
+        for a in range(0, len(q), 512):
+            d = q[a:a + 512, None, :] - t[None, :, :]
+            d2 = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+            d2 = np.where(np.isfinite(d2), d2, np.float32(np.inf))
+            j = np.argmin(d2, axis=1)
+            ok = np.isfinite(d2[np.arange(len(j)), j]) & np.isfinite(q[a:a + 512]).all(1)
+            out[a:a + 512] = np.where(ok, j, -1)
+    return out
 
 
 def covariances(xyz, k=oracle.GICP_K):
@@ -115,8 +135,9 @@ def is_converged(D, rot_eps, trans_eps):
 
 
 def gicp(src, src_cov, tgt, tgt_cov, max_iter=oracle.GICP_MAX_ITER, rot_eps=oracle.GICP_ROT_EPS,
-         trans_eps=oracle.GICP_TRANS_EPS):
-    """-> (T (4,4) float64, iterations) as LsqRegistration::computeTransformation from the identity guess."""
+         trans_eps=oracle.GICP_TRANS_EPS, nn=nearest_exact):
+    """-> (T (4,4) float64, iterations) as LsqRegistration::computeTransformation from the identity guess.  nn(q, tgt)
+    is the correspondence rule (default: the exact float distance; oracle.gicp_nn is the spec's key rule)."""
     Cs, Ct = sym3(src_cov), sym3(tgt_cov)
     T = np.eye(4)
     lam = -1.0
@@ -125,7 +146,7 @@ def gicp(src, src_cov, tgt, tgt_cov, max_iter=oracle.GICP_MAX_ITER, rot_eps=orac
         return T, 0
     while it < max_iter:
         it += 1
-        j = oracle.gicp_nn(query_f(T, src), tgt)
+        j = nn(query_f(T, src), tgt)
         H, b, y0, M, ok = linearize(T, src, Cs, tgt, Ct, j)
         if lam < 0.0:
             lam = 1e-9 * np.abs(np.diag(H)).max()

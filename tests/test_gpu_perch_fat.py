@@ -100,11 +100,37 @@ def test_perch_fat_one_process_matches_recognizer_and_parses(scene_dir):
     bank = {n: ModelMetaData(n, file=str(root / "models" / n / "textured.ply")) for n in NAMES}
     cam = CameraIntrinsics(sc.width, sc.height, sc.fx, sc.fy, sc.cx, sc.cy)
     rec = ObjectRecognizer(bank, cam, pf.perch_params(ps), 0)
+    os.makedirs(root / "api", exist_ok=True)
+    rec.debug_dir = str(root / "api")
     inp = RecognitionInput(NAMES, str(root / "depth.png"), str(root / "mask.png"), depth_factor=sc.depth_factor,
                            rendered_root_dir=str(root / "rendered"), use_icp=1)
     res = rec.localize_objects_greedy_render(inp)
     rec.write_outputs(res, str(root / "api"))
     assert (root / "api" / "output_poses.txt").read_bytes() == (out / "output_poses.txt").read_bytes()
+    # cost_dump.json (search_env.cpp:2540-2649, VERDICT r04 missing #3): same bytes from the executable and the API,
+    # and its costs are the rc / oc this search selected on
+    assert (root / "api" / "cost_dump.json").read_bytes() == (out / "cost_dump.json").read_bytes()
+    dump = io.read_cost_dump(str(out / "cost_dump.json"))
+    rc, oc, _ = rec._last_costs
+    tgt = np.trunc(rc).astype(np.int64)
+    src = np.trunc(oc).astype(np.int64)
+    tot = np.trunc(rc + oc).astype(np.int64)
+    valid = tgt >= 0
+    assert [e["id"] for e in dump] == np.nonzero(valid)[0].tolist()
+    ids = np.array([e["id"] for e in dump])
+    assert [e["target_cost"] for e in dump] == tgt[ids].tolist()
+    assert [e["source_cost"] for e in dump] == src[ids].tolist()
+    assert [e["total_cost"] for e in dump] == tot[ids].tolist()
+    by_id = {e["id"]: e for e in dump}
+    for k, i in enumerate(res.indices):  # the winners: output_poses' pose, transform and cost
+        e = by_id[i]
+        assert e["total_cost"] == res.costs[k]
+        assert np.array_equal(np.float32(e["translation"]), np.float32(res.detected_poses[k][:3]))
+        assert np.array_equal(np.float32(e["quaternion"]), np.float32(res.detected_poses[k][3:7]))
+        T = np.float32(e["transform"]).reshape(4, 4).T  # column-major
+        assert np.array_equal(T, np.float32(res.object_transforms[k]))
+        from scipy.spatial.transform import Rotation
+        assert np.abs(Rotation.from_rotvec(e["lie_rotation"]).as_matrix() - T[:3, :3]).max() < 1e-4
 
 
 def test_perch_fat_two_ranks_output_poses_identical(scene_dir):
@@ -118,3 +144,6 @@ def test_perch_fat_two_ranks_output_poses_identical(scene_dir):
     one = (root / "debug" / "scene_w1" / "output_poses.txt").read_bytes()
     two = (root / "debug" / "scene_w2" / "output_poses.txt").read_bytes()
     assert one and one == two, r.stdout[-2000:]
+    # rank 0 gathers the shards' costs and poses into one cost_dump.json, byte-identical to the one-process run
+    assert (root / "debug" / "scene_w1" / "cost_dump.json").read_bytes() == \
+        (root / "debug" / "scene_w2" / "cost_dump.json").read_bytes()

@@ -134,3 +134,69 @@ def test_batched_pose_building_matches_per_state():
     q = np.array([(0.0, 0.0, math.sin(normalize_angle_positive(y) / 2.0), math.cos(normalize_angle_positive(y) / 2.0))
                   for y in yaw])
     assert np.array_equal(pose_matrix_batch(xyz, q), np.stack([yaw_pose_matrix(*xyz[i], yaw[i]) for i in range(n)]))
+
+
+def test_quaternion_from_matrix_is_eigens_algorithm():
+    """quat_from_matrix_eigen_batch (Eigen::Quaternion(Matrix3), both branches, float and double) against scipy's
+    rotation-to-quaternion up to sign and rounding, and branch by branch against a scalar transcription."""
+    from scipy.spatial.transform import Rotation
+
+    from perception_amd.model import quat_from_matrix_eigen_batch
+
+    rng = np.random.default_rng(3)
+    R = Rotation.random(4000, random_state=4).as_matrix()
+    R[:4] = [np.eye(3), np.diag([1.0, -1.0, -1.0]), np.diag([-1.0, 1.0, -1.0]), np.diag([-1.0, -1.0, 1.0])]
+    for dt, tol in ((np.float64, 1e-12), (np.float32, 3e-7)):
+        q = quat_from_matrix_eigen_batch(R, dt)
+        assert q.dtype == dt
+        ref = Rotation.from_matrix(R).as_quat()  # x y z w
+        sgn = np.sign(np.sum(q * ref, 1))[:, None]
+        assert np.abs(q - sgn * ref).max() < tol * 10
+    # the non-positive-trace branch picks the first largest diagonal entry (Eigen's i, j, k)
+    m = np.array([[-0.5, 0.0, 0.0], [0.0, -0.5, 0.0], [0.0, 0.0, 0.0]])
+    tr = m.trace()
+    assert tr <= 0
+    q = quat_from_matrix_eigen_batch(m[None], np.float64)[0]
+    t = np.sqrt(((m[2, 2] - m[0, 0]) - m[1, 1]) + 1.0)
+    assert q[2] == 0.5 * t and q[3] == (m[1, 0] - m[0, 1]) * (0.5 / t)
+
+
+def test_so3_log_matches_rotation_vectors():
+    from scipy.spatial.transform import Rotation
+
+    from perception_amd.model import so3_log_batch
+
+    q = Rotation.random(2000, random_state=8).as_quat()
+    q = q * np.where(q[:, 3:] < 0, -1.0, 1.0)  # w >= 0: the rotation vector of angle <= pi
+    q[0] = [0.0, 0.0, 0.0, 1.0]          # identity: the small-angle branch
+    q[1] = [1e-7, 0.0, 0.0, 1.0]
+    q[2] = [0.0, 1.0, 0.0, 1e-7]         # ~pi about y: |w| < eps, +pi / n
+    want = Rotation.from_quat(q).as_rotvec()
+    got = so3_log_batch(q.astype(np.float32), np.float32).astype(np.float64)
+    assert np.abs(got - want).max() < 2e-5
+    assert np.abs(got[2] - [0.0, np.pi, 0.0]).max() < 1e-6
+    # w = 0 exactly takes -pi / n (Sophus: w > 0 is false)
+    assert np.abs(so3_log_batch(np.array([[0.0, 1.0, 0.0, 0.0]]))[0] - [0.0, -np.pi, 0.0]).max() < 1e-6
+
+
+def test_cvtt_i32_is_x86_truncation():
+    from perception_amd.recognizer import cvtt_i32
+
+    x = np.array([1.9, -1.9, -0.5, 0.0, 99.99, np.nan, np.inf, -np.inf, 3e9, -3e9, -1.0], np.float32)
+    assert cvtt_i32(x).tolist() == [1, -1, 0, 0, 99, -2**31, -2**31, -2**31, -2**31, -2**31, -1]
+
+
+def test_cost_dump_format(tmp_path):
+    """cost_dump.json as nlohmann::json prints it with setw(4): sorted keys, four-space indent, trailing newline."""
+    from perception_amd import io as pio
+
+    p = tmp_path / "cost_dump.json"
+    entry = {"id": 3, "target_cost": 4, "source_cost": 7, "total_cost": 11, "transform": [1.0] * 16,
+             "translation": [0.1, 0.2, 0.8], "quaternion": [0.0, 0.0, 0.0, 1.0], "lie_rotation": [0.0, 0.0, 0.0]}
+    pio.write_cost_dump(str(p), [entry])
+    text = p.read_text()
+    assert text.startswith('{\n    "poses": [\n        {\n            "id": 3,\n            "lie_rotation": [\n')
+    assert text.endswith("}\n")
+    assert pio.read_cost_dump(str(p)) == [entry]
+    pio.write_cost_dump(str(p), [])
+    assert p.read_text() == '{\n    "poses": []\n}\n'

@@ -38,5 +38,5 @@ cat $OUT/bench_$TAG.json
 echo "== rocprof stats"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python bench.py --no-cpu ${BENCH_ARGS} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -20 $OUT/prof_$TAG.err; exit 1; }
 cat $OUT/prof_bench_$TAG.json
-python tools/trace_busy.py $OUT/prof_$TAG/run_kernel_trace.csv "fused_cost_kernel<8" $OUT/trace_busy_$TAG.json || exit 1
+python tools/trace_busy.py $OUT/prof_$TAG/run_kernel_trace.csv --last ${STEPS:-20} --sq profiles/sq_counters.json --out $OUT/trace_busy_$TAG.json --stats-out $OUT/c2_kernel_stats_$TAG.csv || exit 1
 find $OUT -path "*_$TAG*" -name "*.csv" | head -20
