@@ -230,7 +230,6 @@ def _gicp_lib():
         L.orc_gicp_linearize.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, _f64p, c_int, _i32p, _f64p]
         L.orc_gicp_se3_exp.argtypes = [_f64p, _f64p]
         L.orc_gicp_lm_solve.argtypes = [_f64p, c_double, _f64p]
-        L.orc_gicp_lm_solve_swaps.argtypes = [_f64p, c_double, _f64p]
         L.orc_sin_d.restype = c_double
         L.orc_sin_d.argtypes = [c_double]
         L.orc_cos_d.restype = c_double
@@ -313,13 +312,12 @@ def gicp_lm_solve(H, b, lam):
     return d
 
 
-def gicp_lm_solve_sys(sys, lam, swaps=False):
-    """The damped solve of a raw 28-term system (upper H row-major, b, error): pcore_gicp_math.h lm_solve (the
-    kernels' pivot-order-first form) or, with swaps=True, lm_solve_swaps (Eigen's in-place swaps)."""
+def gicp_lm_solve_sys(sys, lam):
+    """The damped solve of a raw 28-term system (upper H row-major, b, error): pcore_gicp_math.h lm_solve_schur, the
+    kernels' solve."""
     sys = np.ascontiguousarray(sys, np.float64).reshape(28)
     d = np.zeros(6, np.float64)
-    L = _gicp_lib()
-    (L.orc_gicp_lm_solve_swaps if swaps else L.orc_gicp_lm_solve)(sys, float(lam), d)
+    _gicp_lib().orc_gicp_lm_solve(sys, float(lam), d)
     return d
 
 

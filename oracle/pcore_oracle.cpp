@@ -646,7 +646,7 @@ int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double&
     for (int trial = 0; trial < gm::kLmMaxTrials; trial++) {
         if (trials) *trials = trial + 1;
         double d[6];
-        gm::lm_solve(sys, lambda, d);
+        gm::lm_solve_schur(sys, lambda, d);
         if (!gm::all_finite6(d)) return gm::kLmFailed;
         double Rd[3][3], td[3];
         gm::se3_exp(d, Rd, td);
@@ -874,8 +874,8 @@ void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, con
     out_sys[27] = (double)err;
 }
 
-// The step's pieces, for the CPU tests of the spec: se3_exp -> 4x4 row-major; the damped LDLT solve of a 28-term
-// system; the double sin / cos.
+// The step's pieces, for the CPU tests of the spec: se3_exp -> 4x4 row-major; the damped solve of a 28-term system
+// (lm_solve_schur); the double sin / cos.
 void orc_gicp_se3_exp(const double* a6, double* out_T) {
     const double a[6] = {a6[0], a6[1], a6[2], a6[3], a6[4], a6[5]};
     double Rd[3][3], td[3];
@@ -889,13 +889,7 @@ void orc_gicp_se3_exp(const double* a6, double* out_T) {
 
 void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d) {
     double d[6];
-    pcore::gicpm::lm_solve(sys, lambda, d);
-    for (int a = 0; a < 6; a++) out_d[a] = d[a];
-}
-// Eigen's in-place LDLT with its row / column swaps (the restatement lm_solve is held to)
-void orc_gicp_lm_solve_swaps(const double* sys, double lambda, double* out_d) {
-    double d[6];
-    pcore::gicpm::lm_solve_swaps(sys, lambda, d);
+    pcore::gicpm::lm_solve_schur(sys, lambda, d);
     for (int a = 0; a < 6; a++) out_d[a] = d[a];
 }
 

@@ -108,8 +108,9 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
  *    of the float squared distance (larger segments); Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I];
  *    H, b and the error e^T M e reduced in the GPU's fixed order (64 per-lane sequential partials, then the wave
  *    shuffle-down tree);
- *  - Levenberg-Marquardt (LsqRegistration::step_lm): lambda0 = 1e-9 max|diag H|, <= 10 trials of Eigen's pivoted
- *    LDLT of H + lambda I, se3_exp (exact so3_exp + V rho), errors of the trials with the iteration's
+ *  - Levenberg-Marquardt (LsqRegistration::step_lm): lambda0 = 1e-9 max|diag H|, <= 10 trials of the damped solve
+ *    of H + lambda I (3x3 block elimination of the translation block, lm_solve_schur; fast_gicp uses Eigen's LDLT),
+ *    se3_exp (exact so3_exp + V rho), errors of the trials with the iteration's
  *    correspondences, accept / reject by rho, lambda update; stop on a converged step
  *    (max(|dR - I| / rot_eps, |dt| / trans_eps) < 1), ten rejections or max_iter iterations.
  * Covariances: double[6] (xx, xy, xz, yy, yz, zz) per point. */
@@ -131,11 +132,10 @@ int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const fl
 void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz,
                         const double* tgt_cov, int nt, const double* T, int textbook, int32_t* out_corr,
                         double* out_sys);
-/* Pieces of the step for the CPU spec tests: se3_exp(a6) -> 4x4; d = LDLT(H + lambda I).solve(-b) of a 28-term
- * system; the double sin / cos of pcore_dmath.h; the spec's correspondences of n float queries. */
+/* Pieces of the step for the CPU spec tests: se3_exp(a6) -> 4x4; d = (H + lambda I)^-1 (-b) of a 28-term system
+ * (lm_solve_schur); the double sin / cos of pcore_dmath.h; the spec's correspondences of n float queries. */
 void orc_gicp_se3_exp(const double* a6, double* out_T);
 void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d);
-void orc_gicp_lm_solve_swaps(const double* sys, double lambda, double* out_d);
 double orc_sin_d(double x);
 double orc_cos_d(double x);
 double orc_cube_rn(double u);   // step_lm's std::pow(u, 3), rounded once

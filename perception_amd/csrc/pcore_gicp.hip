@@ -13,8 +13,8 @@
 //                      k-NN of every point inside its segment (candidates staged through LDS), double
 //                      mean / covariance, 6-sweep Jacobi, PLANE regularisation.
 //   gicp_kernel        one wave per pose: per-lane sequential partial sums of J^T M J / J^T M e / e^T M e,
-//                      the shuffle-down tree in registers (wave_tree_sums), the LM iteration (the damped solve
-//                      with a row per lane, the rest uniform), the correspondence history, then
+//                      the shuffle-down tree in registers (wave_tree_sums), the LM iteration (uniform: the
+//                      damped solve by 3x3 block elimination, se3_exp, the trial), the correspondence history, then
 //                      concatenate_transforms (renderer.cu:1412-1429).
 //   gicp_wide_kernel   small batches: eight waves search a pose's correspondences, wave 0 as gicp_kernel.
 #include "pcore_internal.h"
@@ -736,7 +736,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
     for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
         GPROF_T(p0);
         double d[6];
-        gicpm::lm_solve_rows(sys, lambda, d);
+        gicpm::lm_solve_schur(sys, lambda, d);
 #pragma unroll
         for (int a = 0; a < 6; a++) d[a] = uniform_d(d[a]);
         GPROF_TD(p1, d[5]);
@@ -1084,12 +1084,12 @@ extern "C" int pcore_debug_gicp_profile(unsigned long long* out, int reset) {
 }
 #endif
 
-// Test hook of the kernels' damped solve (gicpm::lm_solve_rows): one wave per 28-term system.
+// Test hook of the kernels' damped solve (gicpm::lm_solve_schur): one wave per 28-term system.
 __global__ void __launch_bounds__(64) lm_solve_test_kernel(const double* sys, const double* lambda, double* out, int n) {
     const int i = blockIdx.x;
     if (i >= n) return;
     double d[6];
-    gicpm::lm_solve_rows(sys + (size_t)gicpm::kTerms * i, lambda[i], d);
+    gicpm::lm_solve_schur(sys + (size_t)gicpm::kTerms * i, lambda[i], d);
     if (threadIdx.x == 0)
         for (int a = 0; a < 6; a++) out[(size_t)6 * i + a] = d[a];
 }

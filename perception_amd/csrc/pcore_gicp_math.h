@@ -14,8 +14,9 @@
 //   terms           H += J^T M J (upper triangle), b += J^T M e, y += e^T M e
 // The products with J's structural zeros and -1 entries are not evaluated: J^T v for a 3-vector v is
 //   (q2 v1 - q1 v2, q0 v2 - q2 v0, q1 v0 - q0 v1, -v0, -v1, -v2).
-// Per iteration (LsqRegistration::step_lm, so3.hpp se3_exp, Eigen's LDLT and Quaternion::toRotationMatrix):
-//   lambda <- 1e-9 max|diag H| on the first iteration; up to 10 trials of d = LDLT(H + lambda I).solve(-b),
+// Per iteration (LsqRegistration::step_lm, so3.hpp se3_exp, Quaternion::toRotationMatrix):
+//   lambda <- 1e-9 max|diag H| on the first iteration; up to 10 trials of d = (H + lambda I)^-1 (-b) (lm_solve_schur:
+//   fast_gicp solves with Eigen's LDLT; the spec eliminates the translation block with 3x3 adjugates),
 //   delta = se3_exp(d), x_i = delta x, y_i = sum e^T M e at x_i with the iteration's correspondences and M,
 //   rho = (y - y_i) / d.(lambda d - b); rho < 0 rejects (stop if delta is converged, else lambda *= nu, nu *= 2),
 //   otherwise x <- x_i and lambda *= max(1/3, 1 - (2 rho - 1)^3).  The search stops when a step is converged
@@ -105,8 +106,8 @@ constexpr int kErr = 27;
 PCORE_GHD constexpr int hdiag(int a) { return a * 6 - (a * (a - 1)) / 2; }
 
 // Lane-parallel evaluation of a few uniform operations (device only).  The LM step is uniform work that every
-// lane of the wave repeats; where it holds several independent IEEE divisions (a pivot column of the LDLT, the
-// pseudo-inverse of D, se3_exp's three quotients) or several sin / cos, lane i evaluates the i-th one in a single
+// lane of the wave repeats; where it holds several independent IEEE divisions (se3_exp's three quotients) or
+// several sin / cos, lane i evaluates the i-th one in a single
 // instruction sequence and the results return through v_readlane.  Every lane still performs the same IEEE
 // operation on the same operands as the scalar code, so the results are bit-identical to the host's (the oracle
 // runs the scalar path).
@@ -140,12 +141,8 @@ PCORE_UNROLL
     if constexpr (N > 4) q[4] = read_lane_d<4>(r);
     if constexpr (N > 5) q[5] = read_lane_d<5>(r);
 }
-// a value every lane holds equally, moved to an SGPR: branches on it are scalar branches (the LDLT's pivot
-// swaps run as one taken block instead of a select chain over every candidate block)
-__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 #else
 #define PCORE_LANE_PAR 0
-inline int uniform_i(int v) { return v; }
 #endif
 
 // e^T M e with M given by its upper triangle (xx, xy, xz, yy, yz, zz): Me row by row, then the dot product
@@ -252,439 +249,42 @@ PCORE_UNROLL
     return kLmInitFactor * m;
 }
 
-// d = LDLT(H + lambda I).solve(-b), Eigen's LDLT<Matrix6d, Lower> (ldlt_inplace::unblocked + _solve_impl):
-// diagonal pivoting on the largest |A_kk| (first on ties), the pivot row / column swapped on the lower triangle,
-// column k updated with temp_j = D_j L_kj and divided by the pivot; a zero first pivot leaves L = I; the solve
-// permutes, runs the unit-lower forward substitution, divides by D (|D_i| <= DBL_MIN gives 0), runs the unit-upper
-// back substitution and permutes back.  Sums run in index order.  sys: 28 terms (upper H row-major, b).
-// WAVE: every lane of the wave solves the same system (the pivots move to SGPRs, the independent divisions run
-// lane-parallel); WAVE = false: each lane (or the host) solves its own system.
-template <bool WAVE = (PCORE_LANE_PAR != 0)>
-PCORE_GHD void lm_solve_swaps(const double* sys, double lambda, double (&d)[6]) {
-    double A[6][6];
-    {
-        int h = 0;
-PCORE_UNROLL
-        for (int a = 0; a < 6; a++)
-PCORE_UNROLL
-            for (int c = a; c < 6; c++) {
-                A[c][a] = a == c ? sys[h] + lambda : sys[h];  // lower triangle of H + lambda I (the upper is unused)
-                h++;
-            }
-    }
-    int tr[6];
-    bool zero = false;
-PCORE_UNROLL
-    for (int k = 0; k < 6; k++) {
-        int p = k;
-        double big = __builtin_fabs(A[k][k]);
-PCORE_UNROLL
-        for (int i = k + 1; i < 6; i++) {
-            const double v = __builtin_fabs(A[i][i]);
-            if (v > big) { big = v; p = i; }
-        }
-        if constexpr (WAVE) p = uniform_i(p);  // identical on every lane
-        tr[k] = p;
-PCORE_UNROLL
-        for (int c = k + 1; c < 6; c++)
-            if (p == c) {
-PCORE_UNROLL
-                for (int j = 0; j < k; j++) { const double x = A[k][j]; A[k][j] = A[c][j]; A[c][j] = x; }
-PCORE_UNROLL
-                for (int i = c + 1; i < 6; i++) { const double x = A[i][k]; A[i][k] = A[i][c]; A[i][c] = x; }
-                { const double x = A[k][k]; A[k][k] = A[c][c]; A[c][c] = x; }
-PCORE_UNROLL
-                for (int i = k + 1; i < c; i++) { const double x = A[i][k]; A[i][k] = A[c][i]; A[c][i] = x; }
-            }
-        if (k > 0) {
-            double temp[6];
-PCORE_UNROLL
-            for (int j = 0; j < k; j++) temp[j] = A[j][j] * A[k][j];
-            double s = A[k][0] * temp[0];
-PCORE_UNROLL
-            for (int j = 1; j < k; j++) s = s + A[k][j] * temp[j];
-            A[k][k] = A[k][k] - s;
-PCORE_UNROLL
-            for (int i = k + 1; i < 6; i++) {
-                double w = A[i][0] * temp[0];
-PCORE_UNROLL
-                for (int j = 1; j < k; j++) w = w + A[i][j] * temp[j];
-                A[i][k] = A[i][k] - w;
-            }
-        }
-        const double akk = A[k][k];
-        const bool valid = WAVE ? uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0 : __builtin_fabs(akk) > 0.0;
-        if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
-            zero = true;
-            break;
-        }
-        if (valid) {
-#if PCORE_LANE_PAR
-            if (WAVE && k < 5) {
-                constexpr int MAXN = 5;
-                double num[MAXN], den[MAXN], q[MAXN];
-PCORE_UNROLL
-                for (int i = 0; i < MAXN; i++) {
-                    num[i] = k + 1 + i < 6 ? A[k + 1 + i < 6 ? k + 1 + i : 5][k] : 0.0;
-                    den[i] = akk;
-                }
-                lane_div<MAXN>(num, den, q);
-PCORE_UNROLL
-                for (int i = k + 1; i < 6; i++) A[i][k] = q[i - k - 1];
-            } else if (!WAVE)
-#endif
-            {
-PCORE_UNROLL
-                for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
-            }
-        }
-    }
-    double x[6];
-PCORE_UNROLL
-    for (int i = 0; i < 6; i++) x[i] = -sys[21 + i];
-    if (zero) {
-        // D = the (zero) diagonal: every row is set to zero by the pseudo-inverse
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) d[i] = 0.0;
-        return;
-    }
-PCORE_UNROLL
-    for (int k = 0; k < 6; k++)
-PCORE_UNROLL
-        for (int c = k + 1; c < 6; c++)
-            if (tr[k] == c) { const double v = x[k]; x[k] = x[c]; x[c] = v; }
-PCORE_UNROLL
-    for (int j = 0; j < 6; j++)
-PCORE_UNROLL
-        for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
-#if PCORE_LANE_PAR
-    if constexpr (WAVE) {
-        double Dd[6], q[6];
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) Dd[i] = A[i][i];
-        lane_div<6>(x, Dd, q);
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) x[i] = __builtin_fabs(Dd[i]) > 2.2250738585072014e-308 ? q[i] : 0.0;
-    } else
-#endif
-    {
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) {
-            const double Di = A[i][i];
-            x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
-        }
-    }
-PCORE_UNROLL
-    for (int i = 4; i >= 0; i--) {
-        double s = A[i + 1][i] * x[i + 1];
-PCORE_UNROLL
-        for (int j = i + 2; j < 6; j++) s = s + A[j][i] * x[j];
-        x[i] = x[i] - s;
-    }
-PCORE_UNROLL
-    for (int k = 5; k >= 0; k--)
-PCORE_UNROLL
-        for (int c = k + 1; c < 6; c++)
-            if (tr[k] == c) { const double v = x[k]; x[k] = x[c]; x[c] = v; }
-PCORE_UNROLL
-    for (int i = 0; i < 6; i++) d[i] = x[i];
+// fused products of the solve: fma is correctly rounded on the GPU (v_fma_f64) and on the host (glibc fma), so the
+// kernels and the oracle evaluate these expressions bit for bit
+PCORE_GHD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
+// a0 b0 + a1 b1 + a2 b2 as fma(a0, b0, fma(a1, b1, a2 b2))
+PCORE_GHD double dot3f(double a0, double a1, double a2, double b0, double b1, double b2) {
+    return fma_d(a0, b0, fma_d(a1, b1, a2 * b2));
 }
-
-// The same solve, bit for bit, with the pivot order found first (the one the kernels run).  Eigen's LDLT is left-
-// looking: when step k searches the diagonal of the unfactored corner for its pivot, those entries are still the
-// original ones (each is updated only at its own step), and every earlier swap only moves values.  So the whole pivot
-// sequence is a selection on |diag(H + lambda I)| -- at step k the first maximum of positions k..5, then the swap --
-// and the factorisation is that of P (H + lambda I) P^T without pivoting: entry (i, j) of the swapped lower triangle
-// is the symmetric matrix's (perm[i], perm[j]), and row perm[i]'s L entries are computed from the same values in the
-// same order wherever the row sat meanwhile.  That replaces the swaps of 21 stored entries per step by a gather of the
-// permuted matrix (one read of sys per entry: from LDS in the kernels) and permutes the right-hand side and the
-// result instead.  tests/test_gicp_spec.py holds this to lm_solve_swaps on random, tied, zero and non-finite systems.
-PCORE_GHD constexpr int hidx(int a, int b) { return a <= b ? hdiag(a) + (b - a) : hdiag(b) + (a - b); }
-
-template <bool WAVE = (PCORE_LANE_PAR != 0)>
-PCORE_GHD void lm_solve(const double* sys, double lambda, double (&d)[6]) {
-    int perm[6];
-    {
-        double mag[6];
-PCORE_UNROLL
-        for (int a = 0; a < 6; a++) {
-            mag[a] = __builtin_fabs(sys[hdiag(a)] + lambda);
-            perm[a] = a;
-        }
-PCORE_UNROLL
-        for (int k = 0; k < 5; k++) {
-            int p = k;
-            double big = mag[k];
-PCORE_UNROLL
-            for (int i = k + 1; i < 6; i++) {
-                const double v = mag[i];
-                if (v > big) { big = v; p = i; }
-            }
-            if constexpr (WAVE) p = uniform_i(p);  // identical on every lane
-PCORE_UNROLL
-            for (int c = k + 1; c < 6; c++)
-                if (p == c) {
-                    const double m = mag[k]; mag[k] = mag[c]; mag[c] = m;
-                    const int q = perm[k]; perm[k] = perm[c]; perm[c] = q;
-                }
-        }
-    }
-    // the permuted lower triangle of H + lambda I
-    double A[6][6];
-PCORE_UNROLL
-    for (int i = 0; i < 6; i++)
-PCORE_UNROLL
-        for (int j = 0; j <= i; j++) A[i][j] = i == j ? sys[hdiag(perm[i])] + lambda : sys[hidx(perm[i], perm[j])];
-    bool zero = false;
-PCORE_UNROLL
-    for (int k = 0; k < 6; k++) {
-        if (k > 0) {
-            double temp[6];
-PCORE_UNROLL
-            for (int j = 0; j < k; j++) temp[j] = A[j][j] * A[k][j];
-            double s = A[k][0] * temp[0];
-PCORE_UNROLL
-            for (int j = 1; j < k; j++) s = s + A[k][j] * temp[j];
-            A[k][k] = A[k][k] - s;
-PCORE_UNROLL
-            for (int i = k + 1; i < 6; i++) {
-                double w = A[i][0] * temp[0];
-PCORE_UNROLL
-                for (int j = 1; j < k; j++) w = w + A[i][j] * temp[j];
-                A[i][k] = A[i][k] - w;
-            }
-        }
-        const double akk = A[k][k];
-        const bool valid = WAVE ? uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0 : __builtin_fabs(akk) > 0.0;
-        if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
-            zero = true;
-            break;
-        }
-        if (valid) {
-#if PCORE_LANE_PAR
-            if (WAVE && k < 5) {
-                constexpr int MAXN = 5;
-                double num[MAXN], den[MAXN], q[MAXN];
-PCORE_UNROLL
-                for (int i = 0; i < MAXN; i++) {
-                    num[i] = k + 1 + i < 6 ? A[k + 1 + i < 6 ? k + 1 + i : 5][k] : 0.0;
-                    den[i] = akk;
-                }
-                lane_div<MAXN>(num, den, q);
-PCORE_UNROLL
-                for (int i = k + 1; i < 6; i++) A[i][k] = q[i - k - 1];
-            } else if (!WAVE)
-#endif
-            {
-PCORE_UNROLL
-                for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
-            }
-        }
-    }
-    if (zero) {
-        // D = the (zero) diagonal: every row is set to zero by the pseudo-inverse
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) d[i] = 0.0;
-        return;
-    }
-    double x[6];
-PCORE_UNROLL
-    for (int i = 0; i < 6; i++) x[i] = -sys[21 + perm[i]];  // P (-b)
-PCORE_UNROLL
-    for (int j = 0; j < 6; j++)
-PCORE_UNROLL
-        for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
-#if PCORE_LANE_PAR
-    if constexpr (WAVE) {
-        double Dd[6], q[6];
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) Dd[i] = A[i][i];
-        lane_div<6>(x, Dd, q);
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) x[i] = __builtin_fabs(Dd[i]) > 2.2250738585072014e-308 ? q[i] : 0.0;
-    } else
-#endif
-    {
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) {
-            const double Di = A[i][i];
-            x[i] = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
-        }
-    }
-PCORE_UNROLL
-    for (int i = 4; i >= 0; i--) {
-        double s = A[i + 1][i] * x[i + 1];
-PCORE_UNROLL
-        for (int j = i + 2; j < 6; j++) s = s + A[j][i] * x[j];
-        x[i] = x[i] - s;
-    }
-    // P^T x: d[perm[i]] = x[i]
-PCORE_UNROLL
-    for (int a = 0; a < 6; a++) {
-        double v = x[0];
-PCORE_UNROLL
-        for (int i = 1; i < 6; i++) v = perm[i] == a ? x[i] : v;
-        d[a] = v;
-    }
-}
-
-#if PCORE_LANE_PAR
-// lm_solve with row i of the permuted system on lane i (device only; lanes 6-63 shadow row 5 and are ignored).  Every
-// entry sees the operations of lm_solve in the same order -- row k's L entries and the diagonal D come to every lane by
-// v_readlane where another row needs them, a row's updates run on its own lane instead of on every lane in turn, and
-// each column's divisions are one division sequence -- so the result is lm_solve's bit for bit (the uniform d on every
-// lane).  tests/test_gpu_gicp_solve.py holds it to the oracle's lm_solve on random, tied, zero and non-finite systems.
-__device__ __forceinline__ double read_lane_k(double v, int k) {
-    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, k);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), k);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ void lm_solve_rows(const double* sys, double lambda, double (&d)[6]) {
-    const int lane = lane_index();
-    const int r = lane < 6 ? lane : 5;
-    int perm[6];
-    {
-        double mag[6];
-PCORE_UNROLL
-        for (int a = 0; a < 6; a++) {
-            mag[a] = __builtin_fabs(sys[hdiag(a)] + lambda);
-            perm[a] = a;
-        }
-PCORE_UNROLL
-        for (int k = 0; k < 5; k++) {
-            int p = k;
-            double big = mag[k];
-PCORE_UNROLL
-            for (int i = k + 1; i < 6; i++) {
-                const double v = mag[i];
-                if (v > big) { big = v; p = i; }
-            }
-            p = uniform_i(p);
-PCORE_UNROLL
-            for (int c = k + 1; c < 6; c++)
-                if (p == c) {
-                    const double m = mag[k]; mag[k] = mag[c]; mag[c] = m;
-                    const int q = perm[k]; perm[k] = perm[c]; perm[c] = q;
-                }
-        }
-    }
-    int pr = perm[0];
-PCORE_UNROLL
-    for (int i = 1; i < 6; i++) pr = r == i ? perm[i] : pr;
-    // this lane's row of the permuted lower triangle (entries past the diagonal are never read)
-    double A[6];
-PCORE_UNROLL
-    for (int j = 0; j < 6; j++) {
-        const double v = sys[hidx(pr, perm[j])];
-        A[j] = j == r ? v + lambda : v;
-    }
-    double D[6];  // the factored diagonal, uniform
-    bool zero = false;
-PCORE_UNROLL
-    for (int k = 0; k < 6; k++) {
-        double akk;
-        if (k > 0) {
-            double temp[6];
-PCORE_UNROLL
-            for (int j = 0; j < k; j++) temp[j] = D[j] * read_lane_k(A[j], k);
-            // row k's diagonal (uniform) ...
-            double s = read_lane_k(A[0], k) * temp[0];
-PCORE_UNROLL
-            for (int j = 1; j < k; j++) s = s + read_lane_k(A[j], k) * temp[j];
-            akk = read_lane_k(A[k], k) - s;
-            // ... and the rows below it, each on its lane
-            double w = A[0] * temp[0];
-PCORE_UNROLL
-            for (int j = 1; j < k; j++) w = w + A[j] * temp[j];
-            A[k] = r > k ? A[k] - w : (r == k ? akk : A[k]);
-        } else {
-            akk = read_lane_k(A[0], 0);
-        }
-        D[k] = akk;
-        const bool valid = uniform_i(__builtin_fabs(akk) > 0.0 ? 1 : 0) != 0;
-        if (k == 0 && !valid) {  // the whole diagonal is zero: L = I, identity transpositions
-            zero = true;
-            break;
-        }
-        if (valid && k < 5) {
-            const double q = A[k] / akk;
-            A[k] = r > k ? q : A[k];
-        }
-    }
-    if (zero) {
-PCORE_UNROLL
-        for (int i = 0; i < 6; i++) d[i] = 0.0;
-        return;
-    }
-    double x = -sys[21 + pr];  // P (-b), this lane's entry
-PCORE_UNROLL
-    for (int j = 0; j < 5; j++) {
-        const double xj = read_lane_k(x, j);
-        if (r > j) x = x - xj * A[j];
-    }
-    {
-        const double Di = A[r];  // lane r's diagonal entry
-        x = __builtin_fabs(Di) > 2.2250738585072014e-308 ? x / Di : 0.0;
-    }
-    double xs[6];
-    xs[5] = read_lane_k(x, 5);
-PCORE_UNROLL
-    for (int i = 4; i >= 0; i--) {
-        const double p = A[i] * x;  // lane j > i: A[j][i] x[j]
-        double s = read_lane_k(p, i + 1);
-PCORE_UNROLL
-        for (int j = i + 2; j < 6; j++) s = s + read_lane_k(p, j);
-        xs[i] = read_lane_k(x, i) - s;
-        if (r == i) x = xs[i];
-    }
-PCORE_UNROLL
-    for (int a = 0; a < 6; a++) {
-        double v = xs[0];
-PCORE_UNROLL
-        for (int i = 1; i < 6; i++) v = perm[i] == a ? xs[i] : v;
-        d[a] = v;
-    }
-}
-#else
-// host pass / plain C++ (the oracle): the scalar solve it restates
-PCORE_GHD void lm_solve_rows(const double* sys, double lambda, double (&d)[6]) { lm_solve<false>(sys, lambda, d); }
-#endif
 
 // Adjugate (upper: 00 01 02 11 12 22) and determinant of a symmetric 3x3 given by its upper triangle (same order)
 PCORE_GHD void adj_sym3(const double (&m)[6], double (&a)[6], double& det) {
-    a[0] = m[3] * m[5] - m[4] * m[4];
-    a[1] = m[2] * m[4] - m[1] * m[5];
-    a[2] = m[1] * m[4] - m[2] * m[3];
-    a[3] = m[0] * m[5] - m[2] * m[2];
-    a[4] = m[1] * m[2] - m[0] * m[4];
-    a[5] = m[0] * m[3] - m[1] * m[1];
-    det = m[0] * a[0] + m[1] * a[1] + m[2] * a[2];
+    a[0] = fma_d(m[3], m[5], -(m[4] * m[4]));
+    a[1] = fma_d(m[2], m[4], -(m[1] * m[5]));
+    a[2] = fma_d(m[1], m[4], -(m[2] * m[3]));
+    a[3] = fma_d(m[0], m[5], -(m[2] * m[2]));
+    a[4] = fma_d(m[1], m[2], -(m[0] * m[4]));
+    a[5] = fma_d(m[0], m[3], -(m[1] * m[1]));
+    det = dot3f(m[0], m[1], m[2], a[0], a[1], a[2]);
 }
-PCORE_GHD constexpr int s3(int i, int j) { return i <= j ? (i == 0 ? j : i == 1 ? 2 + j : 5) : s3(j, i); }
 
-// d = (H + lambda I)^-1 (-b) by the 3x3 block elimination of the translation block (the candidate spec of the damped
-// solve): with H = [[A, B], [B^T, C]] (A rotation, C translation, both + lambda I) and r = -b,
+// d = (H + lambda I)^-1 (-b) by the 3x3 block elimination of the translation block: with
+// H = [[A, B], [B^T, C]] (A rotation, C translation, both + lambda I) and r = -b,
 //   adj(C), det(C) = dC;  P = B adj(C);  S~ = dC A - P B^T (= dC times the Schur complement, upper triangle);
 //   u~ = dC r_rot - P r_trans;  x_rot = adj(S~) u~ / det(S~);  x_trans = adj(C) (r_trans - B^T x_rot) / dC,
-// every sum in index order.  H + lambda I is positive definite whenever it is not zero (H is a sum of J^T M J with M
-// positive definite, lambda = 1e-9 max|H_aa| > 0 unless H = 0): a zero diagonal gives d = 0 (Eigen's LDLT of the zero
-// matrix); a non-finite system gives a non-finite d, which stops the pose (lm_iteration's guard).  The dependent
-// chain is two adjugates, two 3-term products and two divisions deep, against the LDLT's six pivot steps.
+// the 3-term sums as fma chains (dot3f).  H + lambda I is positive definite whenever it is not zero (H is a sum of
+// J^T M J with M positive definite, lambda = 1e-9 max|H_aa| > 0 unless H = 0): a zero diagonal gives d = 0 (Eigen's
+// LDLT of the zero matrix); a non-finite system gives a non-finite d, which stops the pose (lm_iteration's guard).
+// The dependent chain is two adjugates, two 3-term products and two divisions deep, against the LDLT's six pivot steps.
 PCORE_GHD void lm_solve_schur(const double* sys, double lambda, double (&d)[6]) {
-    double A[6], C[6], B[3][3], r[6];
-PCORE_UNROLL
-    for (int i = 0; i < 3; i++) {
-PCORE_UNROLL
-        for (int j = i; j < 3; j++) {
-            A[s3(i, j)] = i == j ? sys[hdiag(i)] + lambda : sys[hidx(i, j)];
-            C[s3(i, j)] = i == j ? sys[hdiag(3 + i)] + lambda : sys[hidx(3 + i, 3 + j)];
-        }
-PCORE_UNROLL
-        for (int j = 0; j < 3; j++) B[i][j] = sys[hidx(i, 3 + j)];
-    }
-PCORE_UNROLL
-    for (int i = 0; i < 6; i++) r[i] = -sys[21 + i];
+    // upper triangles (00 01 02 11 12 22) of the rotation block A and the translation block C, + lambda on the diagonal
+    const double A[6] = {sys[0] + lambda, sys[1], sys[2], sys[6] + lambda, sys[7], sys[11] + lambda};
+    const double C[6] = {sys[15] + lambda, sys[16], sys[17], sys[18] + lambda, sys[19], sys[20] + lambda};
+    // B[i][j] = H[i][3 + j]
+    const double B00 = sys[3], B01 = sys[4], B02 = sys[5];
+    const double B10 = sys[8], B11 = sys[9], B12 = sys[10];
+    const double B20 = sys[12], B21 = sys[13], B22 = sys[14];
+    const double r0 = -sys[21], r1 = -sys[22], r2 = -sys[23], r3 = -sys[24], r4 = -sys[25], r5 = -sys[26];
     if (A[0] == 0.0 && A[3] == 0.0 && A[5] == 0.0 && C[0] == 0.0 && C[3] == 0.0 && C[5] == 0.0) {
 PCORE_UNROLL
         for (int i = 0; i < 6; i++) d[i] = 0.0;  // the zero system
@@ -692,48 +292,57 @@ PCORE_UNROLL
     }
     double aC[6], dC;
     adj_sym3(C, aC, dC);
-    double P[3][3];
-PCORE_UNROLL
-    for (int i = 0; i < 3; i++)
-PCORE_UNROLL
-        for (int j = 0; j < 3; j++)
-            P[i][j] = B[i][0] * aC[s3(0, j)] + B[i][1] * aC[s3(1, j)] + B[i][2] * aC[s3(2, j)];
-    double St[6], ut[3];
-PCORE_UNROLL
-    for (int i = 0; i < 3; i++) {
-PCORE_UNROLL
-        for (int j = i; j < 3; j++)
-            St[s3(i, j)] = dC * A[s3(i, j)] - (P[i][0] * B[j][0] + P[i][1] * B[j][1] + P[i][2] * B[j][2]);
-        ut[i] = dC * r[i] - (P[i][0] * r[3] + P[i][1] * r[4] + P[i][2] * r[5]);
-    }
+    // P = B adj(C) (adj(C) symmetric: column j = (aC[j0], aC[j1], aC[j2]))
+    const double P00 = dot3f(B00, B01, B02, aC[0], aC[1], aC[2]);
+    const double P01 = dot3f(B00, B01, B02, aC[1], aC[3], aC[4]);
+    const double P02 = dot3f(B00, B01, B02, aC[2], aC[4], aC[5]);
+    const double P10 = dot3f(B10, B11, B12, aC[0], aC[1], aC[2]);
+    const double P11 = dot3f(B10, B11, B12, aC[1], aC[3], aC[4]);
+    const double P12 = dot3f(B10, B11, B12, aC[2], aC[4], aC[5]);
+    const double P20 = dot3f(B20, B21, B22, aC[0], aC[1], aC[2]);
+    const double P21 = dot3f(B20, B21, B22, aC[1], aC[3], aC[4]);
+    const double P22 = dot3f(B20, B21, B22, aC[2], aC[4], aC[5]);
+    // S~ = dC A - P B^T (upper), u~ = dC r_rot - P r_trans
+    const double St[6] = {fma_d(dC, A[0], -dot3f(P00, P01, P02, B00, B01, B02)),
+                          fma_d(dC, A[1], -dot3f(P00, P01, P02, B10, B11, B12)),
+                          fma_d(dC, A[2], -dot3f(P00, P01, P02, B20, B21, B22)),
+                          fma_d(dC, A[3], -dot3f(P10, P11, P12, B10, B11, B12)),
+                          fma_d(dC, A[4], -dot3f(P10, P11, P12, B20, B21, B22)),
+                          fma_d(dC, A[5], -dot3f(P20, P21, P22, B20, B21, B22))};
+    const double u0 = fma_d(dC, r0, -dot3f(P00, P01, P02, r3, r4, r5));
+    const double u1 = fma_d(dC, r1, -dot3f(P10, P11, P12, r3, r4, r5));
+    const double u2 = fma_d(dC, r2, -dot3f(P20, P21, P22, r3, r4, r5));
     double aS[6], dS;
     adj_sym3(St, aS, dS);
-    double x1[3];
-PCORE_UNROLL
-    for (int i = 0; i < 3; i++) x1[i] = (aS[s3(i, 0)] * ut[0] + aS[s3(i, 1)] * ut[1] + aS[s3(i, 2)] * ut[2]) / dS;
-    double w[3];
-PCORE_UNROLL
-    for (int j = 0; j < 3; j++) w[j] = r[3 + j] - (B[0][j] * x1[0] + B[1][j] * x1[1] + B[2][j] * x1[2]);
-PCORE_UNROLL
-    for (int j = 0; j < 3; j++) {
-        d[j] = x1[j];
-        d[3 + j] = (aC[s3(j, 0)] * w[0] + aC[s3(j, 1)] * w[1] + aC[s3(j, 2)] * w[2]) / dC;
-    }
+    const double x0 = dot3f(aS[0], aS[1], aS[2], u0, u1, u2) / dS;
+    const double x1 = dot3f(aS[1], aS[3], aS[4], u0, u1, u2) / dS;
+    const double x2 = dot3f(aS[2], aS[4], aS[5], u0, u1, u2) / dS;
+    // w = r_trans - B^T x_rot
+    const double w0 = r3 - dot3f(B00, B10, B20, x0, x1, x2);
+    const double w1 = r4 - dot3f(B01, B11, B21, x0, x1, x2);
+    const double w2 = r5 - dot3f(B02, B12, B22, x0, x1, x2);
+    d[0] = x0;
+    d[1] = x1;
+    d[2] = x2;
+    d[3] = dot3f(aC[0], aC[1], aC[2], w0, w1, w2) / dC;
+    d[4] = dot3f(aC[1], aC[3], aC[4], w0, w1, w2) / dC;
+    d[5] = dot3f(aC[2], aC[4], aC[5], w0, w1, w2) / dC;
 }
 
-// se3_exp (fast_gicp so3.hpp): so3_exp quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
+// se3_exp (fast_gicp so3.hpp): so3_exp's quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
 // cos(theta/2)), Eigen's Quaternion::toRotationMatrix, translation V rho with
-// V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10)
-// WAVE: as lm_solve's (the sin / cos and quotients lane-parallel when every lane holds the same step)
+// V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10),
+// formed without V as rho + c1 (omega x rho) + c2 (omega x (omega x rho)) (Omega v = omega x v); products and sums
+// fused (fma_d / dot3f).  WAVE: every lane holds the same step, so the four sin / cos and the three quotients run
+// lane-parallel (lane_div).
 template <bool WAVE = (PCORE_LANE_PAR != 0)>
 PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]) {
     const double w0 = a[0], w1 = a[1], w2 = a[2];
-    const double theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
-    const double theta = __builtin_sqrt(theta_sq);  // so3_exp's and se3_exp's sqrt(omega . omega)
+    const double theta_sq = dot3f(w0, w1, w2, w0, w1, w2);
+    const double theta = __builtin_sqrt(theta_sq);
     double quo[3] = {0.0, 0.0, 0.0}, cos_h = 0.0;
 #if PCORE_LANE_PAR
     if constexpr (WAVE) {
-        // the four sin / cos on lanes 0..3 and the three quotients on lanes 0..2, one sequence each (same values)
         const int l = lane_index();
         const double half_theta = 0.5 * theta;
         const double tv = dmath::sincos_d(l < 2 ? half_theta : theta, (l & 1) != 0);
@@ -748,8 +357,8 @@ PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]
     double imag, real;
     if (theta_sq < 1e-10) {
         const double theta_quad = theta_sq * theta_sq;
-        imag = 0.5 - 1.0 / 48.0 * theta_sq + 1.0 / 3840.0 * theta_quad;
-        real = 1.0 - 1.0 / 8.0 * theta_sq + 1.0 / 384.0 * theta_quad;
+        imag = fma_d(1.0 / 3840.0, theta_quad, fma_d(-1.0 / 48.0, theta_sq, 0.5));
+        real = fma_d(1.0 / 384.0, theta_quad, fma_d(-1.0 / 8.0, theta_sq, 1.0));
     } else if (WAVE && PCORE_LANE_PAR) {
         imag = quo[0];
         real = cos_h;
@@ -760,31 +369,20 @@ PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]
     }
     const double qw = real, qx = imag * w0, qy = imag * w1, qz = imag * w2;
     const double tx = 2.0 * qx, ty = 2.0 * qy, tz = 2.0 * qz;
-    const double twx = tx * qw, twy = ty * qw, twz = tz * qw;
-    const double txx = tx * qx, txy = ty * qx, txz = tz * qx;
-    const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
-    Rd[0][0] = 1.0 - (tyy + tzz);
-    Rd[0][1] = txy - twz;
-    Rd[0][2] = txz + twy;
-    Rd[1][0] = txy + twz;
-    Rd[1][1] = 1.0 - (txx + tzz);
-    Rd[1][2] = tyz - twx;
-    Rd[2][0] = txz - twy;
-    Rd[2][1] = tyz + twx;
-    Rd[2][2] = 1.0 - (txx + tyy);
-    double V[3][3];
+    Rd[0][0] = 1.0 - fma_d(ty, qy, tz * qz);
+    Rd[0][1] = fma_d(ty, qx, -(tz * qw));
+    Rd[0][2] = fma_d(tz, qx, ty * qw);
+    Rd[1][0] = fma_d(ty, qx, tz * qw);
+    Rd[1][1] = 1.0 - fma_d(tx, qx, tz * qz);
+    Rd[1][2] = fma_d(tz, qy, -(tx * qw));
+    Rd[2][0] = fma_d(tz, qx, -(ty * qw));
+    Rd[2][1] = fma_d(tz, qy, tx * qw);
+    Rd[2][2] = 1.0 - fma_d(tx, qx, ty * qy);
+    const double r0 = a[3], r1 = a[4], r2 = a[5];
     if (theta < 1e-10) {
 PCORE_UNROLL
-        for (int r = 0; r < 3; r++)
-PCORE_UNROLL
-            for (int c = 0; c < 3; c++) V[r][c] = Rd[r][c];
+        for (int r = 0; r < 3; r++) td[r] = dot3f(Rd[r][0], Rd[r][1], Rd[r][2], r0, r1, r2);
     } else {
-        const double O[3][3] = {{0.0, -w2, w1}, {w2, 0.0, -w0}, {-w1, w0, 0.0}};
-        double O2[3][3];
-PCORE_UNROLL
-        for (int r = 0; r < 3; r++)
-PCORE_UNROLL
-            for (int c = 0; c < 3; c++) O2[r][c] = O[r][0] * O[0][c] + O[r][1] * O[1][c] + O[r][2] * O[2][c];
         double c1, c2;
         if (WAVE && PCORE_LANE_PAR) {
             c1 = quo[1];
@@ -794,23 +392,22 @@ PCORE_UNROLL
             c1 = (1.0 - dmath::cos_d(theta)) / th2;
             c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
         }
-PCORE_UNROLL
-        for (int r = 0; r < 3; r++)
-PCORE_UNROLL
-            for (int c = 0; c < 3; c++) V[r][c] = ((r == c ? 1.0 : 0.0) + c1 * O[r][c]) + c2 * O2[r][c];
+        const double a0 = fma_d(w1, r2, -(w2 * r1)), a1 = fma_d(w2, r0, -(w0 * r2)), a2 = fma_d(w0, r1, -(w1 * r0));
+        const double b0 = fma_d(w1, a2, -(w2 * a1)), b1 = fma_d(w2, a0, -(w0 * a2)), b2 = fma_d(w0, a1, -(w1 * a0));
+        td[0] = fma_d(c2, b0, fma_d(c1, a0, r0));
+        td[1] = fma_d(c2, b1, fma_d(c1, a1, r1));
+        td[2] = fma_d(c2, b2, fma_d(c1, a2, r2));
     }
-PCORE_UNROLL
-    for (int r = 0; r < 3; r++) td[r] = V[r][0] * a[3] + V[r][1] * a[4] + V[r][2] * a[5];
 }
 
-// x_i = delta * x (Isometry3d product): R_i = R_d R, t_i = R_d t + t_d
+// x_i = delta * x (Isometry3d product): R_i = R_d R, t_i = R_d t + t_d, fused
 PCORE_GHD void compose(const double (&Rd)[3][3], const double (&td)[3], const double (&R)[3][3], const double (&t)[3],
                        double (&Ro)[3][3], double (&to)[3]) {
 PCORE_UNROLL
     for (int r = 0; r < 3; r++) {
 PCORE_UNROLL
-        for (int c = 0; c < 3; c++) Ro[r][c] = Rd[r][0] * R[0][c] + Rd[r][1] * R[1][c] + Rd[r][2] * R[2][c];
-        to[r] = Rd[r][0] * t[0] + Rd[r][1] * t[1] + Rd[r][2] * t[2] + td[r];
+        for (int c = 0; c < 3; c++) Ro[r][c] = dot3f(Rd[r][0], Rd[r][1], Rd[r][2], R[0][c], R[1][c], R[2][c]);
+        to[r] = fma_d(Rd[r][0], t[0], fma_d(Rd[r][1], t[1], fma_d(Rd[r][2], t[2], td[r])));
     }
 }
 

@@ -83,20 +83,40 @@ def test_se3_exp_matches_matrix_exponential(scale):
 
 
 def test_lm_solve_matches_dense_solve():
-    """Eigen's LDLT with diagonal pivoting of H + lambda I, solve(-b): the dense solution to 1e-10; a diagonal
-    ordered so that every column pivots; a zero system gives a zero step (Eigen's pseudo-inverse of D)."""
+    """The damped solve (pcore_gicp_math.h lm_solve_schur: 3x3 block elimination of the translation block with
+    adjugates) against numpy's dense solve of H + lambda I, -b: random SPD systems with column scales over four
+    decades, half of them with the largest diagonal last; the error is bounded by cond(H + lambda I) times a few ulps.
+    A zero system gives a zero step (as Eigen's LDLT of the zero matrix does)."""
     rng = np.random.default_rng(5)
     for trial in range(200):
         A = rng.normal(size=(6, 6)) * rng.uniform(0.01, 100, 6)
         H = A @ A.T
         if trial % 2:
-            H = H[::-1, ::-1].copy()  # largest diagonal last: pivoting reorders every column
+            H = H[::-1, ::-1].copy()
         b = rng.normal(size=6)
         lam = [0.0, 1e-9, 1e-3][trial % 3] * np.abs(np.diag(H)).max()
         d = oracle.gicp_lm_solve(H, b, lam)
         ref = np.linalg.solve(H + lam * np.eye(6), -b)
-        assert np.abs(d - ref).max() <= 1e-10 * np.abs(ref).max() * np.linalg.cond(H + lam * np.eye(6)) ** 0.5 + 1e-300
+        cond = np.linalg.cond(H + lam * np.eye(6))
+        assert np.abs(d - ref).max() <= 1e-14 * cond * np.abs(ref).max(), (trial, cond)
     assert np.all(oracle.gicp_lm_solve(np.zeros((6, 6)), np.ones(6), 0.0) == 0.0)
+
+
+def test_lm_solve_on_gicp_systems_matches_dense_solve(c3_pairs):
+    """On the normal equations GICP actually forms (C3 candidates at the identity, at a perturbed pose and at the
+    converged one, damped by the first iteration's lambda; condition numbers up to ~2e5): the block solve within
+    1e-15 cond(H + lambda I) relative of numpy's (measured: <= 1e-16 cond)."""
+    rng = np.random.default_rng(9)
+    for src, scov, tgt, tcov in c3_pairs:
+        T_conv, _ = oracle.gicp(src, scov, tgt, tcov)
+        pert = gref.se3_exp(np.concatenate([rng.normal(size=3) * 0.05, rng.normal(size=3) * 0.01]))
+        for T in (np.eye(4), pert, T_conv):
+            _, H, b, _ = oracle.gicp_linearize(src, scov, tgt, tcov, T)
+            lam = 1e-9 * np.abs(np.diag(H)).max()
+            d = oracle.gicp_lm_solve(H, b, lam)
+            ref = np.linalg.solve(H + lam * np.eye(6), -b)
+            cond = np.linalg.cond(H + lam * np.eye(6))
+            assert np.abs(d - ref).max() <= 1e-15 * cond * np.abs(ref).max()
 
 
 def _rel(a, b):
@@ -317,14 +337,20 @@ def lm_solve_cases():
     return cases
 
 
-def test_lm_solve_pivot_order_first_equals_eigen_swaps():
-    """The kernels' LDLT (pivot sequence found first as a selection on |diag|, then the permuted matrix factored
-    without swaps) is bit-identical to the restatement of Eigen's in-place LDLT with its row / column swaps, on random
-    SPD and indefinite systems, tied and zero diagonals, a zero system, huge / tiny scales and non-finite entries."""
-    cases = lm_solve_cases()
-    for sysv, lam in cases:
-        a = oracle.gicp_lm_solve_sys(sysv, lam)
-        b = oracle.gicp_lm_solve_sys(sysv, lam, swaps=True)
-        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)) or (np.isnan(a) == np.isnan(b)).all() and \
-            np.array_equal(np.where(np.isnan(a), 0, a).view(np.uint64), np.where(np.isnan(b), 0, b).view(np.uint64)), \
-            (sysv, lam, a, b)
+def test_lm_solve_degenerate_systems():
+    """The block solve's edge cases over the systems the GPU test also runs (tests/test_gpu_gicp_solve.py): the zero
+    system gives d = 0 with or without damping; a non-finite entry gives a non-finite step (lm_iteration's guard then
+    stops the pose); a finite SPD system a finite step."""
+    for sysv, lam in lm_solve_cases():
+        d = oracle.gicp_lm_solve_sys(sysv, lam)
+        H = np.zeros((6, 6))
+        H[np.triu_indices(6)] = sysv[:21]
+        if not np.isfinite(sysv).all():
+            assert not np.isfinite(d).all()
+        elif not np.any(np.diag(H) + lam):
+            assert np.all(d == 0.0)
+        else:
+            Hs = H + np.triu(H, 1).T + lam * np.eye(6)
+            if np.all(np.linalg.eigvalsh(Hs) > 1e-12 * np.abs(Hs).max()) and np.linalg.cond(Hs) < 1e10:
+                ref = np.linalg.solve(Hs, -sysv[21:27])
+                assert np.abs(d - ref).max() <= 1e-14 * np.linalg.cond(Hs) * np.abs(ref).max() + 1e-300

@@ -1,6 +1,7 @@
-"""The GICP kernels' damped LM solve on the GPU (gicpm::lm_solve_rows: row i of the permuted system on lane i, through
-pcore_debug_lm_solve) against the oracle's restatement (pcore_gicp_math.h lm_solve, itself held bit for bit to Eigen's
-in-place pivoted LDLT by tests/test_gicp_spec.py), on the same 4,000+ random, tied, zero and non-finite systems."""
+"""The GICP kernels' damped LM solve on the GPU (gicpm::lm_solve_schur, uniform on the wave, through
+pcore_debug_lm_solve) against the oracle's host build of the same function (held to numpy's dense solve by
+tests/test_gicp_spec.py), bit for bit on the same 4,000+ random SPD and indefinite, tied, zero and non-finite systems:
+the fused products (fma) and IEEE divisions round identically on both sides."""
 import numpy as np
 import pytest
 

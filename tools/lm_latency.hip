@@ -1,8 +1,10 @@
 // lm_latency.hip -- measurement tool (not product code): shader clocks of the uniform pieces of one GICP LM step on
 // gfx950, one wave per call chain, at 1 wave per CU (no contention) and at 3 waves per SIMD (gicp_kernel's occupancy).
-// Pieces: gicpm::lm_solve_rows (pivoted LDLT, row per lane), gicpm::lm_solve_schur (the block / adjugate solve),
-// gicpm::se3_exp + compose, and one IEEE f64 division chain for calibration.  Every call's inputs come from LDS
-// (as the 28 reduced sums do in gicp_kernel) and its result feeds the next call's damping, so calls do not overlap.
+// Pieces: gicpm::lm_solve_schur (the block / adjugate solve), gicpm::se3_exp + compose, and a chain of six dependent
+// IEEE f64 divisions.  Every call's inputs come from LDS (as the 28 reduced sums do in gicp_kernel) and its result
+// feeds the next call's damping, so calls do not overlap.  Round 5, the same box (profiles/r05c/lm_latency.txt), clocks
+// per call at 1 / 12 waves per CU: the row-per-lane pivoted LDLT it replaced 4270 / 6141, lm_solve_schur 1198 / 1853;
+// se3_exp + compose 1358 / 2071 unfused, 1305 / 1954 fused; six divisions 461 / 656.
 //   hipcc --offload-arch=gfx950 -O2 -std=c++17 -ffp-contract=off -o tools/bin/lm_latency tools/lm_latency.hip
 #include <hip/hip_runtime.h>
 
@@ -54,11 +56,9 @@ __global__ void __launch_bounds__(64) lm_bench(const double* systems, int nsys, 
         const double l0 = s[0] + lambda;
         TD(t0, l0);
         double d[6];
-        if constexpr (V == 0) {
-            gicpm::lm_solve_rows(s, lambda, d);
-        } else if constexpr (V == 1) {
+        if constexpr (V == 1) {
             gicpm::lm_solve_schur(s, lambda, d);
-        } else if constexpr (V == 2) {
+        } else if constexpr (V == 4) {
             double a6[6];
             for (int i = 0; i < 6; i++) a6[i] = s[21 + i] * 1e-3 + lambda;
             double Rd[3][3], td[3], R[3][3], tt[3], Ro[3][3], to[3];
@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(64) lm_bench(const double* systems, int nsys, 
             for (int i = 0; i < 3; i++) d[i] = Ro[i][i];
             for (int i = 0; i < 3; i++) d[3 + i] = to[i];
         } else {
-            double x = l0;
+            double x = s[1] + l0;  // an LDS read after the first mark: the chain cannot start before it
             for (int i = 0; i < 6; i++) {
                 x = 1.0 / x + 0.5;
                 d[i] = x;
@@ -133,8 +133,7 @@ int main() {
     CHECK(hipMalloc(&d_clk, sizeof(unsigned long long) * cus * 12));
     CHECK(hipMemcpy(d_sys, sys.data(), sizeof(double) * sys.size(), hipMemcpyHostToDevice));
     if (run<3>("6 dependent f64 divisions", d_sys, nsys, d_out, d_clk, cus)) return 1;
-    if (run<0>("lm_solve_rows (LDLT)", d_sys, nsys, d_out, d_clk, cus)) return 1;
     if (run<1>("lm_solve_schur", d_sys, nsys, d_out, d_clk, cus)) return 1;
-    if (run<2>("se3_exp + compose", d_sys, nsys, d_out, d_clk, cus)) return 1;
+    if (run<4>("se3_exp + compose", d_sys, nsys, d_out, d_clk, cus)) return 1;
     return 0;
 }
