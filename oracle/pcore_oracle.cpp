@@ -649,7 +649,7 @@ int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double&
         gm::lm_solve_schur(sys, lambda, d);
         if (!gm::all_finite6(d)) return gm::kLmFailed;
         double Rd[3][3], td[3];
-        gm::se3_exp(d, Rd, td);
+        gm::se3_exp(d, Rd, td, gm::kSe3Coef);
         OXform xi;
         gm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
         std::fill(part.begin(), part.end(), 0.0);
@@ -879,7 +879,7 @@ void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, con
 void orc_gicp_se3_exp(const double* a6, double* out_T) {
     const double a[6] = {a6[0], a6[1], a6[2], a6[3], a6[4], a6[5]};
     double Rd[3][3], td[3];
-    pcore::gicpm::se3_exp(a, Rd, td);
+    pcore::gicpm::se3_exp(a, Rd, td, pcore::gicpm::kSe3Coef);
     for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) out_T[4 * r + c] = Rd[r][c];
         out_T[4 * r + 3] = td[r];

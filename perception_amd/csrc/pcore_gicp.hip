@@ -650,11 +650,17 @@ __device__ __forceinline__ void xform_identity(Xform& x) {
     }
 }
 
-// The first round of source points' inputs to the trials' errors, kept in the wave's LDS (SoA, conflict-free):
-// M as three double2 per lane, the source point and the correspondence's target (w = 1 when the point has one).
-// Later rounds go through the per-pose scratch slots in HBM / L2.  ~4.6 KB per wave.
+// The first kLdsRounds rounds of source points' inputs to the trials' errors, kept in the wave's LDS (SoA,
+// conflict-free): M as three double2 per point, the source point and the correspondence's target (w = 1 when the
+// point has one).  Later rounds go through the per-pose scratch slots in HBM / L2.  5 KB per round and wave: two
+// rounds cover C3's clouds (111 source points on average), so their trials read no HBM scratch; 10.4 KB per wave at
+// 12 waves per CU is 125 KB of the CU's 160 KB.
+#ifndef PCORE_GICP_LDS_ROUNDS
+#define PCORE_GICP_LDS_ROUNDS 2
+#endif
+constexpr int kLdsPts = 64 * PCORE_GICP_LDS_ROUNDS;
 struct Round0 {
-    double2 (*m)[64];
+    double2 (*m)[kLdsPts];
     float4* s;
     float4* t;
 };
@@ -692,7 +698,7 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
     }
     GPROF_TD(t_s1, j);
     GPROF_ADD(0, t_s0, t_s1);
-    const bool first = i < 64;
+    const bool first = i < kLdsPts;  // a point of the rounds kept in LDS
     if (first && !(act && j >= 0)) r0.t[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (act && j >= 0) {
         const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
@@ -722,6 +728,11 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
     GPROF_ADD(1, t_s1, t_s2);
 }
 
+// se3_exp's series coefficients as the kernels read them: an LDS copy through an address-space-3 volatile pointer, so
+// every use is a ds_read at the use (a generic volatile pointer made them flat loads and spilled 75 more VGPRs; the
+// literal constants were hoisted into 64 VGPRs for the whole kernel)
+typedef __attribute__((address_space(3))) const volatile double lds_cvd;
+
 // One Levenberg-Marquardt iteration of one wave (LsqRegistration::step_lm) on the reduced system `sys` (28 sums in
 // LDS: upper H, b, the error y0 at x): up to kLmMaxTrials solves of (H + lambda I) d = -b, each scored by the error
 // at delta * x with the iteration's correspondences and M (point i on lane i % 64, summed by the shuffle-down tree).
@@ -729,7 +740,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
 template <typename CorrPtr>
 __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double& lambda, const float4* src,
                                             CorrPtr corr, const double* mah, const float4* tgt, int ns, int lane,
-                                            const Round0& r0, double rot_eps, double trans_eps GPROF_PARAM) {
+                                            const Round0& r0, const lds_cvd* se3c, double rot_eps,
+                                            double trans_eps GPROF_PARAM) {
     const double y0 = uniform_d(sys[gicpm::kErr]);
     if (lambda < 0.0) lambda = uniform_d(gicpm::lm_init_lambda(sys));
     double nu = 2.0;
@@ -743,7 +755,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
         GPROF_ADD(4, p0, p1);
         if (!gicpm::all_finite6(d)) return gicpm::kLmFailed;  // guard: a non-finite system
         double Rd[3][3], td[3];
-        gicpm::se3_exp(d, Rd, td);
+        gicpm::se3_exp(d, Rd, td, se3c);
         Xform xi;
         gicpm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
 #pragma unroll
@@ -766,16 +778,20 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
             return gicpm::mahal_err(M6, e);
         };
         double ea = 0.0;
-        // round 0 from the wave's LDS copy (written by the linearisation), the later rounds from the scratch slots
-        {
-            const float4 t0 = r0.t[lane];
+        // the first rounds from the wave's LDS copy (written by the linearisation; a round past ns is not read), the
+        // later rounds from the scratch slots
+#pragma unroll
+        for (int i0 = 0; i0 < kLdsPts; i0 += 64) {
+            if (i0 > 0 && i0 >= ns) break;
+            const int i = i0 + lane;
+            const float4 t0 = r0.t[i];
             if (t0.w != 0.0f) {
-                const double2 a = r0.m[0][lane], b = r0.m[1][lane], c = r0.m[2][lane];
+                const double2 a = r0.m[0][i], b = r0.m[1][i], c = r0.m[2][i];
                 const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-                ea += err_of(r0.s[lane], t0, M6);
+                ea += err_of(r0.s[i], t0, M6);
             }
         }
-        for (int i0 = 64; i0 < ns; i0 += 64) {
+        for (int i0 = kLdsPts; i0 < ns; i0 += 64) {
             const int i = i0 + lane;
             const int j = i < ns ? corr[i] : -1;
             if (j >= 0) {
@@ -880,11 +896,13 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
 gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ double sRed[gicpm::kTerms];
-    __shared__ double2 sM0[3][64];
-    __shared__ float4 sS0[64], sT0[64];
+    __shared__ double2 sM0[3][kLdsPts];
+    __shared__ float4 sS0[kLdsPts], sT0[kLdsPts];
     __shared__ int sPose;
+    __shared__ double sSe3[4 * gicpm::kSe3Terms];  // se3_exp's series coefficients, read at their use
     const int lane = threadIdx.x;
     const Round0 r0{sM0, sS0, sT0};
+    if (lane < 4 * gicpm::kSe3Terms) sSe3[lane] = gicpm::kSe3Coef[lane];
     GPROF_DECL;
     for (;;) {
         wave_lds_sync();  // the previous pose's reads of sPose are done
@@ -955,8 +973,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 GPROF_T(t_b);
                 const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
-                const int st = lm_iteration(sys, x, lambda, P.src, cset, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
-                                            g.trans_eps GPROF_ARG);
+                const int st = lm_iteration(sys, x, lambda, P.src, cset, P.mah, P.tgt, P.ns, lane, r0, (const lds_cvd*)sSe3,
+                                            g.rot_eps, g.trans_eps GPROF_ARG);
                 GPROF_TD(t_d, st);
                 GPROF_ADD(2, t_b, t_c);
                 GPROF_ADD(3, t_c, t_d);
@@ -979,12 +997,14 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
     constexpr int NT = 64 * WPP;
     extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
     __shared__ double sRed[gicpm::kTerms];
-    __shared__ double2 sM0[3][64];
-    __shared__ float4 sS0[64], sT0[64];
+    __shared__ double2 sM0[3][kLdsPts];
+    __shared__ float4 sS0[kLdsPts], sT0[kLdsPts];
     __shared__ double sX[12];
     __shared__ int sPose, sFlag;
+    __shared__ double sSe3[4 * gicpm::kSe3Terms];
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const Round0 r0{sM0, sS0, sT0};  // wave 0's
+    if (tid < 4 * gicpm::kSe3Terms) sSe3[tid] = gicpm::kSe3Coef[tid];
     GPROF_DECL;  // wave 0's phases: [0] the searches of all waves (to the barrier), [1] contributions, [2] tree, [3] LM
     for (;;) {
         __syncthreads();
@@ -1039,8 +1059,8 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 GPROF_TD(t_w2, acc[0]);
                 const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_w3, sys[0]);
-                const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, g.rot_eps,
-                                            g.trans_eps GPROF_ARG);
+                const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, (const lds_cvd*)sSe3,
+                                            g.rot_eps, g.trans_eps GPROF_ARG);
                 GPROF_TD(t_w4, st);
                 GPROF_ADD(2, t_w2, t_w3);  // [1]: linearize_round's own marks
                 GPROF_ADD(3, t_w3, t_w4);

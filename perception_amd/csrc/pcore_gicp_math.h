@@ -329,43 +329,78 @@ PCORE_UNROLL
     d[5] = dot3f(aC[2], aC[4], aC[5], w0, w1, w2) / dC;
 }
 
-// se3_exp (fast_gicp so3.hpp): so3_exp's quaternion (Taylor below theta^2 = 1e-10, else sin(theta/2)/theta and
-// cos(theta/2)), Eigen's Quaternion::toRotationMatrix, translation V rho with
-// V = I + (1 - cos theta)/theta^2 Omega + (theta - sin theta)/theta^3 Omega^2 (V = the rotation below theta = 1e-10),
-// formed without V as rho + c1 (omega x rho) + c2 (omega x (omega x rho)) (Omega v = omega x v); products and sums
-// fused (fma_d / dot3f).  WAVE: every lane holds the same step, so the four sin / cos and the three quotients run
-// lane-parallel (lane_div).
-template <bool WAVE = (PCORE_LANE_PAR != 0)>
-PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]) {
+// se3_exp's four functions of theta as even power series in u = theta^2 (Horner, fused), used below theta^2 = 1/4:
+//   imag = sin(theta / 2) / theta = sum (-1)^k u^k / (2^(2k+1) (2k+1)!)     real = cos(theta / 2) = sum (-1)^k u^k / (2^(2k) (2k)!)
+//   c1 = (1 - cos theta) / theta^2 = sum (-1)^k u^k / (2k+2)!               c2 = (theta - sin theta) / theta^3 = sum (-1)^k u^k / (2k+3)!
+// Eight terms: below u = 1/4 the first omitted one is < 1e-17 of the sum.  The coefficients are the doubles nearest
+// the exact rationals.  (so3_exp's own Taylor branch below theta^2 = 1e-10 is the first two terms of imag / real.)
+constexpr int kSe3Terms = 8;
+constexpr double kSe3SeriesMax = 0.25;
+// imag, real, c1, c2: kSe3Terms coefficients each, lowest power first
+constexpr double kSe3Coef[4 * kSe3Terms] = {
+    0.5, -0.020833333333333332, 0.00026041666666666666, -1.5500992063492063e-06, 5.382288910934745e-09,
+    -1.2232474797578965e-11, 1.9603324996120133e-14, -2.333729166204778e-17,
+    1.0, -0.125, 0.0026041666666666665, -2.170138888888889e-05, 9.68812003968254e-08, -2.691144455467372e-10,
+    5.096864498991235e-13, -7.001187498614334e-16,
+    0.5, -0.041666666666666664, 0.001388888888888889, -2.48015873015873e-05, 2.755731922398589e-07,
+    -2.08767569878681e-09, 1.1470745597729725e-11, -4.779477332387385e-14,
+    0.16666666666666666, -0.008333333333333333, 0.0001984126984126984, -2.7557319223985893e-06,
+    2.505210838544172e-08, -1.6059043836821613e-10, 7.647163731819816e-13, -2.8114572543455206e-15};
+// Horner in u of the coefficients c[0 .. kSe3Terms).  The kernels pass a volatile LDS copy of kSe3Coef (read at the
+// use: as 32 literal doubles the constants were hoisted out of the iteration loop into 64 VGPRs for the whole kernel);
+// the host passes kSe3Coef.
+template <typename P>
+PCORE_GHD double se3_series(P c, double u) {
+    double p = c[kSe3Terms - 1];
+PCORE_UNROLL
+    for (int k = kSe3Terms - 2; k >= 0; k--) p = fma_d(p, u, c[k]);
+    return p;
+}
+
+// se3_exp (fast_gicp so3.hpp): so3_exp's quaternion (imag = sin(theta/2)/theta, real = cos(theta/2)), Eigen's
+// Quaternion::toRotationMatrix, translation V rho with V = I + c1 Omega + c2 Omega^2, c1 = (1 - cos theta)/theta^2,
+// c2 = (theta - sin theta)/theta^3 (V = the rotation below theta = 1e-10, as published: here theta^2 < 1e-20), formed
+// without V as rho + c1 (omega x rho) + c2 (omega x (omega x rho)) (Omega v = omega x v); products and sums fused
+// (fma_d / dot3f).  Below theta^2 = 1/4 -- nearly every LM step -- imag, real, c1 and c2 are the power series above:
+// no square root, no sin / cos, no division, and no cancellation in 1 - cos theta or theta - sin theta (the published
+// quotients lose ~eps / theta^2 of relative accuracy there).  Larger steps take the published quotients; WAVE: every
+// lane holds the same step, so their four sin / cos and three divisions run lane-parallel (lane_div).
+template <bool WAVE = (PCORE_LANE_PAR != 0), typename P = const double*>
+PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3], P coef) {
     const double w0 = a[0], w1 = a[1], w2 = a[2];
     const double theta_sq = dot3f(w0, w1, w2, w0, w1, w2);
-    const double theta = __builtin_sqrt(theta_sq);
-    double quo[3] = {0.0, 0.0, 0.0}, cos_h = 0.0;
-#if PCORE_LANE_PAR
-    if constexpr (WAVE) {
-        const int l = lane_index();
-        const double half_theta = 0.5 * theta;
-        const double tv = dmath::sincos_d(l < 2 ? half_theta : theta, (l & 1) != 0);
-        const double sin_h = read_lane_d<0>(tv);
-        cos_h = read_lane_d<1>(tv);
-        const double sin_t = read_lane_d<2>(tv), cos_t = read_lane_d<3>(tv);
-        const double th2 = theta * theta;
-        const double num[3] = {sin_h, 1.0 - cos_t, theta - sin_t}, den[3] = {theta, th2, th2 * theta};
-        lane_div<3>(num, den, quo);
-    }
-#endif
-    double imag, real;
-    if (theta_sq < 1e-10) {
-        const double theta_quad = theta_sq * theta_sq;
-        imag = fma_d(1.0 / 3840.0, theta_quad, fma_d(-1.0 / 48.0, theta_sq, 0.5));
-        real = fma_d(1.0 / 384.0, theta_quad, fma_d(-1.0 / 8.0, theta_sq, 1.0));
-    } else if (WAVE && PCORE_LANE_PAR) {
-        imag = quo[0];
-        real = cos_h;
+    double imag, real, c1, c2;
+    if (theta_sq < kSe3SeriesMax) {
+        imag = se3_series(coef, theta_sq);
+        real = se3_series(coef + kSe3Terms, theta_sq);
+        c1 = se3_series(coef + 2 * kSe3Terms, theta_sq);
+        c2 = se3_series(coef + 3 * kSe3Terms, theta_sq);
     } else {
+        const double theta = __builtin_sqrt(theta_sq);
         const double half_theta = 0.5 * theta;
-        imag = dmath::sin_d(half_theta) / theta;
-        real = dmath::cos_d(half_theta);
+        const double th2 = theta * theta;
+#if PCORE_LANE_PAR
+        if constexpr (WAVE) {
+            // the four sin / cos on lanes 0..3 and the three quotients on lanes 0..2, one sequence each (same values)
+            const int l = lane_index();
+            const double tv = dmath::sincos_d(l < 2 ? half_theta : theta, (l & 1) != 0);
+            const double sin_h = read_lane_d<0>(tv), cos_h = read_lane_d<1>(tv);
+            const double sin_t = read_lane_d<2>(tv), cos_t = read_lane_d<3>(tv);
+            const double num[3] = {sin_h, 1.0 - cos_t, theta - sin_t}, den[3] = {theta, th2, th2 * theta};
+            double quo[3];
+            lane_div<3>(num, den, quo);
+            imag = quo[0];
+            real = cos_h;
+            c1 = quo[1];
+            c2 = quo[2];
+        } else
+#endif
+        {
+            imag = dmath::sin_d(half_theta) / theta;
+            real = dmath::cos_d(half_theta);
+            c1 = (1.0 - dmath::cos_d(theta)) / th2;
+            c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
+        }
     }
     const double qw = real, qx = imag * w0, qy = imag * w1, qz = imag * w2;
     const double tx = 2.0 * qx, ty = 2.0 * qy, tz = 2.0 * qz;
@@ -379,19 +414,10 @@ PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]
     Rd[2][1] = fma_d(tz, qy, tx * qw);
     Rd[2][2] = 1.0 - fma_d(tx, qx, ty * qy);
     const double r0 = a[3], r1 = a[4], r2 = a[5];
-    if (theta < 1e-10) {
+    if (theta_sq < 1e-20) {
 PCORE_UNROLL
         for (int r = 0; r < 3; r++) td[r] = dot3f(Rd[r][0], Rd[r][1], Rd[r][2], r0, r1, r2);
     } else {
-        double c1, c2;
-        if (WAVE && PCORE_LANE_PAR) {
-            c1 = quo[1];
-            c2 = quo[2];
-        } else {
-            const double th2 = theta * theta;
-            c1 = (1.0 - dmath::cos_d(theta)) / th2;
-            c2 = (theta - dmath::sin_d(theta)) / (th2 * theta);
-        }
         const double a0 = fma_d(w1, r2, -(w2 * r1)), a1 = fma_d(w2, r0, -(w0 * r2)), a2 = fma_d(w0, r1, -(w1 * r0));
         const double b0 = fma_d(w1, a2, -(w2 * a1)), b1 = fma_d(w2, a0, -(w0 * a2)), b2 = fma_d(w0, a1, -(w1 * a0));
         td[0] = fma_d(c2, b0, fma_d(c1, a0, r0));

@@ -354,3 +354,17 @@ def test_lm_solve_degenerate_systems():
             if np.all(np.linalg.eigvalsh(Hs) > 1e-12 * np.abs(Hs).max()) and np.linalg.cond(Hs) < 1e10:
                 ref = np.linalg.solve(Hs, -sysv[21:27])
                 assert np.abs(d - ref).max() <= 1e-14 * np.linalg.cond(Hs) * np.abs(ref).max() + 1e-300
+
+
+def test_se3_exp_series_and_quotients_meet_at_the_switch():
+    """se3_exp switches from the power series of imag / real / c1 / c2 (theta^2 < 1/4) to the published quotients of
+    sin / cos: on both sides of the switch the result is within a few ulps of scipy's expm of the twist, and small steps
+    (theta ~ 1e-3, where the published (theta - sin theta) / theta^3 loses ~1e-10 relative to cancellation) match expm
+    to 1e-15."""
+    rng = np.random.default_rng(17)
+    for theta in (0.5 * (1 - 1e-12), 0.5, 0.5 * (1 + 1e-12), 1e-3, 3e-5):
+        for _ in range(10):
+            w = rng.normal(size=3)
+            w = w / np.linalg.norm(w) * theta
+            d = np.concatenate([w, rng.normal(size=3) * 0.05])
+            assert np.abs(oracle.gicp_se3_exp(d) - gref.se3_exp(d)).max() < 3e-16 * 8
