@@ -467,6 +467,12 @@ typedef __attribute__((address_space(4))) const f4v cf4v;
 #ifndef PCORE_SCAN_UNROLL
 #define PCORE_SCAN_UNROLL 4  // quad pairs per loop trip (C3: 2 -> 4: 20.60 -> 20.45 ms per step; 1: 21.25)
 #endif
+#ifndef PCORE_GICP_PAIR_SCAN
+#define PCORE_GICP_PAIR_SCAN 1  // 0: scan a round pair's queries one after the other (A/B)
+#endif
+#ifndef PCORE_SCAN2_UNROLL
+#define PCORE_SCAN2_UNROLL 2  // scan_quads2: quad pairs per loop trip
+#endif
 
 __device__ __forceinline__ void scan_quads(const float* seg_quads, int nt, float qx, float qy, float qz, float& best,
                                            int& j) {
@@ -516,6 +522,69 @@ __device__ __forceinline__ void scan_quads(const float* seg_quads, int nt, float
         // pick slot 3, padding in a segment's last quad) inside the segment
         j = min(4 * oA + k, nt - 1);
     }
+}
+
+// scan_quads for two queries per lane (the pose's source points i and i + 64): every scalar load of a quad feeds both,
+// so a pair of rounds reads the segment's key quads once.  Each query keeps its own two chains (alternate quads) and
+// its own winner recovery, so (best, j) of each is scan_quads' bit for bit.
+__device__ __forceinline__ void scan_quads2(const float* seg_quads, int nt, float ax, float ay, float az, float bx,
+                                            float by, float bz, int& ja, int& jb) {
+    const int nq = (nt + 3) >> 2;
+    const cf4v* hq = (const cf4v*)seg_quads;
+    const f4v org = hq[0];
+    ax = ax - org.x; ay = ay - org.y; az = az - org.z;
+    bx = bx - org.x; by = by - org.y; bz = bz - org.z;
+    const bool fa = __builtin_isfinite(ax) && __builtin_isfinite(ay) && __builtin_isfinite(az);
+    const bool fb = __builtin_isfinite(bx) && __builtin_isfinite(by) && __builtin_isfinite(bz);
+    const cf4v* tq = hq + 4;
+    const f2v ax2 = {ax, ax}, ay2 = {ay, ay}, az2 = {az, az};
+    const f2v bx2 = {bx, bx}, by2 = {by, by}, bz2 = {bz, bz};
+    float aA = INFINITY, aB = INFINITY, bA = INFINITY, bB = INFINITY;
+    int oaA = -1, oaB = -1, obA = -1, obB = -1;
+    auto qmin2 = [&](const cf4v* q, float& ma, float& mb) {
+        const f4v X = q[0], Y = q[1], Z = q[2], T = q[3];
+        const f2v ka = __builtin_elementwise_fma(X.xy, ax2, __builtin_elementwise_fma(Y.xy, ay2,
+                                                  __builtin_elementwise_fma(Z.xy, az2, T.xy)));
+        const f2v kb = __builtin_elementwise_fma(X.zw, ax2, __builtin_elementwise_fma(Y.zw, ay2,
+                                                  __builtin_elementwise_fma(Z.zw, az2, T.zw)));
+        ma = fminf(fminf(fminf(ka.x, ka.y), kb.x), kb.y);
+        const f2v la = __builtin_elementwise_fma(X.xy, bx2, __builtin_elementwise_fma(Y.xy, by2,
+                                                  __builtin_elementwise_fma(Z.xy, bz2, T.xy)));
+        const f2v lb = __builtin_elementwise_fma(X.zw, bx2, __builtin_elementwise_fma(Y.zw, by2,
+                                                  __builtin_elementwise_fma(Z.zw, bz2, T.zw)));
+        mb = fminf(fminf(fminf(la.x, la.y), lb.x), lb.y);
+    };
+    int o = 0;
+    const cf4v* q = tq;
+#pragma unroll PCORE_SCAN2_UNROLL
+    for (; o + 2 <= nq; o += 2, q += 8) {
+        float ma, mb;
+        qmin2(q, ma, mb);
+        if (ma < aA) { aA = ma; oaA = o; }
+        if (mb < bA) { bA = mb; obA = o; }
+        qmin2(q + 4, ma, mb);
+        if (ma < aB) { aB = ma; oaB = o + 1; }
+        if (mb < bB) { bB = mb; obB = o + 1; }
+    }
+    if (o < nq) {
+        float ma, mb;
+        qmin2(q, ma, mb);
+        if (ma < aA) { aA = ma; oaA = o; }
+        if (mb < bA) { bA = mb; obA = o; }
+    }
+    if (aB < aA || (aB == aA && oaB >= 0 && oaB < oaA)) { aA = aB; oaA = oaB; }
+    if (bB < bA || (bB == bA && obB >= 0 && obB < obA)) { bA = bB; obA = obB; }
+    auto element = [&](int oq, float m, float qx, float qy, float qz) {
+        const float* Q = seg_quads + 16 + 16 * oq;
+        const float4 X = *reinterpret_cast<const float4*>(Q), Y = *reinterpret_cast<const float4*>(Q + 4);
+        const float4 Z = *reinterpret_cast<const float4*>(Q + 8), T = *reinterpret_cast<const float4*>(Q + 12);
+        const int k = gicpm::nn_key(X.x, Y.x, Z.x, T.x, qx, qy, qz) == m ? 0
+                    : gicpm::nn_key(X.y, Y.y, Z.y, T.y, qx, qy, qz) == m ? 1
+                    : gicpm::nn_key(X.z, Y.z, Z.z, T.z, qx, qy, qz) == m ? 2 : 3;
+        return min(4 * oq + k, nt - 1);
+    };
+    ja = fa && aA < INFINITY ? element(oaA, aA, ax, ay, az) : -1;
+    jb = fb && bA < INFINITY ? element(obA, bA, bx, by, bz) : -1;
 }
 
 __device__ __forceinline__ void load_cov(const double* cov, int i, double (&c)[6]) {
@@ -967,9 +1036,51 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 double acc[gicpm::kTerms];
 #pragma unroll
                 for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-                for (int i0 = 0; i0 < P.ns; i0 += 64)
-                    linearize_round<true>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
-                                          P.tquads, P.nt, -1, cset, P.mah, r0, acc, !reuse GPROF_ARG);
+                // rounds in pairs: both rounds' correspondences first (one pass over the key quads serves both:
+                // scan_quads2), then their contributions in point order -- the sums are those of round-by-round
+                // linearisation, bit for bit
+                for (int i0 = 0; i0 < P.ns; i0 += 128) {
+                    const int ia = i0 + lane, ib = ia + 64;
+                    const bool two = i0 + 64 < P.ns;  // uniform
+                    GPROF_T(t_s0);
+                    int ja = -1, jb = -1;
+                    if (reuse) {
+                        if (ia < P.ns) ja = cset[ia];
+                        if (two && ib < P.ns) jb = cset[ib];
+                    } else {
+                        const float4 sa = ia < P.ns ? P.src[ia] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        const float4 sb = two && ib < P.ns ? P.src[ib] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        float qa[3], qb[3];
+                        gicpm::query_f(Rf, tf, sa.x, sa.y, sa.z, qa);
+                        gicpm::query_f(Rf, tf, sb.x, sb.y, sb.z, qb);
+                        if (P.use_grid) {
+                            float best;
+                            if (ia < P.ns) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qa[0], qa[1], qa[2], best, ja);
+                            if (two && ib < P.ns)
+                                grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qb[0], qb[1], qb[2], best, jb);
+                        } else if (two && PCORE_GICP_PAIR_SCAN) {
+                            scan_quads2(P.tquads, P.nt, qa[0], qa[1], qa[2], qb[0], qb[1], qb[2], ja, jb);
+                        } else if (two) {  // A/B: the pair's queries scanned one after the other
+                            float best = INFINITY;
+                            scan_quads(P.tquads, P.nt, qa[0], qa[1], qa[2], best, ja);
+                            best = INFINITY;
+                            scan_quads(P.tquads, P.nt, qb[0], qb[1], qb[2], best, jb);
+                        } else {
+                            float best = INFINITY;
+                            scan_quads(P.tquads, P.nt, qa[0], qa[1], qa[2], best, ja);
+                        }
+                        if (ia < P.ns) cset[ia] = ja;
+                        if (two && ib < P.ns) cset[ib] = jb;
+                    }
+                    GPROF_TD(t_s1, ja + jb);
+                    GPROF_ADD(0, t_s0, t_s1);
+                    linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, ia, P.use_grid, G, g,
+                                           P.tquads, P.nt, ia < P.ns ? ja : -1, nullptr, P.mah, r0, acc, false GPROF_ARG);
+                    if (two)
+                        linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, ib, P.use_grid, G, g,
+                                               P.tquads, P.nt, ib < P.ns ? jb : -1, nullptr, P.mah, r0, acc,
+                                               false GPROF_ARG);
+                }
                 GPROF_T(t_b);
                 const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
