@@ -617,9 +617,8 @@ void gicp_linearize_spec(const OXform& x, const float* src_xyz, const double* sr
         const int j = gicp_nn(qf, tgt_xyz, nt, keys, org);
         corr[i] = j;
         if (j < 0) continue;
-        const double s0 = (double)s[0], s1 = (double)s[1], s2 = (double)s[2];
         double q[3];
-        for (int r = 0; r < 3; r++) q[r] = x.R[r][0] * s0 + x.R[r][1] * s1 + x.R[r][2] * s2 + x.t[r];
+        pcore::gicpm::transform_point(x.R, x.t, (double)s[0], (double)s[1], (double)s[2], q);
         double cs[6], ct[6], M6[6], acc[NT];
         for (int e = 0; e < 6; e++) { cs[e] = src_cov[(size_t)6 * i + e]; ct[e] = tgt_cov[(size_t)6 * j + e]; }
         const double tj[3] = {(double)tgt_xyz[3 * (size_t)j + 0], (double)tgt_xyz[3 * (size_t)j + 1],
@@ -656,16 +655,14 @@ int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double&
         for (int i = 0; i < ns; i++) {
             const int j = corr[i];
             if (j < 0) continue;
-            const double s0 = (double)src_xyz[3 * (size_t)i], s1 = (double)src_xyz[3 * (size_t)i + 1],
-                         s2 = (double)src_xyz[3 * (size_t)i + 2];
+            double q[3];
+            gm::transform_point(xi.R, xi.t, (double)src_xyz[3 * (size_t)i], (double)src_xyz[3 * (size_t)i + 1],
+                                (double)src_xyz[3 * (size_t)i + 2], q);
             double e[3];
-            for (int r = 0; r < 3; r++) {
-                const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
-                e[r] = (double)tgt_xyz[3 * (size_t)j + r] - q;
-            }
+            for (int r = 0; r < 3; r++) e[r] = (double)tgt_xyz[3 * (size_t)j + r] - q[r];
             double M6[6];
             for (int k = 0; k < 6; k++) M6[k] = mah[(size_t)6 * i + k];
-            part[i % 64] += gm::mahal_err(M6, e);
+            part[i % 64] = gm::mahal_err_add(M6, e, part[i % 64]);
         }
         const double yi = lane_tree(part.data(), 1, 0);
         const double rho = gm::lm_rho(sys, lambda, d, y0, yi);

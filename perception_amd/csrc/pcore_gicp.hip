@@ -770,10 +770,8 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
     const bool first = i < kLdsPts;  // a point of the rounds kept in LDS
     if (first && !(act && j >= 0)) r0.t[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (act && j >= 0) {
-        const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
         double q[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++) q[r] = x.R[r][0] * s0 + x.R[r][1] * s1 + x.R[r][2] * s2 + x.t[r];
+        gicpm::transform_point(x.R, x.t, (double)sp.x, (double)sp.y, (double)sp.z, q);
         double cs[6], ct[6], M6[6];
         load_cov(scov, i, cs);
         load_cov(tcov, j, ct);
@@ -836,15 +834,11 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
         GPROF_TD(p2, xi.t[2]);
         GPROF_ADD(5, p1, p2);
         // the error at x_i (FastGICP::compute_error: this iteration's correspondences and Mahalanobis matrices)
-        auto err_of = [&](const float4& sp, const float4& tj, const double (&M6)[6]) {
-            const double s0 = (double)sp.x, s1 = (double)sp.y, s2 = (double)sp.z;
-            double e[3];
-#pragma unroll
-            for (int r = 0; r < 3; r++) {
-                const double q = xi.R[r][0] * s0 + xi.R[r][1] * s1 + xi.R[r][2] * s2 + xi.t[r];
-                e[r] = (double)(r == 0 ? tj.x : r == 1 ? tj.y : tj.z) - q;
-            }
-            return gicpm::mahal_err(M6, e);
+        auto err_add = [&](const float4& sp, const float4& tj, const double (&M6)[6], double y) {
+            double q[3];
+            gicpm::transform_point(xi.R, xi.t, (double)sp.x, (double)sp.y, (double)sp.z, q);
+            const double e[3] = {(double)tj.x - q[0], (double)tj.y - q[1], (double)tj.z - q[2]};
+            return gicpm::mahal_err_add(M6, e, y);
         };
         double ea = 0.0;
         // the first rounds from the wave's LDS copy (written by the linearisation; a round past ns is not read), the
@@ -857,7 +851,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
             if (t0.w != 0.0f) {
                 const double2 a = r0.m[0][i], b = r0.m[1][i], c = r0.m[2][i];
                 const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-                ea += err_of(r0.s[i], t0, M6);
+                ea = err_add(r0.s[i], t0, M6, ea);
             }
         }
         for (int i0 = kLdsPts; i0 < ns; i0 += 64) {
@@ -867,7 +861,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
                 const double2* m2 = reinterpret_cast<const double2*>(mah + (size_t)6 * i);
                 const double2 a = m2[0], b = m2[1], c = m2[2];
                 const double M6[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-                ea += err_of(src[i], tgt[j], M6);
+                ea = err_add(src[i], tgt[j], M6, ea);
             }
         }
         const double yi = uniform_d(wave_sum_lane0(ea));  // lane 0: the tree's sum

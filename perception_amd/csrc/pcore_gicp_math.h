@@ -88,22 +88,34 @@ PCORE_UNROLL
     for (int r = 0; r < 3; r++) qf[r] = Rf[r][0] * sx + Rf[r][1] * sy + Rf[r][2] * sz + tf[r];
 }
 
-// J^T v (the 6-vector above)
-PCORE_GHD void jt_mul(const double (&q)[3], const double (&v)[3], double (&o)[6]) {
-    o[0] = q[2] * v[1] - q[1] * v[2];
-    o[1] = q[0] * v[2] - q[2] * v[0];
-    o[2] = q[1] * v[0] - q[0] * v[1];
-    o[3] = -v[0];
-    o[4] = -v[1];
-    o[5] = -v[2];
-}
-
 // Terms of the normal equations a point adds: acc[0..20] upper(J^T M J) row-major, acc[21..26] J^T M e,
 // acc[27] e^T M e (the error y of step_lm).
 constexpr int kTerms = 28;
 constexpr int kErr = 27;
 // index of H[a][a] in the upper triangle
 PCORE_GHD constexpr int hdiag(int a) { return a * 6 - (a * (a - 1)) / 2; }
+
+// Fused products (spec round 5): fma is correctly rounded on the GPU (v_fma_f64) and on the host (glibc fma), so the
+// kernels and the oracle evaluate every expression built from these bit for bit.  The linearisation, the trials'
+// errors, the damped solve, se3_exp and compose all use them: about 40 % fewer f64 instructions than separate
+// products and sums, which is what the GICP kernel's VALU time is made of (f64: 57 % of its VALU cycles in round 4).
+PCORE_GHD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
+// a0 b0 + a1 b1 + a2 b2 as fma(a0, b0, fma(a1, b1, a2 b2))
+PCORE_GHD double dot3f(double a0, double a1, double a2, double b0, double b1, double b2) {
+    return fma_d(a0, b0, fma_d(a1, b1, a2 * b2));
+}
+
+// Adjugate (upper: 00 01 02 11 12 22) and determinant of a symmetric 3x3 given by its upper triangle (same order)
+PCORE_GHD void adj_sym3(const double (&m)[6], double (&a)[6], double& det) {
+    a[0] = fma_d(m[3], m[5], -(m[4] * m[4]));
+    a[1] = fma_d(m[2], m[4], -(m[1] * m[5]));
+    a[2] = fma_d(m[1], m[4], -(m[2] * m[3]));
+    a[3] = fma_d(m[0], m[5], -(m[2] * m[2]));
+    a[4] = fma_d(m[1], m[2], -(m[0] * m[4]));
+    a[5] = fma_d(m[0], m[3], -(m[1] * m[1]));
+    det = dot3f(m[0], m[1], m[2], a[0], a[1], a[2]);
+}
+
 
 // Lane-parallel evaluation of a few uniform operations (device only).  The LM step is uniform work that every
 // lane of the wave repeats; where it holds several independent IEEE divisions (se3_exp's three quotients) or
@@ -145,92 +157,87 @@ PCORE_UNROLL
 #define PCORE_LANE_PAR 0
 #endif
 
-// e^T M e with M given by its upper triangle (xx, xy, xz, yy, yz, zz): Me row by row, then the dot product
-PCORE_GHD double mahal_err(const double (&M6)[6], const double (&e)[3]) {
-    const double me0 = M6[0] * e[0] + M6[1] * e[1] + M6[2] * e[2];
-    const double me1 = M6[1] * e[0] + M6[3] * e[1] + M6[4] * e[2];
-    const double me2 = M6[2] * e[0] + M6[4] * e[1] + M6[5] * e[2];
-    return e[0] * me0 + e[1] * me1 + e[2] * me2;
+// q = R s + t row by row, fused: the transformed source point of the linearisation and of the trials' errors
+PCORE_GHD void transform_point(const double (&R)[3][3], const double (&t)[3], double s0, double s1, double s2,
+                               double (&q)[3]) {
+PCORE_UNROLL
+    for (int r = 0; r < 3; r++) q[r] = fma_d(R[r][0], s0, fma_d(R[r][1], s1, fma_d(R[r][2], s2, t[r])));
 }
 
-// M = (C_t + R C_s R^T)^-1 of one point (xx, xy, xz, yy, yz, zz), contrib's first half
+// y + e^T M e with M given by its upper triangle (xx, xy, xz, yy, yz, zz): Me row by row (dot3f), then
+// fma(e0, Me0, fma(e1, Me1, fma(e2, Me2, y))).  The linearisation's error term (contrib) and the trials' errors use
+// this one expression, so a trial at the linearisation point reproduces its error bit for bit.
+PCORE_GHD double mahal_err_add(const double (&M6)[6], const double (&e)[3], double y) {
+    const double me0 = dot3f(M6[0], M6[1], M6[2], e[0], e[1], e[2]);
+    const double me1 = dot3f(M6[1], M6[3], M6[4], e[0], e[1], e[2]);
+    const double me2 = dot3f(M6[2], M6[4], M6[5], e[0], e[1], e[2]);
+    return fma_d(e[0], me0, fma_d(e[1], me1, fma_d(e[2], me2, y)));
+}
+
+// M = (C_t + R C_s R^T)^-1 of one point (xx, xy, xz, yy, yz, zz), contrib's first half: row r of R C_s, then row r
+// of A = C_t + (R C_s) R^T with C_t as the innermost addend (only one row of R C_s is live at a time); the adjugate
+// and determinant of the symmetric A (adj_sym3) and M = adj(A) * (1 / det)
 PCORE_GHD void mahal_matrix(const double (&R)[3][3], const double (&cs)[6], const double (&ct)[6], double (&M6)[6]) {
-    const double Cs[3][3] = {{cs[0], cs[1], cs[2]}, {cs[1], cs[3], cs[4]}, {cs[2], cs[4], cs[5]}};
-    const double Ct[3][3] = {{ct[0], ct[1], ct[2]}, {ct[1], ct[3], ct[4]}, {ct[2], ct[4], ct[5]}};
-    // A = C_t + R C_s R^T row by row (row r of R C_s, then A's row r): only one row of R C_s is live at a time
-    double A[3][3];
+    constexpr int S3[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+    double A[6];
 PCORE_UNROLL
     for (int r = 0; r < 3; r++) {
         double RC[3];
 PCORE_UNROLL
-        for (int c = 0; c < 3; c++) RC[c] = R[r][0] * Cs[0][c] + R[r][1] * Cs[1][c] + R[r][2] * Cs[2][c];
+        for (int c = 0; c < 3; c++) RC[c] = dot3f(R[r][0], R[r][1], R[r][2], cs[S3[0][c]], cs[S3[1][c]], cs[S3[2][c]]);
 PCORE_UNROLL
-        for (int c = r; c < 3; c++) A[r][c] = Ct[r][c] + (RC[0] * R[c][0] + RC[1] * R[c][1] + RC[2] * R[c][2]);
+        for (int c = r; c < 3; c++)
+            A[S3[r][c]] = fma_d(RC[0], R[c][0], fma_d(RC[1], R[c][1], fma_d(RC[2], R[c][2], ct[S3[r][c]])));
     }
-    A[1][0] = A[0][1];
-    A[2][0] = A[0][2];
-    A[2][1] = A[1][2];
-    // adjugate of the symmetric A (symmetric too) and the determinant
-    double m[3][3];
-    m[0][0] = A[1][1] * A[2][2] - A[1][2] * A[2][1];
-    m[0][1] = A[0][2] * A[2][1] - A[0][1] * A[2][2];
-    m[0][2] = A[0][1] * A[1][2] - A[0][2] * A[1][1];
-    m[1][1] = A[0][0] * A[2][2] - A[0][2] * A[2][0];
-    m[1][2] = A[0][2] * A[1][0] - A[0][0] * A[1][2];
-    m[2][2] = A[0][0] * A[1][1] - A[0][1] * A[1][0];
-    m[1][0] = m[0][1];
-    m[2][0] = m[0][2];
-    m[2][1] = m[1][2];
-    const double det = A[0][0] * m[0][0] + A[0][1] * m[1][0] + A[0][2] * m[2][0];
+    double adj[6], det;
+    adj_sym3(A, adj, det);
     const double inv = 1.0 / det;
-    double M[3][3];
 PCORE_UNROLL
-    for (int r = 0; r < 3; r++)
-PCORE_UNROLL
-        for (int c = 0; c < 3; c++) M[r][c] = m[r][c] * inv;
-    M6[0] = M[0][0]; M6[1] = M[0][1]; M6[2] = M[0][2];
-    M6[3] = M[1][1]; M6[4] = M[1][2]; M6[5] = M[2][2];
+    for (int k = 0; k < 6; k++) M6[k] = adj[k] * inv;
 }
 
 // One point's contribution for the transformed point q (double), its correspondence tj and both covariances
-// (xx, xy, xz, yy, yz, zz); M6 receives the point's Mahalanobis matrix (kept for the trials' errors).  M is
-// symmetric bit for bit (m[r][c] = m[c][r], both scaled by the same 1 / det), so its 3x3 form is rebuilt from M6.
+// (xx, xy, xz, yy, yz, zz); M6 receives the point's Mahalanobis matrix (kept for the trials' errors).
+// H[a][b] (a <= b) column by column: column b of M J as a 3-vector cb (b < 3: the skew part, one fma and one product
+// per entry; b >= 3: -M's column), then for every a <= b the J^T row a against cb fused into the sum:
+// acc = fma(q2, cb1, fma(-q1, cb2, acc)) for a = 0 (and the cyclic forms for a = 1, 2), acc - cb[a - 3] for a >= 3.
+// Each sum takes one term per point, so the column order of the updates changes no sum, and only one column is live
+// at a time.  b += J^T M e the same way, y by mahal_err_add.
 PCORE_GHD void contrib(const double (&R)[3][3], const double (&q)[3], const double (&cs)[6], const double (&tj)[3],
                        const double (&ct)[6], double (&acc)[kTerms], double (&M6)[6]) {
     mahal_matrix(R, cs, ct, M6);
     const double M[3][3] = {{M6[0], M6[1], M6[2]}, {M6[1], M6[3], M6[4]}, {M6[2], M6[4], M6[5]}};
     const double e[3] = {tj[0] - q[0], tj[1] - q[1], tj[2] - q[2]};
-    // H[a][b] (a <= b) column by column: column b of M J as a 3-vector (b < 3: the skew part; b >= 3: -M's column),
-    // then its J^T product for every a <= b into acc[hdiag(a) + b - a].  Each sum takes one term per point, so the
-    // column order of the updates changes no sum, and only one column is live at a time.
+    // J^T row a (a < 3) against v, fused into the sum s
+    auto jt_add = [&](int a, const double (&v)[3], double sum) {
+        return a == 0 ? fma_d(q[2], v[1], fma_d(-q[1], v[2], sum))
+             : a == 1 ? fma_d(q[0], v[2], fma_d(-q[2], v[0], sum))
+                      : fma_d(q[1], v[0], fma_d(-q[0], v[1], sum));
+    };
 PCORE_UNROLL
     for (int b = 0; b < 6; b++) {
         double cb[3];
 PCORE_UNROLL
         for (int r = 0; r < 3; r++) {
-            if (b == 0) cb[r] = M[r][1] * q[2] - M[r][2] * q[1];
-            else if (b == 1) cb[r] = M[r][2] * q[0] - M[r][0] * q[2];
-            else if (b == 2) cb[r] = M[r][0] * q[1] - M[r][1] * q[0];
+            if (b == 0) cb[r] = fma_d(M[r][1], q[2], -(M[r][2] * q[1]));
+            else if (b == 1) cb[r] = fma_d(M[r][2], q[0], -(M[r][0] * q[2]));
+            else if (b == 2) cb[r] = fma_d(M[r][0], q[1], -(M[r][1] * q[0]));
             else cb[r] = -M[r][b - 3];
         }
 PCORE_UNROLL
         for (int a = 0; a <= b; a++) {
-            double v;
-            if (a == 0) v = q[2] * cb[1] - q[1] * cb[2];
-            else if (a == 1) v = q[0] * cb[2] - q[2] * cb[0];
-            else if (a == 2) v = q[1] * cb[0] - q[0] * cb[1];
-            else v = -cb[a - 3];
-            acc[hdiag(a) + b - a] += v;
+            double& h = acc[hdiag(a) + b - a];
+            h = a < 3 ? jt_add(a, cb, h) : h - cb[a - 3];
         }
     }
     double Me[3];
 PCORE_UNROLL
-    for (int r = 0; r < 3; r++) Me[r] = M[r][0] * e[0] + M[r][1] * e[1] + M[r][2] * e[2];
-    double g[6];
-    jt_mul(q, Me, g);
+    for (int r = 0; r < 3; r++) Me[r] = dot3f(M[r][0], M[r][1], M[r][2], e[0], e[1], e[2]);
 PCORE_UNROLL
-    for (int a = 0; a < 6; a++) acc[21 + a] += g[a];
-    acc[kErr] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+    for (int a = 0; a < 3; a++) acc[21 + a] = jt_add(a, Me, acc[21 + a]);
+PCORE_UNROLL
+    for (int a = 3; a < 6; a++) acc[21 + a] = acc[21 + a] - Me[a - 3];
+    acc[kErr] = mahal_err_add(M6, e, acc[kErr]);
 }
 
 // ---- the step (uniform per pose) ----------------------------------------------------------------------------
@@ -247,25 +254,6 @@ PCORE_UNROLL
         m = v > m ? v : m;
     }
     return kLmInitFactor * m;
-}
-
-// fused products of the solve: fma is correctly rounded on the GPU (v_fma_f64) and on the host (glibc fma), so the
-// kernels and the oracle evaluate these expressions bit for bit
-PCORE_GHD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
-// a0 b0 + a1 b1 + a2 b2 as fma(a0, b0, fma(a1, b1, a2 b2))
-PCORE_GHD double dot3f(double a0, double a1, double a2, double b0, double b1, double b2) {
-    return fma_d(a0, b0, fma_d(a1, b1, a2 * b2));
-}
-
-// Adjugate (upper: 00 01 02 11 12 22) and determinant of a symmetric 3x3 given by its upper triangle (same order)
-PCORE_GHD void adj_sym3(const double (&m)[6], double (&a)[6], double& det) {
-    a[0] = fma_d(m[3], m[5], -(m[4] * m[4]));
-    a[1] = fma_d(m[2], m[4], -(m[1] * m[5]));
-    a[2] = fma_d(m[1], m[4], -(m[2] * m[3]));
-    a[3] = fma_d(m[0], m[5], -(m[2] * m[2]));
-    a[4] = fma_d(m[1], m[2], -(m[0] * m[4]));
-    a[5] = fma_d(m[0], m[3], -(m[1] * m[1]));
-    det = dot3f(m[0], m[1], m[2], a[0], a[1], a[2]);
 }
 
 // d = (H + lambda I)^-1 (-b) by the 3x3 block elimination of the translation block: with
