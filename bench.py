@@ -387,7 +387,7 @@ def main():
         "definition": "per timed step, host perf_counter: wait = works[b].wait() for the lane's previous exchange "
                       "(gloo: host-blocking; RCCL: a stream dependency), launch_call = fill + evaluate call + "
                       "event records, exchange_issue = the async all_reduce call; launch_span = HIP events around "
-                      "the fill + stage-COST launch on the lane's stream",
+                      "the stage-COST launch on the lane's stream",
     }
 
     best_cost, best_idx = decode_keys(keys)

@@ -171,3 +171,34 @@ extern "C" int stream_bank_sim(const float* tri_xyz, int T, int num_streams, int
     out[0] = extra; out[1] = reads; out[2] = steps;
     return 0;
 }
+
+// The builder's steps for one mesh: out_orig[64 * step + slot] = the original triangle index of the slot, or -1 for
+// padding (at most max_steps steps); returns the number of steps (tools/step_skip_estimate.py).
+extern "C" int stream_steps(const float* tri_xyz, int T, int num_streams, int vring, int ref_passes, int chunks,
+                            int32_t* out_orig, int max_steps) {
+    struct K { uint32_t x, y, z; bool operator==(const K& o) const { return x == o.x && y == o.y && z == o.z; } };
+    struct H { size_t operator()(const K& k) const { return (size_t)k.x * 73856093u ^ (size_t)k.y * 19349663u ^ (size_t)k.z * 83492791u; } };
+    std::unordered_map<K, int, H> idx;
+    std::vector<int> tv(3 * (size_t)T);
+    std::vector<float> vxyz;
+    for (int t = 0; t < T; t++)
+        for (int k = 0; k < 3; k++) {
+            const float* p = tri_xyz + 9 * (size_t)t + 3 * k;
+            K key;
+            std::memcpy(&key.x, p, 4); std::memcpy(&key.y, p + 1, 4); std::memcpy(&key.z, p + 2, 4);
+            auto it = idx.find(key);
+            int id;
+            if (it == idx.end()) { id = (int)vxyz.size() / 3; idx.emplace(key, id); vxyz.insert(vxyz.end(), p, p + 3); }
+            else id = it->second;
+            tv[3 * (size_t)t + k] = id;
+        }
+    pcore::streams::Built b;
+    pcore::streams::build_model(tv, vxyz, 0, num_streams, vring, ref_passes, b, chunks);
+    const int steps = (int)b.steps;
+    for (int s = 0; s < steps && s < max_steps; s++)
+        for (int l = 0; l < 64; l++) {
+            const uint32_t w = b.stris[(size_t)64 * s + l];
+            out_orig[(size_t)64 * s + l] = (w >> 31) ? -1 : (int32_t)b.sorig[(size_t)64 * s + l];
+        }
+    return steps;
+}
