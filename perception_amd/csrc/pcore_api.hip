@@ -93,8 +93,9 @@ struct pcore_ctx {
     DevBuf<int32_t> colour_id;    // N x nsamp scratch of the fused kernel's colour id pass
     DevBuf<int32_t> fb_ctr;       // FusedArgs::fb_ctr
     DevBuf<int32_t> win_hist;     // FusedArgs::win_hist
+    DevBuf<int32_t> fb_ctr_cap;   // the same for captured launches: counted into, never published or read
+    DevBuf<int32_t> win_hist_cap;
     int32_t* fb_host = nullptr;   // mapped host memory (FusedArgs::fb_host), host view
-    bool fb_dirty = false;        // a captured launch ran: clear the feedback counters before the next eager one
     int32_t* fb_dev = nullptr;    // the same, device view
     int32_t fb_seq = 0;           // sequence number of the last fused launch
     int32_t tile_key_seq = 0;     // first sequence number launched with the current tile configuration
@@ -684,17 +685,20 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hip
         if ((e = hipMemset(c->fb_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
         if ((e = hipMemset(c->win_hist.p, 0, 2 * (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
     }
-    // a captured launch keeps one parity and never publishes: its replays leave counts behind, cleared (on the
-    // stream) before the next eager launch
+    // A captured launch counts into buffers of its own that nothing publishes or reads: its replays can
+    // never add to the parity histograms the eager launches publish.  A stream whose capture state cannot be queried
+    // (hipStreamIsCapturing fails, e.g. on the legacy stream while another stream captures in global mode) is treated
+    // as capturing: no window probe, no feedback.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if ((e = hipStreamIsCapturing(s, &cap)) != hipSuccess) return e;
-    const bool capturing = cap != hipStreamCaptureStatusNone;
-    if (!capturing && c->fb_dirty) {
-        if ((e = hipMemsetAsync(c->fb_ctr.p, 0, 2 * sizeof(int32_t), s)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(c->win_hist.p, 0, 2 * (kTileTiers + 1) * sizeof(int32_t), s)) != hipSuccess) return e;
-        c->fb_dirty = false;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        cap = hipStreamCaptureStatusActive;
     }
-    if (capturing) c->fb_dirty = true;
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    if (capturing && !c->fb_ctr_cap.p) {
+        if ((e = dev_reserve(c->fb_ctr_cap, 2)) != hipSuccess) return e;
+        if ((e = dev_reserve(c->win_hist_cap, 2 * (kTileTiers + 1))) != hipSuccess) return e;
+    }
     int edge[kTileTiers];
     for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, c->dinfo);
     const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);
@@ -733,8 +737,8 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hip
         a.tcap = std::min(std::max(atoi(env), 1), nsamp);
     for (int t = 0; t < kTileTiers; t++) a.hist_edge[t] = c->tile_edge[t] = edge[t];
     c->tile_tcap = a.tcap;
-    a.fb_ctr = c->fb_ctr.p;
-    a.win_hist = c->win_hist.p;
+    a.fb_ctr = capturing ? c->fb_ctr_cap.p : c->fb_ctr.p;
+    a.win_hist = capturing ? c->win_hist_cap.p : c->win_hist.p;
     a.fb_host = capturing ? nullptr : c->fb_dev;
     a.fb_seq = ++c->fb_seq;
     a.fb_par = a.fb_seq & 1;
@@ -1145,10 +1149,10 @@ int pcore_debug_lm_solve(const double* d_sys, const double* d_lambda, double* d_
 
 int pcore_debug_covariances(const float* d_xyzw, const int32_t* d_seg_off, const int32_t* d_seg_cnt, int32_t num_segs,
                             int32_t k, double* d_out_cov6, pcore_stream stream) {
-    if (num_segs < 0 || k <= 0 || (num_segs > 0 && (!d_xyzw || !d_seg_off || !d_seg_cnt || !d_out_cov6)))
+    if (num_segs < 0 || k <= 0 || k > 16 || (num_segs > 0 && (!d_xyzw || !d_seg_off || !d_seg_cnt || !d_out_cov6)))
         return PCORE_E_INVALID_ARG;
     return launch_covariances(reinterpret_cast<const float4*>(d_xyzw), d_seg_off, d_seg_cnt, 0, num_segs, k, d_out_cov6,
-                              (hipStream_t)stream, INT_MAX) == hipSuccess ? PCORE_OK : PCORE_E_INVALID_ARG;
+                              (hipStream_t)stream, INT_MAX) == hipSuccess ? PCORE_OK : PCORE_E_HIP;
 }
 
 int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,

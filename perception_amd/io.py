@@ -227,6 +227,25 @@ _POSES_STAT: "OrderedDict[str, tuple]" = OrderedDict()  # abspath -> (stat signa
 _SETTLED_NS = 2_000_000_000
 
 
+def _fs_now_ns(directory: str):
+    """The current time on the clock of the file system holding `directory`: the ctime of a temporary file created
+    there (None when none can be created, e.g. a read-only data set)."""
+    import tempfile
+
+    try:
+        fd, tmp = tempfile.mkstemp(prefix=".pcore_clock_", dir=directory)
+    except OSError:
+        return None
+    try:
+        return os.fstat(fd).st_ctime_ns
+    finally:
+        os.close(fd)
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+
+
 def _stat_signature(st: os.stat_result) -> tuple:
     return st.st_dev, st.st_ino, st.st_size, st.st_mtime_ns, st.st_ctime_ns
 
@@ -239,8 +258,10 @@ def read_poses_txt_cached(path: str, use_cache: bool = True) -> np.ndarray:
 
     A file whose status change time was already 2 s old when it was read is not read again while its (device,
     inode, size, mtime, ctime) stay the same: any write after that read sets ctime to the current time, which no
-    utime call can set back, so an unchanged signature means unchanged bytes.  A file changed within the last 2 s
-    (the kernel's timestamp clock is coarse) is read and hashed every time.  Least-recently-used eviction past 64
+    utime call can set back, so an unchanged signature means unchanged bytes.  "Now" is the file system's own clock
+    (the ctime of a temporary file created beside it), not this host's, so a server clock that lags (NFS) cannot make a
+    fresh file look settled; where no temporary file can be created the file is never taken as settled.
+    A file changed within the last 2 s (the kernel's timestamp clock is coarse) is read and hashed every time.  Least-recently-used eviction past 64
     files.  use_cache=False (or PCORE_POSES_CACHE=0) parses every time.  Returns a read-only array."""
     if not use_cache or os.environ.get("PCORE_POSES_CACHE", "1") == "0":
         return read_poses_txt(path)
@@ -258,7 +279,8 @@ def read_poses_txt_cached(path: str, use_cache: bool = True) -> np.ndarray:
         sig_read = _stat_signature(os.fstat(f.fileno()))
     key = (apath, _content_digest(data))
     _POSES_STAT.pop(apath, None)
-    if sig_open == sig_read and time.time_ns() - sig_read[4] > _SETTLED_NS:
+    fs_now = _fs_now_ns(os.path.dirname(apath)) if sig_open == sig_read else None
+    if fs_now is not None and fs_now - sig_read[4] > _SETTLED_NS:
         _POSES_STAT[apath] = (sig_read, key[1])
         while len(_POSES_STAT) > _POSES_CACHE_MAX:
             _POSES_STAT.popitem(last=False)

@@ -41,3 +41,12 @@ def test_create_without_gpu_fails_cleanly():
     h = ctypes.c_void_p()
     assert lib.pcore_create(0, ctypes.byref(h)) != 0
     assert lib.pcore_destroy(None) is None
+
+
+def test_debug_covariances_rejects_k_outside_1_16():
+    """pcore_debug_covariances validates 1 <= k <= 16 (pcore.h) before any launch."""
+    lib = _native.load()
+    lib.pcore_debug_covariances.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                                                    ctypes.c_void_p]
+    for k in (0, 17, -1):
+        assert lib.pcore_debug_covariances(None, None, None, 0, k, None, None) == _native.PCORE_E_INVALID_ARG

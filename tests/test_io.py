@@ -164,8 +164,8 @@ def test_read_poses_txt_cached_settled_file_skips_the_read(tmp_path, monkeypatch
     rows = np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]])
     pio.write_poses_txt(p, rows)
     st = os.stat(p)
-    real_ns = time.time_ns
-    monkeypatch.setattr(pio.time, "time_ns", lambda: real_ns() + 10 * pio._SETTLED_NS)  # pretend the file is old
+    real_fs_now = pio._fs_now_ns
+    monkeypatch.setattr(pio, "_fs_now_ns", lambda d: real_fs_now(d) + 10 * pio._SETTLED_NS)  # pretend the file is old
     a = pio.read_poses_txt_cached(p)
     digests = []
     monkeypatch.setattr(pio, "_content_digest", lambda d: digests.append(1) or b"x" * 16)
@@ -177,3 +177,28 @@ def test_read_poses_txt_cached_settled_file_skips_the_read(tmp_path, monkeypatch
     monkeypatch.undo()
     b = pio.read_poses_txt_cached(p)
     assert b[0, 0] == 0.2 and a[0, 0] == 0.1
+
+
+def test_read_poses_txt_cached_settles_on_the_file_systems_clock(tmp_path, monkeypatch):
+    """"settled" is judged on the file system's clock (a temporary file's ctime beside the file), so a
+    local clock far ahead of the server's (NFS) does not make a fresh file look settled; a directory where no
+    temporary file can be created never settles (every read hashes)."""
+    from perception_amd import io as pio
+    import time
+    p = str(tmp_path / "poses.txt")
+    pio.write_poses_txt(p, np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]]))
+    real_ns = time.time_ns
+    monkeypatch.setattr(pio.time, "time_ns", lambda: real_ns() + 100 * pio._SETTLED_NS)  # local clock far ahead
+    a = pio.read_poses_txt_cached(p)
+    digests = []
+    real_digest = pio._content_digest
+    monkeypatch.setattr(pio, "_content_digest", lambda d: digests.append(1) or real_digest(d))
+    assert pio.read_poses_txt_cached(p) is a and digests  # fresh on the file system's clock: read and hashed again
+    fs_now = pio._fs_now_ns(str(tmp_path))
+    assert fs_now is not None and abs(fs_now - real_ns()) < 60 * 10**9
+    monkeypatch.setattr(pio, "_fs_now_ns", lambda d: None)  # no temporary file possible
+    digests.clear()
+    pio._POSES_STAT.clear()
+    pio.read_poses_txt_cached(p)
+    pio.read_poses_txt_cached(p)
+    assert len(digests) == 2
