@@ -682,6 +682,9 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hip
         if ((e = hipHostGetDevicePointer((void**)&c->fb_dev, c->fb_host, 0)) != hipSuccess) return e;
         if ((e = dev_reserve(c->fb_ctr, 2)) != hipSuccess) return e;
         if ((e = dev_reserve(c->win_hist, 2 * (kTileTiers + 1))) != hipSuccess) return e;
+        // captured launches' own counters, allocated here: no allocation may happen while a stream captures
+        if ((e = dev_reserve(c->fb_ctr_cap, 2)) != hipSuccess) return e;
+        if ((e = dev_reserve(c->win_hist_cap, 2 * (kTileTiers + 1))) != hipSuccess) return e;
         if ((e = hipMemset(c->fb_ctr.p, 0, 2 * sizeof(int32_t))) != hipSuccess) return e;
         if ((e = hipMemset(c->win_hist.p, 0, 2 * (kTileTiers + 1) * sizeof(int32_t))) != hipSuccess) return e;
     }
@@ -695,10 +698,6 @@ static hipError_t set_fused_tiles(pcore_ctx* c, int num_poses, FusedArgs& a, hip
         cap = hipStreamCaptureStatusActive;
     }
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    if (capturing && !c->fb_ctr_cap.p) {
-        if ((e = dev_reserve(c->fb_ctr_cap, 2)) != hipSuccess) return e;
-        if ((e = dev_reserve(c->win_hist_cap, 2 * (kTileTiers + 1))) != hipSuccess) return e;
-    }
     int edge[kTileTiers];
     for (int t = 0; t < kTileTiers; t++) edge[t] = fused_tier_samples(t, a.ws, a.hs, a.bitmap_words, colour, c->dinfo);
     const long long key = (((long long)a.ws * 4096 + a.hs) * 65536 + a.bitmap_words) * 2 + (colour ? 1 : 0);

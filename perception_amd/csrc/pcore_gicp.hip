@@ -34,6 +34,9 @@ namespace pcore {
 namespace {
 
 constexpr int kGThreads = 256;
+#ifndef PCORE_COV_SKIP
+#define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
+#endif
 constexpr int kMaxK = 16;
 // Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only):
 // [0] correspondence search, [1] contributions (+ M stores), [2] wave reduction, [3] LM iteration, which splits into [4] damped
@@ -259,7 +262,12 @@ __device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[K
 #pragma unroll
     for (int e = 0; e < 6; e++) c6[e] = c6[e] / kd;
     double r6[6];
+#if PCORE_COV_SKIP & 1  // ablation timing only (wrong results): no eigen-decomposition / PLANE regularisation
+#pragma unroll
+    for (int e = 0; e < 6; e++) r6[e] = c6[e];
+#else
     plane_regularize(c6, r6);
+#endif
 #pragma unroll
     for (int e = 0; e < 6; e++) out6[e] = r6[e];
 }
@@ -316,7 +324,13 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
             if (cnt < k) cnt++;
             nan_list = nan_list || d != d;
         };
+#if PCORE_COV_SKIP & 2  // ablation timing only (wrong results): the first k points instead of the k-NN search
+        for (int q = 0; q < KMAX; q++)
+            if (q < k && q < n) { nb[q] = q; cnt = q + 1; }
+        for (int j0 = n; j0 < n; j0 += kCovLanes) {
+#else
         for (int j0 = 0; j0 < n; j0 += kCovLanes) {
+#endif
             wave_lds_sync();  // the previous tile is read
             if (j0 + lane < n) tile[lane] = P[j0 + lane];
             wave_lds_sync();
@@ -977,8 +991,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
         const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
         if (pose >= num_poses) break;
         const GicpPose P = gicp_pose(g, pose);
-        LabelGrid G{};
-        if (P.use_grid) G = g.grids[P.seg];
+        const LabelGrid G{};  // linearize_round's grid argument, unused here: the searches below load the grid
         Xform x;
         xform_identity(x);
         double lambda = -1.0;
@@ -1047,11 +1060,12 @@ gicp_kernel(GicpArgs g, int num_poses) {
                         float qa[3], qb[3];
                         gicpm::query_f(Rf, tf, sa.x, sa.y, sa.z, qa);
                         gicpm::query_f(Rf, tf, sb.x, sb.y, sb.z, qb);
-                        if (P.use_grid) {
+                        if (P.use_grid) {  // segments above kGridNNMin (the grid is read here, not held per pose)
+                            const LabelGrid Gs = g.grids[P.seg];
                             float best;
-                            if (ia < P.ns) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qa[0], qa[1], qa[2], best, ja);
+                            if (ia < P.ns) grid_nn(Gs, g.cell_start, g.grid_pts, P.tgt, P.nt, qa[0], qa[1], qa[2], best, ja);
                             if (two && ib < P.ns)
-                                grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qb[0], qb[1], qb[2], best, jb);
+                                grid_nn(Gs, g.cell_start, g.grid_pts, P.tgt, P.nt, qb[0], qb[1], qb[2], best, jb);
                         } else if (two && PCORE_GICP_PAIR_SCAN) {
                             scan_quads2(P.tquads, P.nt, qa[0], qa[1], qa[2], qb[0], qb[1], qb[2], ja, jb);
                         } else if (two) {  // A/B: the pair's queries scanned one after the other
