@@ -2,7 +2,7 @@
 restatement (orc_covariances: fast_gicp's k-nearest-neighbour covariance with PLANE regularisation, DESIGN.md section
 5), on segments that exercise the k-NN list: random clouds, clouds on a lattice (many equal distances, so the
 placement of ties decides the neighbour lists), duplicated points, fewer points than k, a single point, and a NaN point
-among the first k candidates (the list that can no longer be sorted)."""
+among the first k candidates (the list that can no longer be sorted), a rendered-like plane patch and 256 / 257 points."""
 import numpy as np
 import pytest
 
@@ -25,6 +25,12 @@ def _segments():
     segs.append(np.concatenate([d, d[:20], d[5:9]]))  # duplicates
     segs.append(rng.normal(size=(7, 3)).astype(np.float32))  # n < k
     segs.append(rng.normal(size=(1, 3)).astype(np.float32))  # one point
+    # a rendered-like patch (a tilted plane sampled on a pixel grid, unprojected: near-equal distances), 256 / 257 points
+    u, v = np.meshgrid(np.arange(12) * 8.0, np.arange(10) * 8.0)
+    z = 0.8 + 0.0005 * u + 0.0002 * v
+    segs.append(np.stack([(u - 40) / 576.0 * z, (v - 30) / 576.0 * z, z], -1).reshape(-1, 3).astype(np.float32))
+    segs.append((rng.normal(size=(256, 3)) * 0.05).astype(np.float32))
+    segs.append((rng.normal(size=(257, 3)) * 0.05).astype(np.float32))
     nanseg = (rng.normal(size=(90, 3)) * 0.02).astype(np.float32)
     nanseg[3] = np.nan  # among the first k candidates of every point
     segs.append(nanseg)
