@@ -809,10 +809,16 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
     GPROF_ADD(1, t_s1, t_s2);
 }
 
-// se3_exp's series coefficients as the kernels read them: an LDS copy through an address-space-3 volatile pointer, so
-// every use is a ds_read at the use (a generic volatile pointer made them flat loads and spilled 75 more VGPRs; the
-// literal constants were hoisted into 64 VGPRs for the whole kernel)
-typedef __attribute__((address_space(3))) const volatile double lds_cvd;
+// se3_exp's series coefficients as the kernels read them: an LDS copy through an address-space-3 pointer offset by an
+// opaque zero produced inside the iteration loop, so the loads cannot be hoisted out of it (as literal constants they
+// were hoisted into 64 VGPRs for the whole kernel; a generic pointer made them flat loads) but can be issued together
+// ahead of the series (a volatile pointer serialised them: one LDS round trip per coefficient, 32 in a row)
+typedef __attribute__((address_space(3))) const double lds_cvd;
+__device__ __forceinline__ int opaque_zero() {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return z;
+}
 
 // One Levenberg-Marquardt iteration of one wave (LsqRegistration::step_lm) on the reduced system `sys` (28 sums in
 // LDS: upper H, b, the error y0 at x): up to kLmMaxTrials solves of (H + lambda I) d = -b, each scored by the error
@@ -836,7 +842,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
         GPROF_ADD(4, p0, p1);
         if (!gicpm::all_finite6(d)) return gicpm::kLmFailed;  // guard: a non-finite system
         double Rd[3][3], td[3];
-        gicpm::se3_exp(d, Rd, td, se3c);
+        gicpm::se3_exp(d, Rd, td, se3c + opaque_zero());
         Xform xi;
         gicpm::compose(Rd, td, x.R, x.t, xi.R, xi.t);
 #pragma unroll

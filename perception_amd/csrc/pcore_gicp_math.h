@@ -324,25 +324,29 @@ PCORE_UNROLL
 // the exact rationals.  (so3_exp's own Taylor branch below theta^2 = 1e-10 is the first two terms of imag / real.)
 constexpr int kSe3Terms = 8;
 constexpr double kSe3SeriesMax = 0.25;
-// imag, real, c1, c2: kSe3Terms coefficients each, lowest power first
+// The coefficients interleaved by power: kSe3Coef[4 k + f] is the coefficient of u^k of imag, real, c1, c2 (f = 0..3)
 constexpr double kSe3Coef[4 * kSe3Terms] = {
-    0.5, -0.020833333333333332, 0.00026041666666666666, -1.5500992063492063e-06, 5.382288910934745e-09,
-    -1.2232474797578965e-11, 1.9603324996120133e-14, -2.333729166204778e-17,
-    1.0, -0.125, 0.0026041666666666665, -2.170138888888889e-05, 9.68812003968254e-08, -2.691144455467372e-10,
-    5.096864498991235e-13, -7.001187498614334e-16,
-    0.5, -0.041666666666666664, 0.001388888888888889, -2.48015873015873e-05, 2.755731922398589e-07,
-    -2.08767569878681e-09, 1.1470745597729725e-11, -4.779477332387385e-14,
-    0.16666666666666666, -0.008333333333333333, 0.0001984126984126984, -2.7557319223985893e-06,
-    2.505210838544172e-08, -1.6059043836821613e-10, 7.647163731819816e-13, -2.8114572543455206e-15};
-// Horner in u of the coefficients c[0 .. kSe3Terms).  The kernels pass a volatile LDS copy of kSe3Coef (read at the
-// use: as 32 literal doubles the constants were hoisted out of the iteration loop into 64 VGPRs for the whole kernel);
-// the host passes kSe3Coef.
+    0.5, 1.0, 0.5, 0.16666666666666666,
+    -0.020833333333333332, -0.125, -0.041666666666666664, -0.008333333333333333,
+    0.00026041666666666666, 0.0026041666666666665, 0.001388888888888889, 0.0001984126984126984,
+    -1.5500992063492063e-06, -2.170138888888889e-05, -2.48015873015873e-05, -2.7557319223985893e-06,
+    5.382288910934745e-09, 9.68812003968254e-08, 2.755731922398589e-07, 2.505210838544172e-08,
+    -1.2232474797578965e-11, -2.691144455467372e-10, -2.08767569878681e-09, -1.6059043836821613e-10,
+    1.9603324996120133e-14, 5.096864498991235e-13, 1.1470745597729725e-11, 7.647163731819816e-13,
+    -2.333729166204778e-17, -7.001187498614334e-16, -4.779477332387385e-14, -2.8114572543455206e-15};
+// The four series by Horner in u, one power at a time for all four (four independent chains; the kernels' LDS copy
+// is then read as two 16-byte loads per power, all issued ahead of the chain).  The kernels pass a pointer into an
+// LDS copy of kSe3Coef whose address they make opaque inside the iteration loop (as 32 literal doubles the constants
+// were hoisted out of it into 64 VGPRs for the whole kernel; read through a volatile pointer each load waited on
+// its own before the next, 32 LDS round trips in a row); the host passes kSe3Coef.
 template <typename P>
-PCORE_GHD double se3_series(P c, double u) {
-    double p = c[kSe3Terms - 1];
+PCORE_GHD void se3_series(P c, double u, double (&out)[4]) {
 PCORE_UNROLL
-    for (int k = kSe3Terms - 2; k >= 0; k--) p = fma_d(p, u, c[k]);
-    return p;
+    for (int f = 0; f < 4; f++) out[f] = c[4 * (kSe3Terms - 1) + f];
+PCORE_UNROLL
+    for (int k = kSe3Terms - 2; k >= 0; k--)
+PCORE_UNROLL
+        for (int f = 0; f < 4; f++) out[f] = fma_d(out[f], u, c[4 * k + f]);
 }
 
 // se3_exp (fast_gicp so3.hpp): so3_exp's quaternion (imag = sin(theta/2)/theta, real = cos(theta/2)), Eigen's
@@ -359,10 +363,12 @@ PCORE_GHD void se3_exp(const double (&a)[6], double (&Rd)[3][3], double (&td)[3]
     const double theta_sq = dot3f(w0, w1, w2, w0, w1, w2);
     double imag, real, c1, c2;
     if (theta_sq < kSe3SeriesMax) {
-        imag = se3_series(coef, theta_sq);
-        real = se3_series(coef + kSe3Terms, theta_sq);
-        c1 = se3_series(coef + 2 * kSe3Terms, theta_sq);
-        c2 = se3_series(coef + 3 * kSe3Terms, theta_sq);
+        double fs[4];
+        se3_series(coef, theta_sq, fs);
+        imag = fs[0];
+        real = fs[1];
+        c1 = fs[2];
+        c2 = fs[3];
     } else {
         const double theta = __builtin_sqrt(theta_sq);
         const double half_theta = 0.5 * theta;

@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(64) lm_bench(const double* systems, int nsys, 
             double a6[6];
             for (int i = 0; i < 6; i++) a6[i] = s[21 + i] * 1e-3 + lambda;
             double Rd[3][3], td[3], R[3][3], tt[3], Ro[3][3], to[3];
-            gicpm::se3_exp(a6, Rd, td, (__attribute__((address_space(3))) const volatile double*)sSe3);
+            gicpm::se3_exp(a6, Rd, td, (__attribute__((address_space(3))) const double*)sSe3);
             for (int i = 0; i < 3; i++) {
                 for (int j = 0; j < 3; j++) R[i][j] = i == j ? 1.0 : 1e-3;
                 tt[i] = 0.1;
