@@ -80,6 +80,17 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// se3_exp's series coefficients as the kernels read them: an LDS copy through an address-space-3 pointer offset by an
+// opaque zero produced inside the iteration loop, so the loads cannot be hoisted out of it (as literal constants they
+// were hoisted into 64 VGPRs for the whole kernel; a generic pointer made them flat loads) but can be issued together
+// ahead of the series (a volatile pointer serialised them: one LDS round trip per coefficient, 32 in a row)
+typedef __attribute__((address_space(3))) const double lds_cvd;
+__device__ __forceinline__ int opaque_zero() {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return z;
+}
+
 __device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
     const float dx = ax - bx, dy = ay - by, dz = az - bz;
     return dx * dx + dy * dy + dz * dz;
@@ -677,7 +688,8 @@ __device__ __forceinline__ const double* wave_tree_sums(const double (&acc)[gicp
         r[0] = own + dpp_d<0x4E, 0xf, 0xf>(0.0, sel);  // quad_perm [2, 3, 0, 1]
     }
     r[0] = r[0] + dpp_d<0xB1, 0xf, 0xf>(0.0, r[0]);    // offset 1: quad_perm [1, 0, 3, 2]
-    if (!(lane & 1) && (lane >> 1) < K) out[lane >> 1] = r[0];
+    // (the slot's address formed here, not hoisted out of the iteration loop into a register that gets spilled)
+    if (!(lane & 1) && (lane >> 1) < K) out[(lane >> 1) + opaque_zero()] = r[0];
     wave_lds_sync();
     return out;
 }
@@ -809,16 +821,6 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
     GPROF_ADD(1, t_s1, t_s2);
 }
 
-// se3_exp's series coefficients as the kernels read them: an LDS copy through an address-space-3 pointer offset by an
-// opaque zero produced inside the iteration loop, so the loads cannot be hoisted out of it (as literal constants they
-// were hoisted into 64 VGPRs for the whole kernel; a generic pointer made them flat loads) but can be issued together
-// ahead of the series (a volatile pointer serialised them: one LDS round trip per coefficient, 32 in a row)
-typedef __attribute__((address_space(3))) const double lds_cvd;
-__device__ __forceinline__ int opaque_zero() {
-    int z;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-    return z;
-}
 
 // One Levenberg-Marquardt iteration of one wave (LsqRegistration::step_lm) on the reduced system `sys` (28 sums in
 // LDS: upper H, b, the error y0 at x): up to kLmMaxTrials solves of (H + lambda I) d = -b, each scored by the error
@@ -875,7 +877,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
             }
         }
         for (int i0 = kLdsPts; i0 < ns; i0 += 64) {
-            const int i = i0 + lane;
+            const int i = i0 + lane + opaque_zero();  // per-lane addresses formed here (hoisted, they were spilled)
             const int j = i < ns ? corr[i] : -1;
             if (j >= 0) {
                 const double2* m2 = reinterpret_cast<const double2*>(mah + (size_t)6 * i);
@@ -983,6 +985,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ float4 sS0[kLdsPts], sT0[kLdsPts];
     __shared__ int sPose;
     __shared__ double sSe3[4 * gicpm::kSe3Terms];  // se3_exp's series coefficients, read at their use
+    __shared__ unsigned sHist[3 * 64];               // the correspondence history's float transforms (below)
     const int lane = threadIdx.x;
     const Round0 r0{sM0, sS0, sT0};
     if (lane < 4 * gicpm::kSe3Terms) sSe3[lane] = gicpm::kSe3Coef[lane];
@@ -1002,11 +1005,12 @@ gicp_kernel(GicpArgs g, int num_poses) {
         xform_identity(x);
         double lambda = -1.0;
         int iters = 0;
-        // correspondence history: lane l holds components 3 (l & 3) + v (v = 0, 1, 2) of set l >> 2's float
-        // transform (R rows 0..2, then t) in hv[v]; `kept` has bit 4e set for every filled set e
+        // correspondence history: sHist[64 v + l] holds component 3 (l & 3) + v (v = 0, 1, 2) of set l >> 2's float
+        // transform (R rows 0..2, then t); `kept` has bit 4e set for every filled set e (the words of unfilled sets
+        // are never compared).  In LDS rather than in three VGPRs per lane: the kernel is at its register budget,
+        // and a history word held in a VGPR was spilled to scratch and reloaded behind a vmcnt(0) every iteration.
         const bool hist = g.corr_hist != nullptr && P.ns <= g.corr_hist_cap;
         int32_t* const hbase = hist ? g.corr_hist + (size_t)pose * kCorrHist * g.corr_hist_cap : nullptr;
-        unsigned hv0 = 0u, hv1 = 0u, hv2 = 0u;
         unsigned long long kept = 0ull;
         int ring = 0;
         const int sub = lane & 3;
@@ -1025,6 +1029,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
                                    b2 = __builtin_bit_cast(unsigned, c2);
                     // bitwise equality (-0 != +0, NaN == NaN): the float queries, and so the correspondences, are
                     // functions of these bits
+                    const unsigned hv0 = sHist[lane], hv1 = sHist[64 + lane], hv2 = sHist[128 + lane];
                     const unsigned long long eq = __ballot(b0 == hv0 && b1 == hv1 && b2 == hv2);
                     const unsigned long long full = eq & (eq >> 1) & (eq >> 2) & (eq >> 3) & kept;
                     int e;
@@ -1035,10 +1040,10 @@ gicp_kernel(GicpArgs g, int num_poses) {
                         e = ring;
                         ring = ring + 1 == kCorrHist ? 0 : ring + 1;
                         kept |= 1ull << (4 * e);
-                        if ((lane >> 2) == e) {
-                            hv0 = b0;
-                            hv1 = b1;
-                            hv2 = b2;
+                        if ((lane >> 2) == e) {  // every lane reads back only the words it wrote itself
+                            sHist[lane] = b0;
+                            sHist[64 + lane] = b1;
+                            sHist[128 + lane] = b2;
                         }
                     }
                     cset = hbase + (size_t)__builtin_amdgcn_readfirstlane(e) * g.corr_hist_cap;
