@@ -526,6 +526,41 @@ def test_evaluate_icp_matches_oracle(fixture, kernel, request, monkeypatch):
     assert _bits_equal(df.cpu().numpy(), odf)
 
 
+@pytest.mark.parametrize("kernel", ["narrow", "wide"])
+def test_evaluate_icp_edge_poses_match_oracle(one_object, kernel, monkeypatch):
+    """GICP on the edge-pose batch: empty source clouds (behind the camera, out of view), clouds of a few points
+    (fewer than k = 10 neighbours), and poses so close that the cloud fills most of the sampled image -- more points
+    than the correspondence history holds and than the trials keep in LDS, so those poses search every iteration and
+    read their later rounds' trial inputs from scratch.  Iterations, refined poses and costs bit for bit."""
+    case, core, t = one_object
+    sc = case.scene
+    p16 = init_from_eigen_batch(_edge_pose_batch())
+    n = len(p16)
+    dev = t["poses"].device
+    poses = torch.from_numpy(p16).to(dev)
+    pm = torch.zeros(n, dtype=torch.int32, device=dev)
+    pl = torch.zeros(n, dtype=torch.int32, device=dev)
+    tot_h = np.full(n, case.pose_obs_total[0], np.float32)
+    tot = torch.from_numpy(tot_h).to(dev)
+    monkeypatch.setenv("PCORE_GICP_KERNEL", kernel)
+    adj, iters, rc, oc, df = core.evaluate_icp(poses, pm, pl, tot, cost_type=2, stride=case.stride)
+    z = np.zeros(n, np.int32)
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, p16, z, z, sc.width, sc.height, sc.proj, sc.src_depth_cm, sc.mask,
+        1.0, case.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, case.obs_xyz, _label_covs(case), case.label_start,
+        case.label_end, tot_h, 2, True, 0.01)
+    counts = [len(oracle.depth_to_cloud(d, case.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0)[0])
+              for d in oracle.render_depth(sc.bank.tris, sc.bank.tris_model_count, p16, z, z, sc.width, sc.height,
+                                           sc.proj, sc.src_depth_cm, sc.mask, 1.0)]
+    # the batch covers the cases named above: empty, fewer than k points, more than kCorrHistCap (512) points
+    assert min(counts) == 0 and any(0 < c < 10 for c in counts) and max(counts) > 512, counts
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert _bits_equal(adj.cpu().numpy(), oadj)
+    assert _bits_equal(rc.cpu().numpy(), orc)
+    assert _bits_equal(oc.cpu().numpy(), ooc)
+    assert _bits_equal(df.cpu().numpy(), odf)
+
+
 def test_evaluate_icp_chunked_cloud_tile_matches_oracle(three_objects, monkeypatch):
     """With a 64-sample tile the GICP source clouds are rastered in chunks of the tile (render_cloud_kernel's row
     bands / column blocks) and appended chunk after chunk: the reference's row-major compaction order, so the refined
