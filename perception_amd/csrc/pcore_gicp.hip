@@ -67,6 +67,22 @@ __device__ unsigned long long g_gicp_prof[kGprof];
 #define GPROF_PARAM
 #define GPROF_ARG
 #endif
+// Build with -DPCORE_GICP_TIMELINE (tools only, tools/gicp_timeline.py): gicp_kernel records, per pose, the real-time
+// clock (100 MHz) when a wave dequeues it and when it writes the refined pose, and per wave its start and exit.
+#ifdef PCORE_GICP_TIMELINE
+constexpr int kTlPoses = 1 << 17, kTlWaves = 1 << 14;
+__device__ unsigned long long g_tl_pose[2 * kTlPoses];
+__device__ unsigned long long g_tl_wave[2 * kTlWaves];
+__device__ unsigned int g_tl_nwaves;
+extern "C" int pcore_debug_gicp_timeline(unsigned long long* poses, unsigned long long* waves, unsigned int* nwaves) {
+    hipError_t e = hipMemcpyFromSymbol(poses, HIP_SYMBOL(g_tl_pose), sizeof(g_tl_pose));
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_tl_wave), sizeof(g_tl_wave));
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(nwaves, HIP_SYMBOL(g_tl_nwaves), sizeof(unsigned int));
+    const unsigned int z = 0;
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_tl_nwaves), &z, sizeof(z));
+    return e == hipSuccess ? 0 : 1;
+}
+#endif
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -990,6 +1006,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
     const Round0 r0{sM0, sS0, sT0};
     if (lane < 4 * gicpm::kSe3Terms) sSe3[lane] = gicpm::kSe3Coef[lane];
     GPROF_DECL;
+#ifdef PCORE_GICP_TIMELINE
+    const unsigned long long tl_w0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (;;) {
         wave_lds_sync();  // the previous pose's reads of sPose are done
         if (lane == 0) {
@@ -1000,6 +1019,9 @@ gicp_kernel(GicpArgs g, int num_poses) {
         const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
         if (pose >= num_poses) break;
         const GicpPose P = gicp_pose(g, pose);
+#ifdef PCORE_GICP_TIMELINE
+        const unsigned long long tl_p0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const LabelGrid G{};  // linearize_round's grid argument, unused here: the searches below load the grid
         Xform x;
         xform_identity(x);
@@ -1112,8 +1134,23 @@ gicp_kernel(GicpArgs g, int num_poses) {
             }
         }
         if (lane == 0) write_pose(g, P.gp, x, iters);
+#ifdef PCORE_GICP_TIMELINE
+        if (lane == 0 && P.gp < kTlPoses) {
+            g_tl_pose[2 * P.gp] = tl_p0;
+            g_tl_pose[2 * P.gp + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
     }
     GPROF_FLUSH;
+#ifdef PCORE_GICP_TIMELINE
+    if (lane == 0) {
+        const unsigned int w = atomicAdd(&g_tl_nwaves, 1u);
+        if (w < (unsigned)kTlWaves) {
+            g_tl_wave[2 * w] = tl_w0;
+            g_tl_wave[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+#endif
 }
 
 
