@@ -307,11 +307,15 @@ __device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[K
 // scan's order (a 256-thread workgroup per segment left two of its four waves idle on C3's ~111-point clouds).
 // C3: 2.65 -> 2.61 ms per 50 k clouds -- the time is the insertion block, which the wave runs whenever any lane
 // inserts (k ln(n / k) + k insertions per point), not the candidate loads.
+// KFIXED: k == KMAX known at compile time (GICP's k = 10): the list's last entry and every `q < k` test are static,
+// so the insertion is straight-line code; with a run-time k the compiler indexed nd[k - 1] through s_set_gpr_idx and
+// branched once per list entry.
 constexpr int kCovLanes = 64;
-template <int KMAX>
+template <int KMAX, bool KFIXED = false>
 __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts, const int32_t* seg_off,
-                                                               const int32_t* seg_cnt, int seg_stride, int k,
+                                                               const int32_t* seg_cnt, int seg_stride, int k_arg,
                                                                double* cov_out, int max_n) {
+    const int k = KFIXED ? KMAX : k_arg;
     __shared__ float4 tile[kCovLanes];
     const int sg = blockIdx.x;
     const int off = seg_off ? seg_off[sg] : sg * seg_stride;
@@ -362,32 +366,31 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
             if (j0 + lane < n) tile[lane] = P[j0 + lane];
             wave_lds_sync();
             const int jn = min(kCovLanes, n - j0);
+            float4 xn = tile[0];  // (jn >= 1 here) the next candidate's read is issued before this one's insertion
             for (int jj = 0; jj < jn; jj++) {
-                const float4 xj = tile[jj];
+                const float4 xj = xn;
+                xn = tile[jj + 1 < jn ? jj + 1 : jj];
                 const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
                 const int j = j0 + jj;
                 if (cnt < k || nan_list) {  // the first k candidates (every lane at once), or a NaN list
                     insert_counting(d, j);
                 } else if (d < nd[k - 1]) {
                     // a full, sorted list (no NaN: one could only enter among the first k): the counting insertion's
-                    // result in one pass -- entry q moves right where nd[q] > d, and the first such entry's slot
-                    // takes the new element (d < nd[k - 1], so there is one)
-                    bool gp = false;  // (old) nd[q - 1] > d
-                    float pd = d;     // old nd[q - 1], nb[q - 1]
-                    int pb = j;
+                    // result in one pass -- the entries greater than d (a suffix, the list being sorted) move right by
+                    // one and d takes the first of their slots (d < nd[k - 1], so there is one).  Written from the
+                    // end, each entry reads its left neighbour before that one is overwritten: no temporaries.
+                    bool g[KMAX];
 #pragma unroll
-                    for (int q = 0; q < KMAX; q++) {
+                    for (int q = 0; q < KMAX; q++) g[q] = q < k && nd[q] > d;
+#pragma unroll
+                    for (int q = KMAX - 1; q >= 1; q--) {
                         if (q < k) {
-                            const float od = nd[q];
-                            const int ob = nb[q];
-                            const bool g = od > d;
-                            nd[q] = g ? (gp ? pd : d) : od;
-                            nb[q] = g ? (gp ? pb : j) : ob;
-                            gp = g;
-                            pd = od;
-                            pb = ob;
+                            nd[q] = g[q - 1] ? nd[q - 1] : (g[q] ? d : nd[q]);
+                            nb[q] = g[q - 1] ? nb[q - 1] : (g[q] ? j : nb[q]);
                         }
                     }
+                    nd[0] = g[0] ? d : nd[0];
+                    nb[0] = g[0] ? j : nb[0];
                 }
             }
         }
@@ -433,7 +436,10 @@ hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const i
                               int num_segs, int k, double* cov_out, hipStream_t s, int max_n) {
     if (num_segs <= 0) return hipSuccess;
     if (k <= 0 || k > kMaxK) return hipErrorInvalidValue;
-    if (k <= 10)
+    if (k == 10)
+        hipLaunchKernelGGL((covariance_kernel<10, true>), dim3(num_segs), dim3(kCovLanes), 0, s, pts, seg_off, seg_cnt,
+                           seg_stride, k, cov_out, max_n);
+    else if (k < 10)
         hipLaunchKernelGGL(covariance_kernel<10>, dim3(num_segs), dim3(kCovLanes), 0, s, pts, seg_off, seg_cnt,
                            seg_stride, k, cov_out, max_n);
     else
