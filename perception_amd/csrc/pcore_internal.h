@@ -55,6 +55,9 @@ struct LabelGrid {
 
 // tile tiers of the fused window launch: workgroups per CU PCORE_TIER_MAX, ..., 3, 2 (the LDS tile that
 // leaves room for that many workgroups); the host picks the tier from the previous call's window histogram
+#ifndef PCORE_DEBUG_SKIP_RT
+#define PCORE_DEBUG_SKIP_RT 0  // 1: the fused kernels honour PCORE_DEBUG_SKIP (ablation builds, tools/ablate_sq.sh)
+#endif
 #ifndef PCORE_TIER_MAX
 #define PCORE_TIER_MAX 6
 #endif
@@ -122,7 +125,7 @@ struct FusedArgs {
     int32_t fb_seq;
     // ablation knob for profiling (PCORE_DEBUG_SKIP): bit0 skip sample raster, bit1 skip triangle stage,
     // bit2 skip phase 2 (cloud/NN), bit3 skip vertex stage.  0 in production.
-    int32_t dbg_skip;
+    int32_t dbg_skip;  // PCORE_DEBUG_SKIP, read by the kernels only in a -DPCORE_DEBUG_SKIP_RT=1 build
     // pcore_evaluate_select: each pose's argmin key (select_kernel's) folded into sel_keys[model] by the launch
     // that scores it (nullptr: plain pcore_evaluate)
     int64_t* sel_keys;

@@ -426,7 +426,13 @@ __device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem
     // vertex pass would overwrite vertices a pending record may reference, at a stream switch and at the end.
     int rec_total = 0, rec_done = 0;
 
+    // PCORE_DEBUG_SKIP ablations only in a -DPCORE_DEBUG_SKIP_RT=1 build (tools/ablate_sq.sh): a run-time flag kept as a
+    // lane-mask boolean across the step loop cost two VALU per test per step
+#if PCORE_DEBUG_SKIP_RT
     const int dbg = a.dbg_skip;
+#else
+    constexpr int dbg = 0;
+#endif
     auto flush = [&](int count) {  // the `count` oldest pending records
         fp.mark(2);
         wave_sync();
@@ -938,7 +944,11 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
         const int k = base + lane;
         bool valid = false;
         int kx = 0, ky = 0;
+#if PCORE_DEBUG_SKIP_RT
         if (k < tn && !(a.dbg_skip & 4)) {
+#else
+        if (k < tn) {
+#endif
             int iy = (int)(((float)k + 0.5f) * inv_nx), ix = k - iy * sw.nx;
             if (ix < 0) { iy--; ix += sw.nx; } else if (ix >= sw.nx) { iy++; ix -= sw.nx; }
             kx = sw.x0 + ix;
