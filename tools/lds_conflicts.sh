@@ -1,7 +1,8 @@
 #!/bin/bash
 # LDS bank conflicts of the fused kernel per library build (LIBS) and PCORE_DEBUG_SKIP ablation mask (MASKS: 1 skips
 # the record flush, 2 the triangle stage, 4 phase 2, 8 the vertex stage): SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE of
-# one counters-only rocprofv3 pass each, on the C2 launch of tools/prof_fused.py.
+# one counters-only rocprofv3 pass each, on the C2 launch of tools/prof_fused.py.  Masks other than 0 need builds with
+# -DPCORE_DEBUG_SKIP_RT=1 (tools/build_variant.sh NAME -DPCORE_DEBUG_SKIP_RT=1): the production library ignores them.
 set -o pipefail
 OUT=${OUT:-gpurun_out}; export TMPDIR=/tmp; mkdir -p $OUT
 for L in ${LIBS:-perception_amd/libpcore.so}; do
