@@ -379,9 +379,13 @@ extern "C" int pcore_debug_flush_stats(unsigned long long* host) {
 }
 #endif
 
-template <int STRIDE, bool IDPASS = false>
-__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw,
+// FD: the pose's fastdiv flag known at compile time (0 / 1; the depth pass instantiates both and picks one per pose, so
+// a fastdiv pose's steps carry no NaN-triangle test or range checks at all), or -1 to read it from the window
+template <int STRIDE, bool IDPASS = false, int FD = -1>
+__device__ __forceinline__ void raster_phase(const FusedArgs& a, const FusedSmem& sm, int pose, const SampleWin& sw_in,
                                              int32_t* cid, FProf& fp) {
+    SampleWin sw = sw_in;
+    if constexpr (FD >= 0) sw.fastdiv = FD;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads of stream headers
     const int lane = tid & 63;
@@ -831,7 +835,8 @@ __device__ __forceinline__ void fused_pose(const FusedArgs& a, const FusedSmem& 
     auto chunk = [&](const SampleWin& sw) __attribute__((always_inline)) {
     const int tn = sw.nx * sw.ny;  // samples of the chunk (tile)
     for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
-    raster_phase<STRIDE>(a, sm, pose, sw, nullptr, fp);
+    if (sw.fastdiv) raster_phase<STRIDE, false, 1>(a, sm, pose, sw, nullptr, fp);
+    else raster_phase<STRIDE, false, 0>(a, sm, pose, sw, nullptr, fp);
     fp.mark(2);
     __syncthreads();
     fp.mark(4);
@@ -1194,7 +1199,8 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
     auto chunk = [&](const SampleWin& cw) __attribute__((always_inline)) {
         const int tn = cw.nx * cw.ny;
         for (int i = tid; i < tn; i += kThreads) sm.zbuf[i] = INT_MAX;
-        raster_phase<STRIDE>(a, sm, pose, cw, nullptr, fp);
+        if (cw.fastdiv) raster_phase<STRIDE, false, 1>(a, sm, pose, cw, nullptr, fp);
+        else raster_phase<STRIDE, false, 0>(a, sm, pose, cw, nullptr, fp);
         __syncthreads();
         const float inv_nx = tn > 0 ? 1.0f / (float)cw.nx : 0.0f;
         for (int base = 0; base < tn; base += kThreads) {
