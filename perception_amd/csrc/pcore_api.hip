@@ -1032,6 +1032,16 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.grids = c->grids.p;
     g.cell_start = c->cell_start.p;
     g.grid_pts = c->grid_pts.p;
+    // the GICP kernel instance with the grid search only when some segment the poses can use is large (gicp_pose:
+    // use_grid = nt > kGridNNMin with grids present); 6-DoF poses use their label's segment, 3-DoF the whole cloud
+    bool grid_needed = false;
+    if (c->grids.p) {
+        if (six) {
+            for (int L = 0; L < nl; L++) grid_needed = grid_needed || c->seg_cnt_h[L] > kGridNNMin;
+        } else {
+            grid_needed = c->seg_cnt_h[nl] > kGridNNMin;
+        }
+    }
     for (int base = 0; base < num_poses; base += chunk) {
         const int n = std::min(chunk, num_poses - base);
         a.poses = d_poses + (size_t)16 * base;
@@ -1057,7 +1067,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
             g.pose_order = c->icp_order_idx.p + chunk;
         }
         if (ev) HIPC(c, hipEventRecord(ev[1], s));
-        HIPC(c, launch_gicp(g, n, c->dinfo, s));
+        HIPC(c, launch_gicp(g, n, c->dinfo, s, grid_needed));
         if (ev) {
             HIPC(c, hipEventRecord(ev[2], s));
             c->icp_ev_used++;

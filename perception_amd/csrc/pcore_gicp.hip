@@ -1000,6 +1000,10 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
 #define PCORE_GICP_WAVES_PER_EU 3
 #endif
 
+// GRID: the kernel holds the exact grid search of large segments (> kGridNNMin targets).  launch_gicp picks the
+// instance without it when no segment of the observation is that large (every C2-C5 label): the search's registers
+// then weigh on no pose (gicp_kernel 12.1 -> 11.9 ms per C3 call).
+template <bool GRID>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
 gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ double sRed[gicpm::kTerms];
@@ -1099,7 +1103,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
                         float qa[3], qb[3];
                         gicpm::query_f(Rf, tf, sa.x, sa.y, sa.z, qa);
                         gicpm::query_f(Rf, tf, sb.x, sb.y, sb.z, qb);
-                        if (P.use_grid) {  // segments above kGridNNMin (the grid is read here, not held per pose)
+                        if (GRID && P.use_grid) {  // segments above kGridNNMin (the grid is read here, not per pose)
                             const LabelGrid Gs = g.grids[P.seg];
                             float best;
                             if (ia < P.ns) grid_nn(Gs, g.cell_start, g.grid_pts, P.tgt, P.nt, qa[0], qa[1], qa[2], best, ja);
@@ -1327,10 +1331,14 @@ hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32
 
 hipError_t gicp_occupancy_per_cu(int* per_cu) {
     *per_cu = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel, 64, 0);
+    int other = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel<true>, 64, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&other, gicp_kernel<false>, 64, 0);
+    if (e == hipSuccess) *per_cu = std::min(*per_cu, other);
+    return e;
 }
 
-hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s) {
+hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s, bool grid) {
     if (num_poses <= 0) return hipSuccess;
     const int resident_wgs = std::max(1, d.gicp_resident_wgs), num_cus = std::max(1, d.num_cus);
     hipError_t e = hipMemsetAsync(g.work_counter, 0, sizeof(int32_t), s);
@@ -1348,7 +1356,10 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hi
                            num_poses);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(gicp_kernel, dim3(std::min(resident_wgs, num_poses)), dim3(64), 0, s, g, num_poses);
+    if (grid)
+        hipLaunchKernelGGL(gicp_kernel<true>, dim3(std::min(resident_wgs, num_poses)), dim3(64), 0, s, g, num_poses);
+    else
+        hipLaunchKernelGGL(gicp_kernel<false>, dim3(std::min(resident_wgs, num_poses)), dim3(64), 0, s, g, num_poses);
     return hipGetLastError();
 }
 

@@ -212,7 +212,8 @@ hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const i
 hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_host, const int32_t* seg_cnt_host,
                                    int num_segs, int first_grid, const LabelGrid* grids, const int32_t* cell_start,
                                    const float4* grid_pts, int k, double* cov_out, hipStream_t s);
-hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s);
+// grid: some segment the poses may use has more than kGridNNMin targets (the kernel instance with the grid search)
+hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s, bool grid = true);
 // scratch of launch_gicp_order: 4 arrays of n 32-bit words + the radix sort's temporary storage
 size_t gicp_order_temp_bytes(int n);
 // g.pose_order for a chunk of n poses whose clouds are rendered (g.src_count): chunk-local indices sorted by
