@@ -110,7 +110,7 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
     import torch
     from perception_amd import distributed as pdist
     from perception_amd import workloads
-    from perception_amd._native import PCORE_KEY_NONE
+    from perception_amd._native import ICP_CYCLE_WINDOW, PCORE_KEY_NONE
     from perception_amd.core import decode_keys
 
     w = workloads.build(names=C3_NAMES, poses_per_model=poses_per_model, device=local, rank=rank)
@@ -119,42 +119,56 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
     out = (torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
            *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)))
     keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev)
-    gicp_ms, icp_s = [], []
+    rec = {"gicp_ms": [], "icp_s": [], "run": [], "exits": []}
 
-    def step(record):
+    def step(record, window):
         keys.fill_(PCORE_KEY_NONE)
         adj, it, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
-                                                  stride=w.stride, out=out)
+                                                  stride=w.stride, out=out, cycle_exit_window=window)
         w.core.select(rc, oc, w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
         if record:
             st = w.core.stats()  # waits for this step's GICP stage (events), not for the re-score
-            gicp_ms.append(st["gicp_ms"])
-            icp_s.append(st["icp_runtime"])
+            rec["gicp_ms"].append(st["gicp_ms"])
+            rec["icp_s"].append(st["icp_runtime"])
+            rec["run"].append(st["gicp_iterations_run"])
+            rec["exits"].append(st["gicp_cycle_exits"])
         work = pdist.allreduce_min_keys_async(keys)
         if work is not None:
             work.wait()
 
-    for _ in range(max(warmup, 1)):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(window):
+        for k in rec:
+            rec[k] = []
+        for _ in range(max(warmup, 1)):
+            step(False, window)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(True, window)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, {k: list(v) for k, v in rec.items()}
+
+    # the A/B first: every iteration run out (fast_gicp's loop, cycle_exit_window 0), then the spec's exit -- the
+    # measured run -- so out / keys hold the spec's results afterwards
+    el_off, rec_off = timed(0)
+    its_off = out[1].cpu().numpy()
+    elapsed, r = timed(ICP_CYCLE_WINDOW)
+    gicp_ms, icp_s = r["gicp_ms"], r["icp_s"]
     its = out[1].cpu().numpy()
     cost, idx = decode_keys(keys)
     g_ms = float(np.mean(gicp_ms)) if gicp_ms else None
     iter_total = int(its.sum())
+    iter_run = int(np.mean(r["run"])) if r["run"] else iter_total
     valu_peak = VALU_SIMDS * VALU_CLOCK_HZ / 2.0
     instr_per_iter, cyc_per_iter, sq_note = None, None, "no profiles/sq_counters_gicp.json"
     sq_path = os.path.join(ROOT, "profiles", "sq_counters_gicp.json")
@@ -172,10 +186,11 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
                            "pass of the same GICP sources)")
         except (OSError, ValueError, KeyError) as e:
             sq_note = f"unreadable counter profile: {e}"
-    achieved = instr_per_iter * iter_total / (g_ms * 1e-3) if (instr_per_iter and g_ms) else None
+    # the executed pose-iterations (the cycle exits' are not run) are the work of the GICP launches
+    achieved = instr_per_iter * iter_run / (g_ms * 1e-3) if (instr_per_iter and g_ms) else None
     # the same work priced in SIMD cycles (f64 and transcendental instructions 4 cycles per wave64 instruction,
     # the rest 2) against 1024 SIMDs x 2.4 GHz
-    busy = (float(cyc_per_iter) * iter_total / (g_ms * 1e-3) / (VALU_SIMDS * VALU_CLOCK_HZ)
+    busy = (float(cyc_per_iter) * iter_run / (g_ms * 1e-3) / (VALU_SIMDS * VALU_CLOCK_HZ)
             if (cyc_per_iter and g_ms) else None)
     return {
         "metric": "candidate poses rendered+GICP-refined+scored/sec @640x480 (C3)",
@@ -190,6 +205,15 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
         "gicp": {"iterations_mean": float(its.mean()), "iterations_p50": float(np.percentile(its, 50)),
                  "iterations_p90": float(np.percentile(its, 90)), "at_max_iterations": int((its >= 150).sum()),
                  "gicp_ms_per_step": g_ms, "icp_stage_ms_per_step": float(np.mean(icp_s)) * 1e3 if icp_s else None,
+                 "cycle_exit_window": ICP_CYCLE_WINDOW,
+                 "iterations_reported_per_step": iter_total, "iterations_run_per_step": iter_run,
+                 "cycle_exits_per_step": int(np.mean(r["exits"])) if r["exits"] else None,
+                 "exit_off": {"value": n * world * steps / el_off, "ms_per_step": el_off * 1e3 / steps,
+                              "gicp_ms_per_step": float(np.mean(rec_off["gicp_ms"])) if rec_off["gicp_ms"] else None,
+                              "iterations_run_per_step": int(np.mean(rec_off["run"])) if rec_off["run"] else None,
+                              "iterations_equal": bool(np.array_equal(its, its_off)),
+                              "note": "the same steps with cycle_exit_window 0 (every iteration run out, as "
+                                      "fast_gicp), timed before the measured run"},
                  "timing": "pcore_get_stats: HIP events on the call's stream around the GICP launches / the "
                            "covariances + GICP launches of every timed step"},
         "roofline": {"bound": "valu", "kernel": "gicp_kernel",

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PCORE_ABI_VERSION 6
+#define PCORE_ABI_VERSION 7
 
 enum pcore_status {
     PCORE_OK = 0,
@@ -149,12 +149,18 @@ int pcore_evaluate(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_m
                    const pcore_eval_params* params, float* d_out_rc, float* d_out_oc, float* d_out_diff,
                    int32_t* d_dbg_zs, pcore_stream stream);
 
-/* GICP settings; the reference hard-codes them at renderer.cu:1696-1705. */
+/* GICP settings; the reference hard-codes the first four at renderer.cu:1696-1705.  cycle_exit_window (no
+ * reference counterpart): a pose whose float transforms have recurred with the same period for
+ * this many iterations, each step accepted at its first trial with an inert damping, stops and reports
+ * max_iterations and the cycle member the remaining iterations end on; 0 runs every iteration out, as fast_gicp
+ * does; the spec's value is 8 (PCORE_GICP_CYCLE_WINDOW). */
+#define PCORE_GICP_CYCLE_WINDOW 8
 typedef struct pcore_icp_params {
     int32_t k_correspondences;      /* covariance neighbours, 10 (<= 16) */
     int32_t max_iterations;         /* 150 */
     double rotation_epsilon;        /* 2e-3 */
     double transformation_epsilon;  /* 5e-4 */
+    int32_t cycle_exit_window;      /* 8 (0 = off) */
 } pcore_icp_params;
 
 /* pcore_evaluate followed by pcore_select in one launch: every pose's argmin key (pcore_select's, global index
@@ -193,12 +199,17 @@ int pcore_render(pcore_ctx* ctx, const float* d_poses, const int32_t* d_pose_mod
  * pcore_evaluate_icp: icp_runtime = seconds of its GICP stage (source covariances + GICP launches, HIP events on
  * the call's stream -- this call waits for them); peak_memory_usage = the most device memory in use (MB,
  * hipMemGetInfo like print_cuda_memory_usage, cuda/utils.cuh:6-24) at a GICP stage since the last reset;
- * gicp_ms = the GICP launches alone; icp_chunks = chunks the batch ran in.  reset != 0 restarts the peak. */
+ * gicp_ms = the GICP launches alone; icp_chunks = chunks the batch ran in; gicp_iterations = the iterations the
+ * poses report (d_out_iters summed), gicp_iterations_run = the iterations executed (fewer by the cycle exits),
+ * gicp_cycle_exits = poses that left by the cycle exit.  reset != 0 restarts the peak. */
 typedef struct pcore_gpu_stats {
     float icp_runtime;
     double peak_memory_usage;
     float gicp_ms;
     int32_t icp_chunks;
+    int64_t gicp_iterations;
+    int64_t gicp_iterations_run;
+    int64_t gicp_cycle_exits;
 } pcore_gpu_stats;
 int pcore_get_stats(pcore_ctx* ctx, pcore_gpu_stats* out, int32_t reset);
 

@@ -217,16 +217,16 @@ def _gicp_lib():
         c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
         L.orc_covariances.argtypes = [_f32p, c_int, c_int, _f64p]
         L.orc_gicp.restype = c_int
-        L.orc_gicp.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, _f64p]
+        L.orc_gicp.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, c_int, _f64p]
         L.orc_concat_pose.argtypes = [_f64p, _f32p, _f32p]
         L.orc_evaluate_icp.argtypes = [_f32p, c_int, _i32p, c_int, _f32p, _i32p, _opt(_i32p), c_int, c_int, c_int,
                                        _f32p, _i32p, _opt(_u8p), c_float, c_int, c_float, c_float, c_float, c_float,
                                        c_float, _f32p, _f64p, c_int, _opt(_i32p), _opt(_i32p), c_int, _opt(_f32p),
-                                       c_int, c_int, c_float, c_int, c_int, c_double, c_double, _f32p, _opt(_i32p),
-                                       _f32p, _f32p, _f32p, c_int]
+                                       c_int, c_int, c_float, c_int, c_int, c_double, c_double, c_int, _f32p,
+                                       _opt(_i32p), _f32p, _f32p, _f32p, c_int]
         L.orc_gicp_trace.restype = c_int
-        L.orc_gicp_trace.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, _f64p,
-                                     _opt(_f64p)]
+        L.orc_gicp_trace.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, c_int,
+                                     _f64p, _opt(_f64p), _opt(_i32p)]
         L.orc_gicp_linearize.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, _f64p, c_int, _i32p, _f64p]
         L.orc_gicp_se3_exp.argtypes = [_f64p, _f64p]
         L.orc_gicp_lm_solve.argtypes = [_f64p, c_double, _f64p]
@@ -246,6 +246,7 @@ GICP_K = 10            # renderer.cu:1697 k_correspondences_
 GICP_MAX_ITER = 150    # renderer.cu:1696
 GICP_ROT_EPS = float(np.float32(2e-3))    # renderer.cu:1698 (a float widened to double)
 GICP_TRANS_EPS = float(np.float32(5e-4))  # renderer.cu:1699 (a float widened to double)
+GICP_CYCLE_WINDOW = 8  # the spec's cycle exit window W (pcore_gicp_math.h kCycleWindow; 0 = run the iterations out)
 
 
 def covariances(xyz, k=GICP_K):
@@ -256,7 +257,8 @@ def covariances(xyz, k=GICP_K):
     return out[:len(xyz)]
 
 
-def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS):
+def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS,
+         cycle_window=GICP_CYCLE_WINDOW):
     src = _c(src, np.float32).reshape(-1, 3)
     tgt = _c(tgt, np.float32).reshape(-1, 3)
     T = np.zeros(16, np.float64)
@@ -264,21 +266,24 @@ def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EP
     it = _gicp_lib().orc_gicp(src.reshape(-1) if len(src) else z3, _c(src_cov, np.float64).reshape(-1) if len(src) else z6,
                               len(src), tgt.reshape(-1) if len(tgt) else z3,
                               _c(tgt_cov, np.float64).reshape(-1) if len(tgt) else z6, len(tgt), max_iter, rot_eps,
-                              trans_eps, T)
+                              trans_eps, int(cycle_window), T)
     return T.reshape(4, 4), it
 
 
-def gicp_trace(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS):
-    """orc_gicp with its per-iteration trace: (T, iterations, trace (iterations, 16): R (9), t (3) after each
-    iteration, the lambda of its first trial, its number of trials, 0, the LM status)."""
+def gicp_trace(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS,
+               cycle_window=0):
+    """orc_gicp with its per-iteration trace: (T, iterations reported, trace (executed iterations, 16): R (9), t (3)
+    after each iteration, the lambda of its first trial, its number of trials, flags (1: lambda inert, 2: accepted
+    with rho >= 1/2), the LM status).  The cycle exit is off unless cycle_window > 0."""
     src = _c(src, np.float32).reshape(-1, 3)
     tgt = _c(tgt, np.float32).reshape(-1, 3)
     T = np.zeros(16, np.float64)
     tr = np.zeros((max_iter, 16), np.float64)
+    ex = np.zeros(1, np.int32)
     it = _gicp_lib().orc_gicp_trace(src.reshape(-1), _c(src_cov, np.float64).reshape(-1), len(src), tgt.reshape(-1),
-                                    _c(tgt_cov, np.float64).reshape(-1), len(tgt), max_iter, rot_eps, trans_eps, T,
-                                    tr.reshape(-1))
-    return T.reshape(4, 4), it, tr[:it]
+                                    _c(tgt_cov, np.float64).reshape(-1), len(tgt), max_iter, rot_eps, trans_eps,
+                                    int(cycle_window), T, tr.reshape(-1), ex)
+    return T.reshape(4, 4), it, tr[:int(ex[0])]
 
 
 def gicp_linearize(src, src_cov, tgt, tgt_cov, T, textbook=False):
@@ -354,7 +359,7 @@ def concat_pose(T, pose):
 def evaluate_icp(tris, tris_model_count, poses, pose_model, pose_label, width, height, proj, src_depth, src_mask,
                  occlusion_threshold, stride, cx, cy, fx, fy, depth_factor, o_xyz, o_cov, label_start, label_end,
                  pose_obs_total, cost_type, calc_obs, sensor_resolution, k=GICP_K, max_iter=GICP_MAX_ITER,
-                 rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS, nthreads=0):
+                 rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS, nthreads=0, cycle_window=GICP_CYCLE_WINDOW):
     """do_icp flow; returns (adjusted poses (N,16), iterations (N,), rc, oc, diff)."""
     tris = _c(tris, np.float32).reshape(-1)
     poses = _c(poses, np.float32).reshape(-1)
@@ -374,7 +379,7 @@ def evaluate_icp(tris, tris_model_count, poses, pose_model, pose_label, width, h
         fx, fy, depth_factor, o_xyz if o_xyz.size else np.zeros(3, np.float32),
         o_cov if o_cov.size else np.zeros(6, np.float64), o_xyz.size // 3, _c(label_start, np.int32),
         _c(label_end, np.int32), nl, _c(pose_obs_total, np.float32), cost_type, int(calc_obs), sensor_resolution, k,
-        max_iter, rot_eps, trans_eps, adj.reshape(-1), iters, rc, oc, df, nthreads)
+        max_iter, rot_eps, trans_eps, int(cycle_window), adj.reshape(-1), iters, rc, oc, df, nthreads)
     return adj, iters, rc, oc, df
 
 

@@ -8,6 +8,7 @@
 #include "../perception_amd/csrc/pcore_colour.h"
 #include "../perception_amd/csrc/pcore_gicp_math.h"
 
+#include <array>
 #include <climits>
 #include <cfloat>
 #include <cmath>
@@ -635,13 +636,14 @@ void gicp_linearize_spec(const OXform& x, const float* src_xyz, const double* sr
 // One LM iteration (LsqRegistration::step_lm) on the reduced system, as the GPU's lm_iteration
 int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double& lambda, const float* src_xyz, int ns,
                       const float* tgt_xyz, const int32_t* corr, const double* mah, double rot_eps, double trans_eps,
-                      double* lambda_used, int* trials = nullptr) {
+                      double* lambda_used, int* trials = nullptr, int* flags = nullptr) {
     namespace gm = pcore::gicpm;
     const double y0 = sys[gm::kErr];
     if (lambda < 0.0) lambda = gm::lm_init_lambda(sys);
     double nu = 2.0;
     std::vector<double> part(64);
     *lambda_used = lambda;
+    if (flags) *flags = gm::lm_lambda_inert(sys, lambda) ? 1 : 0;
     for (int trial = 0; trial < gm::kLmMaxTrials; trial++) {
         if (trials) *trials = trial + 1;
         double d[6];
@@ -673,6 +675,7 @@ int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double&
             continue;
         }
         x = xi;
+        if (flags && rho >= 0.5) *flags |= 2;
         lambda = gm::lm_accept_lambda(lambda, rho);
         return gm::is_converged(Rd, td, rot_eps, trans_eps) ? gm::kLmConverged : gm::kLmAccepted;
     }
@@ -781,22 +784,41 @@ void orc_covariances(const float* xyz, int n, int k, double* out_cov6) {
 }
 
 // The spec's GICP with an optional per-iteration trace (max_iter x 16: R, t after the iteration, the lambda of its
-// first trial, its number of trials, 0, the LM status).
+// first trial, its number of trials, flags (1: lambda inert on its system, 2: accepted with rho >= 1/2), the LM
+// status) and the cycle exit of window cycle_window (0: off; pcore_gicp_math.h cycle_update).  Returns the iterations
+// reported (max_iter after a cycle exit); *executed (nullable) the iterations run.
 int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
-                   int nt, int max_iter, double rot_eps, double trans_eps, double* out_T, double* trace) {
+                   int nt, int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T,
+                   double* trace, int* executed) {
     namespace gm = pcore::gicpm;
     OXform x;
     for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) x.R[r][c] = r == c ? 1.0 : 0.0;
         x.t[r] = 0.0;
     }
-    int it = 0;
+    int it = 0, reported = 0;
     if (ns > 0 && nt > 0) {
         std::vector<gm::NNTarget> keys;
         float org[3];
         gicp_keys(tgt_xyz, nt, keys, org);
         std::vector<int32_t> corr(ns);
         std::vector<double> mah((size_t)6 * ns);
+        // T_f(j), j = 1.. (float(x_{j-1}), bit patterns): the cycle exit's record
+        std::vector<std::array<uint32_t, 12>> tf;
+        auto float_bits = [](const OXform& v) {
+            std::array<uint32_t, 12> b;
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++) {
+                    const float f = (float)v.R[r][c];
+                    std::memcpy(&b[3 * r + c], &f, 4);
+                }
+                const float f = (float)v.t[r];
+                std::memcpy(&b[9 + r], &f, 4);
+            }
+            return b;
+        };
+        tf.push_back(float_bits(x));
+        gm::CycleRun cyc{0, 0, 0};
         double lambda = -1.0;
         for (it = 0; it < max_iter;) {
             const int k = it;
@@ -805,18 +827,41 @@ int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const fl
             gicp_linearize_spec(x, src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, keys.empty() ? nullptr : keys.data(),
                                 org, corr.data(), mah.data(), sys);
             double lam_used;
-            int trials = 0;
+            int trials = 0, flags = 0;
             const int st = gicp_lm_iteration(sys, x, lambda, src_xyz, ns, tgt_xyz, corr.data(), mah.data(), rot_eps,
-                                             trans_eps, &lam_used, &trials);
+                                             trans_eps, &lam_used, &trials, &flags);
             if (trace) {
                 double* tr = trace + (size_t)16 * k;
                 for (int r = 0; r < 3; r++) {
                     for (int c = 0; c < 3; c++) tr[3 * r + c] = x.R[r][c];
                     tr[9 + r] = x.t[r];
                 }
-                tr[12] = lam_used; tr[13] = trials; tr[14] = 0.0; tr[15] = st;
+                tr[12] = lam_used; tr[13] = trials; tr[14] = flags; tr[15] = st;
             }
             if (st != gm::kLmAccepted) break;
+            if (it >= max_iter) break;
+            // the cycle exit after iteration it's accepted step: T_f(it + 1) against the last kCycleLags
+            const int cur = it + 1;
+            tf.push_back(float_bits(x));
+            int p = 0;
+            for (int q = 1; q <= gm::kCycleLags && cur - q >= 1; q++)
+                if (tf[cur - 1] == tf[cur - 1 - q]) { p = q; break; }
+            const bool inert = trials == 1 && flags == 3;
+            if (gm::cycle_update(cyc, p, inert, cycle_window)) {
+                const auto& m = tf[gm::cycle_member(cur, p, max_iter) - 1];
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++) {
+                        float f;
+                        std::memcpy(&f, &m[3 * r + c], 4);
+                        x.R[r][c] = f;
+                    }
+                    float f;
+                    std::memcpy(&f, &m[9 + r], 4);
+                    x.t[r] = f;
+                }
+                reported = max_iter;
+                break;
+            }
         }
     }
     for (int r = 0; r < 3; r++) {
@@ -824,12 +869,14 @@ int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const fl
         out_T[4 * r + 3] = x.t[r];
     }
     out_T[12] = 0.0; out_T[13] = 0.0; out_T[14] = 0.0; out_T[15] = 1.0;
-    return it;
+    if (executed) *executed = it;
+    return reported ? reported : it;
 }
 
 int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov, int nt,
-             int max_iter, double rot_eps, double trans_eps, double* out_T) {
-    return orc_gicp_trace(src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, max_iter, rot_eps, trans_eps, out_T, nullptr);
+             int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T) {
+    return orc_gicp_trace(src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, max_iter, rot_eps, trans_eps, cycle_window, out_T,
+                          nullptr, nullptr);
 }
 
 // The linearisation at T (double 4x4 row-major) two ways, on the spec's correspondences (out_corr, ns):
@@ -924,8 +971,8 @@ void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model
                       float depth_factor, const float* o_xyz, const double* o_cov, int num_o,
                       const int32_t* label_start, const int32_t* label_end, int num_labels,
                       const float* pose_obs_total, int cost_type, int calc_obs, float sensor_resolution, int k_corr,
-                      int max_iter, double rot_eps, double trans_eps, float* out_adj, int32_t* out_iters,
-                      float* out_rc, float* out_oc, float* out_diff, int nthreads) {
+                      int max_iter, double rot_eps, double trans_eps, int cycle_window, float* out_adj,
+                      int32_t* out_iters, float* out_rc, float* out_oc, float* out_diff, int nthreads) {
     (void)num_tris;
     std::vector<int> lo, hi;
     model_ranges(tris_model_count, num_models, lo, hi);
@@ -958,7 +1005,7 @@ void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model
             for (int i = 0; i < nr; i++) covariance_one(xyz.data(), nr, i, k, cov.data() + (size_t)6 * i);
             double T[16];
             const int iters = orc_gicp(xyz.data(), cov.data(), nr, o_xyz + (size_t)3 * l0, o_cov + (size_t)6 * l0,
-                                       l1 - l0, max_iter, rot_eps, trans_eps, T);
+                                       l1 - l0, max_iter, rot_eps, trans_eps, cycle_window, T);
             if (out_iters) out_iters[n] = iters;
             float* adj = out_adj + (size_t)16 * n;
             orc_concat_pose(T, pose, adj);

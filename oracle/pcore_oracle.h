@@ -116,14 +116,17 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
  * Covariances: double[6] (xx, xy, xz, yy, yz, zz) per point. */
 void orc_covariances(const float* xyz, int n, int k, double* out_cov6);
 
-/* Returns iterations run (linearisations); out_T: double 4x4 row-major (source -> target, metres). */
+/* Returns iterations (linearisations; max_iter after a cycle exit); out_T: double 4x4 row-major (source -> target,
+ * metres).  cycle_window: the cycle exit's W (pcore_gicp_math.h cycle_update; 0 runs the iterations out). */
 int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
-             int nt, int max_iter, double rot_eps, double trans_eps, double* out_T);
+             int nt, int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T);
 
 /* orc_gicp with a per-iteration trace (nullable; max_iter x 16 doubles: R (9) and t (3) after the iteration, the
- * lambda of its first trial, 0, 0, the LM status 0 accepted / 1 converged / 2 failed). */
+ * lambda of its first trial, its trials, flags (1 lambda inert, 2 rho >= 1/2), the LM status 0 accepted /
+ * 1 converged / 2 failed); *executed (nullable): the iterations run (rows of the trace). */
 int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
-                   int nt, int max_iter, double rot_eps, double trans_eps, double* out_T, double* trace);
+                   int nt, int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T,
+                   double* trace, int* executed);
 
 /* The linearisation at T (4x4 row-major double) on the spec's correspondences (out_corr: ns, -1 = none):
  * textbook = 0 the spec's arithmetic and reduction order, textbook = 1 an independent long-double restatement of
@@ -156,8 +159,8 @@ void orc_evaluate_icp(const float* tris, int num_tris, const int32_t* tris_model
                       const float* o_xyz, const double* o_cov, int num_o, const int32_t* label_start,
                       const int32_t* label_end, int num_labels, const float* pose_obs_total, int cost_type,
                       int calc_obs, float sensor_resolution, int k_corr, int max_iter, double rot_eps,
-                      double trans_eps, float* out_adj, int32_t* out_iters, float* out_rc, float* out_oc,
-                      float* out_diff, int nthreads);
+                      double trans_eps, int cycle_window, float* out_adj, int32_t* out_iters, float* out_rc,
+                      float* out_oc, float* out_diff, int nthreads);
 
 /* Colour cost (cost_type 1, f4): rgb2lab with the cost's channel order, the CIEDE2000 distance of the
  * shared colour spec, its float transcendentals, and the 3-DoF RGB-D evaluation (serial raster keeping

@@ -56,7 +56,8 @@ class EvalParams(ctypes.Structure):
 class GpuStats(ctypes.Structure):
     """pcore_gpu_stats (include/pcore.h; the reference's gpu_stats, model.h:24-27)."""
     _fields_ = [("icp_runtime", ctypes.c_float), ("peak_memory_usage", ctypes.c_double), ("gicp_ms", ctypes.c_float),
-                ("icp_chunks", ctypes.c_int32)]
+                ("icp_chunks", ctypes.c_int32), ("gicp_iterations", ctypes.c_int64),
+                ("gicp_iterations_run", ctypes.c_int64), ("gicp_cycle_exits", ctypes.c_int64)]
 
 
 MAX_TILE_TIERS = 8
@@ -72,7 +73,8 @@ class TileInfo(ctypes.Structure):
 
 class IcpParams(ctypes.Structure):
     _fields_ = [("k_correspondences", ctypes.c_int32), ("max_iterations", ctypes.c_int32),
-                ("rotation_epsilon", ctypes.c_double), ("transformation_epsilon", ctypes.c_double)]
+                ("rotation_epsilon", ctypes.c_double), ("transformation_epsilon", ctypes.c_double),
+                ("cycle_exit_window", ctypes.c_int32)]
 
 
 # renderer.cu:1696-1699
@@ -81,6 +83,8 @@ ICP_MAX_ITER = 150
 # renderer.cu:1698-1699 declares both as float and passes them to set_*_epsilon(double): the float values widened
 ICP_ROT_EPS = float(np.float32(2e-3))
 ICP_TRANS_EPS = float(np.float32(5e-4))
+# the GICP cycle exit's window (include/pcore.h PCORE_GICP_CYCLE_WINDOW; 0 = off)
+ICP_CYCLE_WINDOW = 8
 
 _lib = None
 

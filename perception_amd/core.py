@@ -221,7 +221,8 @@ class PoseCore:
                      k: int = _native.ICP_K, max_iterations: int = _native.ICP_MAX_ITER,
                      rotation_epsilon: float = _native.ICP_ROT_EPS,
                      transformation_epsilon: float = _native.ICP_TRANS_EPS, out=None,
-                     color_distance_threshold: float = 15.0, stream=None):
+                     color_distance_threshold: float = 15.0, stream=None,
+                     cycle_exit_window: int = _native.ICP_CYCLE_WINDOW):
         """Stage COST with do_icp = true.  Returns (adjusted poses (N,16), iterations (N,), rc, oc, diff)."""
         n = int(poses.shape[0])
         dev = poses.device
@@ -231,7 +232,8 @@ class PoseCore:
         adj, iters, rc, oc, df = out
         p = EvalParams(int(cost_type), int(bool(calc_obs_cost)), int(stride), float(depth_factor),
                        float(sensor_resolution), float(occlusion_threshold), float(color_distance_threshold))
-        ip = IcpParams(int(k), int(max_iterations), float(rotation_epsilon), float(transformation_epsilon))
+        ip = IcpParams(int(k), int(max_iterations), float(rotation_epsilon), float(transformation_epsilon),
+                       int(cycle_exit_window))
         self._check(self.lib.pcore_evaluate_icp(
             self._h, _ptr(poses, torch.float32, "poses"), _ptr(pose_model, torch.int32, "pose_model"),
             _ptr(pose_label, torch.int32, "pose_label"), _ptr(pose_obs_total, torch.float32, "pose_obs_total"),
@@ -262,7 +264,8 @@ class PoseCore:
         st = _native.GpuStats()
         self._check(self.lib.pcore_get_stats(self._h, ctypes.byref(st), int(bool(reset))))
         return {"icp_runtime": st.icp_runtime, "peak_memory_usage": st.peak_memory_usage, "gicp_ms": st.gicp_ms,
-                "icp_chunks": st.icp_chunks}
+                "icp_chunks": st.icp_chunks, "gicp_iterations": st.gicp_iterations,
+                "gicp_iterations_run": st.gicp_iterations_run, "gicp_cycle_exits": st.gicp_cycle_exits}
 
     def tile_info(self) -> dict:
         """pcore_get_tile_info: the fused window launch's tile tier and the last published window histogram."""

@@ -83,6 +83,7 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_corr_hist;  // GicpArgs::corr_hist
     DevBuf<double> icp_mahal;   // GicpArgs::mahal
     DevBuf<int32_t> icp_counter;
+    DevBuf<unsigned long long> icp_iter_stats;  // GicpArgs::iter_stats, zeroed per pcore_evaluate_icp
     DevBuf<uint32_t> icp_order_keys;  // 2 x chunk keys (in, out)
     DevBuf<int32_t> icp_order_idx;    // 2 x chunk indices (in, out = GicpArgs::pose_order)
     DevBuf<unsigned char> icp_order_temp;
@@ -317,7 +318,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->scratch_dc_pre); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->scratch_dc_pre); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_iter_stats); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part); (void)dev_free(c->tri_rgb); (void)dev_free(c->render_tri);
     for (hipEvent_t e : c->icp_ev) (void)hipEventDestroy(e);
@@ -922,6 +923,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     if (!c || !p || !ip) return PCORE_E_INVALID_ARG;
     if (ip->k_correspondences <= 0 || ip->k_correspondences > 16 || ip->max_iterations < 0)
         return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: k_correspondences must be in [1, 16]");
+    if (ip->cycle_exit_window < 0)
+        return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: cycle_exit_window must be >= 0");
     if (num_poses > 0 && !d_out_poses) return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: null d_out_poses");
     if (p->cost_type != PCORE_COST_DEPTH_3DOF && p->cost_type != PCORE_COST_DEPTH_6DOF)
         return fail(c, PCORE_E_INVALID_ARG, "evaluate_icp: cost_type must be 0 or 2");
@@ -983,6 +986,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     if (use_hist) HIPC(c, dev_reserve(c->icp_corr_hist, (size_t)chunk * kCorrHist * hist_cap));
     HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 1));
+    HIPC(c, dev_reserve(c->icp_iter_stats, 3));
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
     const size_t order_temp = gicp_order_temp_bytes(chunk);
@@ -999,6 +1003,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, hipStreamIsCapturing(s, &cap_status));
     const bool timed = cap_status == hipStreamCaptureStatusNone;
     c->icp_ev_used = 0;
+    HIPC(c, hipMemsetAsync(c->icp_iter_stats.p, 0, 3 * sizeof(unsigned long long), s));
     while (timed && c->icp_ev.size() < (size_t)3 * nchunks) {
         hipEvent_t e;
         HIPC(c, hipEventCreate(&e));
@@ -1027,6 +1032,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.rot_eps = ip->rotation_epsilon;
     g.trans_eps = ip->transformation_epsilon;
     g.work_counter = c->icp_counter.p;
+    g.cycle_window = ip->cycle_exit_window;
+    g.iter_stats = c->icp_iter_stats.p;
     g.tgt_quads = c->tgt_quads.p;
     g.seg_qoff = c->seg_qoff.p;
     g.grids = c->grids.p;
@@ -1126,6 +1133,12 @@ int pcore_get_stats(pcore_ctx* c, pcore_gpu_stats* out, int32_t reset) {
     out->peak_memory_usage = c->peak_mem_mb;
     out->gicp_ms = (float)gicp_ms;
     out->icp_chunks = c->icp_ev_used;
+    unsigned long long it[3] = {0ull, 0ull, 0ull};
+    if (c->icp_ev_used > 0 && c->icp_iter_stats.p)  // the last chunk's end event has completed
+        HIPC(c, hipMemcpy(it, c->icp_iter_stats.p, sizeof(it), hipMemcpyDeviceToHost));
+    out->gicp_iterations = (int64_t)it[0];
+    out->gicp_iterations_run = (int64_t)it[1];
+    out->gicp_cycle_exits = (int64_t)it[2];
     if (reset) c->peak_mem_mb = 0.0;
     return PCORE_OK;
 }

@@ -852,9 +852,10 @@ template <typename CorrPtr>
 __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double& lambda, const float4* src,
                                             CorrPtr corr, const double* mah, const float4* tgt, int ns, int lane,
                                             const Round0& r0, const lds_cvd* se3c, double rot_eps,
-                                            double trans_eps GPROF_PARAM) {
+                                            double trans_eps, bool& inert GPROF_PARAM) {
     const double y0 = uniform_d(sys[gicpm::kErr]);
     if (lambda < 0.0) lambda = uniform_d(gicpm::lm_init_lambda(sys));
+    inert = false;
     double nu = 2.0;
     for (int trial = 0; trial < gicpm::kLmMaxTrials; trial++) {
         GPROF_T(p0);
@@ -921,6 +922,8 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
             continue;
         }
         x = xi;
+        // the cycle exit's condition: accepted at the first trial, lambda not growing and inert on this system
+        inert = trial == 0 && rho >= 0.5 && gicpm::lm_lambda_inert(sys, lambda);
         lambda = uniform_d(gicpm::lm_accept_lambda(lambda, rho));
         return gicpm::is_converged(Rd, td, rot_eps, trans_eps) ? gicpm::kLmConverged : gicpm::kLmAccepted;
     }
@@ -952,6 +955,97 @@ __device__ __forceinline__ void xform_float(const Xform& x, float (&Rf)[3][3], f
         for (int c = 0; c < 3; c++) Rf[r][c] = uniform_f((float)x.R[r][c]);
         tf[r] = uniform_f((float)x.t[r]);
     }
+}
+
+// A 16-slot ring of float transforms in LDS (the correspondence history and the cycle exit): lane l holds components
+// 3 (l & 3) + v (v = 0, 1, 2) of slot l >> 2 in word v (R rows 0..2, then t), as bit patterns (-0 != +0, NaN == NaN).
+__device__ __forceinline__ void xf_lane_words(const float (&Rf)[3][3], const float (&tf)[3], int sub, unsigned& b0,
+                                              unsigned& b1, unsigned& b2) {
+    const float c0 = sub == 0 ? Rf[0][0] : sub == 1 ? Rf[1][0] : sub == 2 ? Rf[2][0] : tf[0];
+    const float c1 = sub == 0 ? Rf[0][1] : sub == 1 ? Rf[1][1] : sub == 2 ? Rf[2][1] : tf[1];
+    const float c2 = sub == 0 ? Rf[0][2] : sub == 1 ? Rf[1][2] : sub == 2 ? Rf[2][2] : tf[2];
+    b0 = __builtin_bit_cast(unsigned, c0);
+    b1 = __builtin_bit_cast(unsigned, c1);
+    b2 = __builtin_bit_cast(unsigned, c2);
+}
+
+// bit s set: all four lanes of slot s hold (b0, b1, b2) (the lanes' current words hv0..hv2)
+__device__ __forceinline__ unsigned ring_match16(unsigned b0, unsigned b1, unsigned b2, unsigned hv0, unsigned hv1,
+                                                 unsigned hv2) {
+    unsigned long long eq = __ballot(b0 == hv0 && b1 == hv1 && b2 == hv2);
+    eq = eq & (eq >> 1) & (eq >> 2) & (eq >> 3) & 0x1111111111111111ull;  // bit 4s: slot s
+    eq = (eq | (eq >> 3)) & 0x0303030303030303ull;                         // gather bit 4s to bit s
+    eq = (eq | (eq >> 6)) & 0x000f000f000f000full;
+    eq = (eq | (eq >> 12)) & 0x000000ff000000ffull;
+    eq = (eq | (eq >> 24)) & 0xffffull;
+    return (unsigned)eq;
+}
+
+// The cycle exit (pcore_gicp_math.h cycle_update) of one wave: the last 16 float transforms T_f(j) in slot
+// (j - 1) % 16 of an LDS ring, the slots written so far and the run counters.
+struct CycleExit {
+    unsigned* ring;  // 3 x 64 words, this wave's
+    unsigned written;
+    gicpm::CycleRun run;
+
+    __device__ __forceinline__ void start(int lane) {  // T_f(1) = float(identity) in slot 0
+        // lane l < 4 writes row l of I (t = 0 for l = 3): word v is 1.0f where v == l; formed here from an opaque lane
+        // index, or the compiler hoists the words and addresses out of the persistent pose loop and holds 4 VGPRs
+        const int l = lane + opaque_zero();
+        if (l < 4) {  // every lane reads back only the words it wrote itself
+            ring[l] = l == 0 ? 0x3f800000u : 0u;
+            ring[64 + l] = l == 1 ? 0x3f800000u : 0u;
+            ring[128 + l] = l == 2 ? 0x3f800000u : 0u;
+        }
+        written = 1u;
+        run = {0, 0, 0};
+    }
+
+    // after iteration `iters`' accepted step (iters < max_iter): T_f(iters + 1) = float(x).  Returns -1, or the ring slot
+    // of the cycle member the pose stops with (read by `member` once the loop has ended).
+    __device__ __forceinline__ int step(const Xform& x, int iters, int max_iter, int window, bool inert, int lane_) {
+        const int lane = lane_ + opaque_zero();  // per-lane values formed here, not hoisted out of the iteration loop
+        float Rf[3][3], tf[3];
+        xform_float(x, Rf, tf);
+        unsigned b0, b1, b2;
+        xf_lane_words(Rf, tf, lane & 3, b0, b1, b2);
+        const int cur = iters + 1, c0 = (cur - 1) & 15;
+        const unsigned hv0 = ring[lane], hv1 = ring[64 + lane], hv2 = ring[128 + lane];
+        const unsigned m = ring_match16(b0, b1, b2, hv0, hv1, hv2) & written;
+        // lag q lives in slot (c0 - q) % 16: in the doubled mask at c0 + 16 - q, so the smallest lag is the highest bit
+        const unsigned t = ((m | (m << 16)) >> c0) & 0xffffu;
+        const int p = t ? 16 - (31 - __builtin_clz(t)) : 0;
+        if ((lane >> 2) == c0) {
+            ring[lane] = b0;
+            ring[64 + lane] = b1;
+            ring[128 + lane] = b2;
+        }
+        written |= 1u << c0;
+        if (!gicpm::cycle_update(run, p, inert, window)) return -1;
+        return (gicpm::cycle_member(cur, p, max_iter) - 1) & 15;
+    }
+
+    // the float transform of ring slot s as the pose's result (after the loop: x is written back, not iterated on; the
+    // ring was written by the whole wave, read here by every lane)
+    __device__ __forceinline__ void member(int s, Xform& x) {
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int v = 0; v < 3; v++) {
+                const double f = (double)__builtin_bit_cast(float, ring[64 * v + 4 * s + r]);
+                if (r < 3) x.R[r][v] = f;
+                else x.t[v] = f;
+            }
+    }
+};
+
+// the launch's iteration counters (GicpArgs::iter_stats): no-return atomics, one lane per pose
+__device__ __forceinline__ void count_iterations(const GicpArgs& g, int reported, int run, bool exited) {
+    if (!g.iter_stats) return;
+    __hip_atomic_fetch_add(g.iter_stats + 0, (unsigned long long)reported, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(g.iter_stats + 1, (unsigned long long)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (exited) __hip_atomic_fetch_add(g.iter_stats + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // the pose a GICP workgroup works on next and its target segment
@@ -1012,6 +1106,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ int sPose;
     __shared__ double sSe3[4 * gicpm::kSe3Terms];  // se3_exp's series coefficients, read at their use
     __shared__ unsigned sHist[3 * 64];               // the correspondence history's float transforms (below)
+    __shared__ unsigned sCyc[3 * 64];                // the cycle exit's last 16 float transforms (CycleExit)
     const int lane = threadIdx.x;
     const Round0 r0{sM0, sS0, sT0};
     if (lane < 4 * gicpm::kSe3Terms) sSe3[lane] = gicpm::kSe3Coef[lane];
@@ -1036,7 +1131,10 @@ gicp_kernel(GicpArgs g, int num_poses) {
         Xform x;
         xform_identity(x);
         double lambda = -1.0;
-        int iters = 0;
+        int iters = 0, iters_run = 0, exit_slot = -1;
+        CycleExit cyc;
+        cyc.ring = sCyc;
+        cyc.start(lane);
         // correspondence history: sHist[64 v + l] holds component 3 (l & 3) + v (v = 0, 1, 2) of set l >> 2's float
         // transform (R rows 0..2, then t); `kept` has bit 4e set for every filled set e (the words of unfilled sets
         // are never compared).  In LDS rather than in three VGPRs per lane: the kernel is at its register budget,
@@ -1054,11 +1152,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 int32_t* cset = P.corr;
                 bool reuse = false;
                 if (hist) {
-                    const float c0 = sub == 0 ? Rf[0][0] : sub == 1 ? Rf[1][0] : sub == 2 ? Rf[2][0] : tf[0];
-                    const float c1 = sub == 0 ? Rf[0][1] : sub == 1 ? Rf[1][1] : sub == 2 ? Rf[2][1] : tf[1];
-                    const float c2 = sub == 0 ? Rf[0][2] : sub == 1 ? Rf[1][2] : sub == 2 ? Rf[2][2] : tf[2];
-                    const unsigned b0 = __builtin_bit_cast(unsigned, c0), b1 = __builtin_bit_cast(unsigned, c1),
-                                   b2 = __builtin_bit_cast(unsigned, c2);
+                    unsigned b0, b1, b2;
+                    xf_lane_words(Rf, tf, sub, b0, b1, b2);
                     // bitwise equality (-0 != +0, NaN == NaN): the float queries, and so the correspondences, are
                     // functions of these bits
                     const unsigned hv0 = sHist[lane], hv1 = sHist[64 + lane], hv2 = sHist[128 + lane];
@@ -1135,15 +1230,28 @@ gicp_kernel(GicpArgs g, int num_poses) {
                 GPROF_T(t_b);
                 const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_c, sys[0]);
+                bool inert;
                 const int st = lm_iteration(sys, x, lambda, P.src, cset, P.mah, P.tgt, P.ns, lane, r0, (const lds_cvd*)sSe3,
-                                            g.rot_eps, g.trans_eps GPROF_ARG);
+                                            g.rot_eps, g.trans_eps, inert GPROF_ARG);
                 GPROF_TD(t_d, st);
                 GPROF_ADD(2, t_b, t_c);
                 GPROF_ADD(3, t_c, t_d);
                 if (st != gicpm::kLmAccepted) break;
+                if (g.cycle_window > 0 && iters < g.max_iter) {
+                    exit_slot = cyc.step(x, iters, g.max_iter, g.cycle_window, inert, lane);
+                    if (exit_slot >= 0) {
+                        iters_run = iters;
+                        iters = g.max_iter;
+                        break;
+                    }
+                }
             }
         }
-        if (lane == 0) write_pose(g, P.gp, x, iters);
+        if (exit_slot >= 0) cyc.member(exit_slot, x);
+        if (lane == 0) {
+            write_pose(g, P.gp, x, iters);
+            count_iterations(g, iters, iters_run ? iters_run : iters, iters_run != 0);
+        }
 #ifdef PCORE_GICP_TIMELINE
         if (lane == 0 && P.gp < kTlPoses) {
             g_tl_pose[2 * P.gp] = tl_p0;
@@ -1169,6 +1277,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
 // indices go to LDS, and wave 0 then adds the contributions and runs the LM iteration exactly as gicp_kernel
 // does -- point i on lane i % 64, in point order -- so the refined poses are bit-identical; only the
 // nearest-target searches, the expensive part against a whole-scene target, run in parallel.
+constexpr int kCycleExited = 3;  // gicp_wide_kernel's flag: wave 0's cycle exit stopped the pose (LmStatus + 1)
+
 template <int WPP>
 __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num_poses) {
     constexpr int NT = 64 * WPP;
@@ -1179,6 +1289,7 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
     __shared__ double sX[12];
     __shared__ int sPose, sFlag;
     __shared__ double sSe3[4 * gicpm::kSe3Terms];
+    __shared__ unsigned sCyc[3 * 64];  // wave 0's cycle exit ring
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const Round0 r0{sM0, sS0, sT0};  // wave 0's
     if (tid < 4 * gicpm::kSe3Terms) sSe3[tid] = gicpm::kSe3Coef[tid];
@@ -1198,7 +1309,10 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
         Xform x;
         xform_identity(x);
         double lambda = -1.0;  // wave 0's
-        int iters = 0;
+        int iters = 0, iters_run = 0;
+        CycleExit cyc;  // wave 0's
+        cyc.ring = sCyc;
+        if (wave == 0) cyc.start(lane);
         const bool run = P.ns > 0 && P.nt > 0;
         for (int it = 0; run && it < g.max_iter; it++) {
             iters++;
@@ -1236,11 +1350,19 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 GPROF_TD(t_w2, acc[0]);
                 const double* sys = wave_tree_sums(acc, sRed, lane);
                 GPROF_TD(t_w3, sys[0]);
-                const int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, (const lds_cvd*)sSe3,
-                                            g.rot_eps, g.trans_eps GPROF_ARG);
+                bool inert;
+                int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, (const lds_cvd*)sSe3,
+                                      g.rot_eps, g.trans_eps, inert GPROF_ARG);
                 GPROF_TD(t_w4, st);
                 GPROF_ADD(2, t_w2, t_w3);  // [1]: linearize_round's own marks
                 GPROF_ADD(3, t_w3, t_w4);
+                if (st == gicpm::kLmAccepted && g.cycle_window > 0 && iters < g.max_iter) {
+                    const int s2 = cyc.step(x, iters, g.max_iter, g.cycle_window, inert, lane);
+                    if (s2 >= 0) {
+                        cyc.member(s2, x);
+                        st = kCycleExited;
+                    }
+                }
                 if (lane == 0) {
                     sFlag = st;
 #pragma unroll
@@ -1259,10 +1381,17 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
                 for (int c = 0; c < 3; c++) x.R[r][c] = uniform_d(sX[3 * r + c]);
                 x.t[r] = uniform_d(sX[9 + r]);
             }
+            if (flag == kCycleExited) {
+                iters_run = iters;
+                iters = g.max_iter;
+            }
             if (flag != gicpm::kLmAccepted) break;
         }
         __syncthreads();
-        if (tid == 0) write_pose(g, P.gp, x, iters);
+        if (tid == 0) {
+            write_pose(g, P.gp, x, iters);
+            count_iterations(g, iters, iters_run ? iters_run : iters, iters_run != 0);
+        }
     }
     if (wave == 0) GPROF_FLUSH;
 }

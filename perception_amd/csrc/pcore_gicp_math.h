@@ -483,6 +483,44 @@ PCORE_GHD double lm_gain(double rho) {
 }
 PCORE_GHD double lm_accept_lambda(double lambda, double rho) { return lambda * lm_gain(rho); }
 
+// The damping is inert on this system: adding lambda changes no diagonal entry of H, so the damped solve is the
+// undamped one bit for bit (the GICP cycle exit's condition).
+PCORE_GHD bool lm_lambda_inert(const double* sys, double lambda) {
+    bool ok = true;
+PCORE_UNROLL
+    for (int a = 0; a < 6; a++) ok = ok && (sys[hdiag(a)] + lambda == sys[hdiag(a)]);
+    return ok;
+}
+
+// ---- the cycle exit -------------------------------------------------------------------
+// A capped pose is an LM 2-cycle (or a longer one): its float transforms T_f(j) = float(x_{j-1}), and so its
+// correspondences, recur with a period p while the doubles drift in their last bits.  After every accepted step of
+// iteration k < max_iter that is not converged, p_k = the smallest lag q <= kCycleLags with T_f(k+1) == T_f(k+1-q)
+// bit for bit (0: none), and the step is "inert" when it was accepted at its first trial with rho >= 1/2 (lambda
+// does not grow) and lambda changed no diagonal entry of H (lm_lambda_inert).  When the last W lags are the same
+// p > 0 and the last W steps are inert, the pose stops: it reports max_iter iterations and the transform T_f(j') of
+// the cycle member j' = max_iter + 1 (mod p) among its last p iterations -- the float transform the remaining
+// iterations would end on while the cycle holds.  W = 0 runs the iterations out (fast_gicp).
+constexpr int kCycleLags = 16;
+constexpr int kCycleWindow = 8;  // the spec's W (tools/cycle_exit_sim.py: 2,000 C3 candidates, 706 exits)
+
+struct CycleRun {
+    int lag, run, okrun;
+};
+
+PCORE_GHD bool cycle_update(CycleRun& c, int p, bool inert, int window) {
+    c.run = p > 0 ? (p == c.lag ? c.run + 1 : 1) : 0;
+    c.lag = p;
+    c.okrun = inert ? c.okrun + 1 : 0;
+    return window > 0 && p > 0 && c.run >= window && c.okrun >= window;
+}
+
+// j' in (cur - p, cur] with j' = max_iter + 1 (mod p), cur = k + 1 <= max_iter
+PCORE_GHD int cycle_member(int cur, int p, int max_iter) {
+    const int d = (max_iter + 1 - cur) % p;
+    return d == 0 ? cur : cur - (p - d);
+}
+
 PCORE_GHD bool all_finite6(const double (&d)[6]) {
     bool ok = true;
 PCORE_UNROLL

@@ -176,6 +176,10 @@ struct GicpArgs {
     // of searching.  Poses with more than corr_hist_cap source points search every iteration (into corr).
     int32_t* corr_hist;       // nullable: no history
     int32_t corr_hist_cap;
+    // the cycle exit's window W (pcore_gicp_math.h cycle_update; 0 = off) and the launch's iteration counters
+    // (nullable; [0] iterations reported, [1] iterations run, [2] cycle exits: one no-return atomic each per pose)
+    int32_t cycle_window;
+    unsigned long long* iter_stats;
 };
 
 constexpr int kCorrHist = 16;      // history sets per pose: lanes 4e .. 4e + 3 of three VGPRs hold set e's 12 floats

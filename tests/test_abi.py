@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(lib, name), name
         assert isinstance(getattr(lib, name), ctypes._CFuncPtr)
-    assert lib.pcore_abi_version() == 6
+    assert lib.pcore_abi_version() == 7
 
 
 def test_library_is_gfx950_code():

@@ -147,7 +147,7 @@ def test_gicp_matches_independent_numpy_lm(c3_pairs):
     iteration, a limit cycle the published step_lm accepts)."""
     iters = []
     for src, scov, tgt, tcov in c3_pairs:
-        T1, it1 = oracle.gicp(src, scov, tgt, tcov)
+        T1, it1 = oracle.gicp(src, scov, tgt, tcov, cycle_window=0)
         T2, it2 = gref.gicp(src, scov, tgt, tcov)
         assert it1 == it2
         assert np.abs(T1 - T2).max() < 1e-9
@@ -269,13 +269,55 @@ def test_gicp_independent_chain_120_c3_poses(c3_pairs_120):
     iters = []
     for src, scov_o, scov_g, tgt, tcov_o, tcov_g in c3_pairs_120:
         assert np.abs(scov_o - scov_g).max() < 1e-12
-        T1, it1 = oracle.gicp(src, scov_o, tgt, tcov_o)
+        T1, it1 = oracle.gicp(src, scov_o, tgt, tcov_o, cycle_window=0)
         T2, it2 = gref.gicp(src, scov_g, tgt, tcov_g)
         assert it1 == it2
         assert np.abs(T1 - T2).max() < 1e-9
         iters.append(it1)
     iters = np.array(iters)
     assert len(iters) >= 100 and (iters >= 150).sum() >= 20 and (iters < 150).sum() >= 20
+
+
+def _float_T(T):
+    return np.concatenate([T[:3, :3].reshape(-1), T[:3, 3]]).astype(np.float32)
+
+
+def test_cycle_exit_against_full_length_chains(c3_pairs_120):
+    """The spec's cycle exit (pcore_gicp_math.h cycle_update, W = 8) against running every
+    iteration out, on the 120 C3 candidates: the same reported iteration counts; the float transform (what
+    concatenate_transforms composes) bit-identical on >= 99 % of the candidates and within 1e-6 on the rest; and the
+    exit's result against the independent numpy chain run to 150 iterations (tests/gicp_reference.py): equal
+    iterations, within 1e-6.  The exits happen (the capped candidates are LM cycles) and save iterations."""
+    same = exits = run_on = run_off = 0
+    worst = 0.0
+    for src, scov_o, scov_g, tgt, tcov_o, tcov_g in c3_pairs_120:
+        T0, it0, tr0 = oracle.gicp_trace(src, scov_o, tgt, tcov_o, cycle_window=0)
+        T1, it1, tr1 = oracle.gicp_trace(src, scov_o, tgt, tcov_o, cycle_window=oracle.GICP_CYCLE_WINDOW)
+        T2, it2 = oracle.gicp(src, scov_o, tgt, tcov_o)  # the default is the spec's window
+        assert np.array_equal(T1, T2) and it1 == it2
+        assert it0 == it1
+        exits += len(tr1) < len(tr0)
+        run_on += len(tr1)
+        run_off += len(tr0)
+        f0, f1 = _float_T(T0), _float_T(T1)
+        same += np.array_equal(f0.view(np.uint32), f1.view(np.uint32))
+        worst = max(worst, float(np.abs(f0 - f1).max()))
+        Tg, itg = gref.gicp(src, scov_g, tgt, tcov_g)
+        assert itg == it1 and np.abs(_float_T(Tg) - f1).max() <= 1e-6
+    n = len(c3_pairs_120)
+    assert same >= 0.99 * n and worst <= 1e-6
+    assert exits >= 20 and run_on < 0.75 * run_off
+
+
+def test_cycle_window_constants_agree():
+    """The spec's window is one number in the oracle, the Python host and include/pcore.h."""
+    import re
+    from pathlib import Path
+
+    from perception_amd import _native
+    h = (Path(__file__).resolve().parents[1] / "include" / "pcore.h").read_text()
+    assert int(re.search(r"#define PCORE_GICP_CYCLE_WINDOW (\d+)", h).group(1)) == 8
+    assert oracle.GICP_CYCLE_WINDOW == _native.ICP_CYCLE_WINDOW == 8
 
 
 def test_gicp_whole_scene_targets_independent_chain():
@@ -298,7 +340,7 @@ def test_gicp_whole_scene_targets_independent_chain():
     iters = []
     for i in range(len(idx)):
         src = oracle.depth_to_cloud(depth[i], 4, sc.cx, sc.cy, sc.fx, sc.fy, 100.0)[0]
-        T1, it1 = oracle.gicp(src, oracle.covariances(src), obs, tcov_o)
+        T1, it1 = oracle.gicp(src, oracle.covariances(src), obs, tcov_o, cycle_window=0)
         T2, it2 = gref.gicp(src, gref.covariances(src), obs, tcov_g)
         assert it1 == it2, (idx[i], it1, it2)
         assert np.abs(T1 - T2).max() < 1e-9

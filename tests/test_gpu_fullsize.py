@@ -207,14 +207,24 @@ def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, monkeypatch):
     assert np.array_equal(dbg.cpu().numpy(), full[:, ::s, ::s])
 
 
-def test_c3_scene_icp_sweep_bit_exact_vs_oracle():
+@pytest.mark.parametrize("window", [8, 0])
+def test_c3_scene_icp_sweep_bit_exact_vs_oracle(window):
     """GICP at scale: 3,000 candidate poses of C3's five-model scene (depth sweep + jitter around each object)
     refined and re-scored on the GPU equal the oracle's adjusted poses, iteration counts and costs bit for
-    bit (the north star's 1e-4 on the transform is met with margin 0)."""
+    bit (the north star's 1e-4 on the transform is met with margin 0), with the spec's cycle exit (window 8) and
+    with every iteration run out (window 0).  The launch's iteration counters (pcore_get_stats) add up: reported
+    iterations = the iteration counts' sum, fewer run by the exits."""
     names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
     w = workloads.build(names=names, poses_per_model=600)
     adj, iters, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
-                                                 stride=w.stride)
+                                                 stride=w.stride, cycle_exit_window=window)
+    st = w.core.stats()
+    its = iters.cpu().numpy()
+    assert st["gicp_iterations"] == int(its.sum())
+    if window:
+        assert st["gicp_cycle_exits"] > 100 and st["gicp_iterations_run"] < 0.8 * st["gicp_iterations"]
+    else:
+        assert st["gicp_cycle_exits"] == 0 and st["gicp_iterations_run"] == st["gicp_iterations"]
     sc = w.scene
     xyz = w.obs_xyz.cpu().numpy()
     lab = w.obs_label.cpu().numpy()
@@ -231,7 +241,7 @@ def test_c3_scene_icp_sweep_bit_exact_vs_oracle():
     oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
         sc.bank.tris, sc.bank.tris_model_count, w.poses.cpu().numpy(), pm, pm, sc.width, sc.height, sc.proj,
         sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, cov, ls, le,
-        w.pose_obs_total.cpu().numpy(), 2, True, 0.01)
+        w.pose_obs_total.cpu().numpy(), 2, True, 0.01, cycle_window=window)
     assert np.array_equal(iters.cpu().numpy(), oit)
     assert np.array_equal(_bits(adj.cpu().numpy()), _bits(oadj))
     assert np.array_equal(_bits(rc.cpu().numpy()), _bits(orc))

@@ -49,11 +49,13 @@ def sweep_costs(batches, n, cam):
     return totals
 
 
-def sweep_icp(n):
+def sweep_icp(n, windows=(8, 0)):
+    """GPU vs oracle for each cycle-exit window (bit for bit), then the exit against running every iteration out
+    (DESIGN.md section 5): refined float poses bit-identical or within 1e-6, iteration counts, post-ICP costs and the
+    per-model argmin (oracle.select) identical."""
     names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can", "024_bowl"]
     w = workloads.build(names=names, poses_per_model=max(1, n // len(names)), seed=syn.SEED + 17)
     sc = w.scene
-    adj, it, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
     p16 = w.poses.cpu().numpy()
     pm = w.pose_model.cpu().numpy()
     pl = w.pose_label.cpu().numpy()
@@ -68,15 +70,44 @@ def sweep_icp(n):
     for L in range(nl):
         if le[L] > ls[L]:
             cov[ls[L]:le[L]] = oracle.covariances(oxyz[ls[L]:le[L]])
-    print(f"icp: GPU done, oracle on {len(p16)} candidates", file=sys.stderr, flush=True)
-    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(sc.bank.tris, sc.bank.tris_model_count, p16, pm, pl, sc.width,
-                                                   sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx,
-                                                   sc.cy, sc.fx, sc.fy, 100.0, oxyz, cov, ls, le, tot, 2, True, 0.01)
-    adj, it = adj.cpu().numpy(), it.cpu().numpy()
-    bad = ((_bits(adj) != _bits(oadj)).any(1) | (it != oit) | (_bits(rc.cpu().numpy()) != _bits(orc))
-           | (_bits(oc.cpu().numpy()) != _bits(ooc)) | (_bits(df.cpu().numpy()) != _bits(odf)))
-    return {"candidates": int(len(p16)), "mismatching": int(bad.sum()), "at_150": int((oit >= 150).sum()),
-            "iterations_mean": float(oit.mean())}
+    res = {}
+    outs = {}
+    for win in windows:
+        adj, it, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                  stride=w.stride, cycle_exit_window=win)
+        st = w.core.stats()
+        print(f"icp window {win}: GPU done, oracle on {len(p16)} candidates", file=sys.stderr, flush=True)
+        oadj, oit, orc, ooc, odf = oracle.evaluate_icp(sc.bank.tris, sc.bank.tris_model_count, p16, pm, pl, sc.width,
+                                                       sc.height, sc.proj, sc.src_depth_cm, sc.mask, 1.0, w.stride,
+                                                       sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, cov, ls, le, tot, 2,
+                                                       True, 0.01, cycle_window=win)
+        adj, it = adj.cpu().numpy(), it.cpu().numpy()
+        rc, oc, df = rc.cpu().numpy(), oc.cpu().numpy(), df.cpu().numpy()
+        bad = ((_bits(adj) != _bits(oadj)).any(1) | (it != oit) | (_bits(rc) != _bits(orc))
+               | (_bits(oc) != _bits(ooc)) | (_bits(df) != _bits(odf)))
+        res[f"window_{win}"] = {"candidates": int(len(p16)), "mismatching_gpu_vs_oracle": int(bad.sum()),
+                                "at_150": int((oit >= 150).sum()), "iterations_mean": float(oit.mean()),
+                                "gicp_iterations": int(st["gicp_iterations"]),
+                                "gicp_iterations_run": int(st["gicp_iterations_run"]),
+                                "gicp_cycle_exits": int(st["gicp_cycle_exits"]), "gicp_ms": float(st["gicp_ms"])}
+        outs[win] = (adj, it, rc, oc, df)
+    if len(windows) == 2:
+        (a1, i1, r1, o1, d1), (a0, i0, r0, o0, d0) = outs[windows[0]], outs[windows[1]]
+        ident = ~(_bits(a1) != _bits(a0)).any(1)
+        diff = np.abs(a1.astype(np.float64) - a0.astype(np.float64)).max(1)
+        scale = np.abs(a0.astype(np.float64)).max(1)
+        k1 = oracle.select(r1, o1, pm, len(names))
+        k0 = oracle.select(r0, o0, pm, len(names))
+        res["exit_vs_full"] = {
+            "poses_bit_identical": int(ident.sum()), "poses_bit_identical_frac": float(ident.mean()),
+            "max_rel_diff_others": float((diff / np.maximum(scale, 1e-30))[~ident].max()) if (~ident).any() else 0.0,
+            "max_abs_diff_others_cm_scaled": float(diff[~ident].max()) if (~ident).any() else 0.0,
+            "iterations_equal": bool(np.array_equal(i1, i0)),
+            "costs_identical": int(((_bits(r1) == _bits(r0)) & (_bits(o1) == _bits(o0))
+                                    & (_bits(d1) == _bits(d0))).sum()),
+            "argmin_identical": bool(np.array_equal(k1[0], k0[0]) and np.array_equal(k1[1], k0[1])),
+            "argmin": [[int(c), int(i)] for c, i in zip(*k1)]}
+    return res
 
 
 def main():
@@ -87,8 +118,10 @@ def main():
     ap.add_argument("--out")
     a = ap.parse_args()
     t0 = time.time()
-    res = {"costs_640": sweep_costs(a.batches, a.poses, "640"),
-           "costs_1280": sweep_costs(max(1, a.batches // 5), a.poses, "1280")}
+    res = {}
+    if a.batches > 0:
+        res["costs_640"] = sweep_costs(a.batches, a.poses, "640")
+        res["costs_1280"] = sweep_costs(max(1, a.batches // 5), a.poses, "1280")
     if a.icp:
         res["icp_c3"] = sweep_icp(a.icp)
     res["seconds"] = time.time() - t0

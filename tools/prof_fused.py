@@ -34,8 +34,11 @@ def main():
         torch.cuda.synchronize()  # steady state: the next call sees this call's window histogram
     if a.iters_json and its is not None:
         import json
+        st = w.core.stats()  # pose_iterations: the executed ones (the cycle exits' remaining iterations are not run)
         with open(a.iters_json, "w") as f:
-            json.dump({"poses": n, "pose_iterations": int(its.sum().item()), "gicp_launches_per_call": 1}, f)
+            json.dump({"poses": n, "pose_iterations": int(st["gicp_iterations_run"]),
+                       "pose_iterations_reported": int(its.sum().item()), "cycle_exits": int(st["gicp_cycle_exits"]),
+                       "gicp_launches_per_call": 1}, f)
     print("done", n)
 
 
