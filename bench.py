@@ -273,6 +273,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--c3-steps", type=int, default=3, help="timed C3 (GICP) steps; 0 skips the C3 leg")
     ap.add_argument("--c3-warmup", type=int, default=1)
+    ap.add_argument("--force-pg", action="store_true",
+                    help="at --gpus 1, start a one-rank process group (RCCL) so every step runs the argmin exchange")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -295,7 +297,7 @@ def main():
     # one rank per GPU; the modulo only matters for a several-ranks-per-GPU rehearsal (PCORE_DIST_BACKEND=gloo)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
-    pdist.init_from_env()
+    pdist.init_from_env(force=True if args.force_pg else None)
     joined = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
     if joined != world:
         raise SystemExit(f"bench.py: {joined} ranks joined, WORLD_SIZE={world}")
@@ -508,7 +510,9 @@ def main():
                                "stride 8, no ICP", "poses_per_gpu": n, "width": w.scene.width,
                    "height": w.scene.height, "stride": s, "parallelism": f"pose-shard x{world}",
                    "batches_in_flight": L, "ranks": joined, "devices": devices,
-                   "dist_backend": torch.distributed.get_backend() if joined > 1 else None},
+                   "dist_backend": torch.distributed.get_backend() if pdist.exchange_active() else None,
+                   "exchange": ("all_reduce(MIN) of the int64 argmin keys per step" if pdist.exchange_active()
+                                else "none (one process)")},
         "roofline": roofline,
         "host_timing": host_timing,
         "argmin": {"best_cost": int(best_cost[0]), "best_index": int(best_idx[0]), "gt_index": int(w.gt_index[0])},

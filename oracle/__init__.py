@@ -226,7 +226,8 @@ def _gicp_lib():
                                        _opt(_i32p), _f32p, _f32p, _f32p, c_int]
         L.orc_gicp_trace.restype = c_int
         L.orc_gicp_trace.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, c_int, c_double, c_double, c_int,
-                                     _f64p, _opt(_f64p), _opt(_i32p)]
+                                     _f64p, _opt(_f64p), _opt(_i32p), c_int]
+        L.orc_gicp_lm_solve_ldlt.argtypes = [_f64p, c_double, _f64p]
         L.orc_gicp_linearize.argtypes = [_f32p, _f64p, c_int, _f32p, _f64p, c_int, _f64p, c_int, _i32p, _f64p]
         L.orc_gicp_se3_exp.argtypes = [_f64p, _f64p]
         L.orc_gicp_lm_solve.argtypes = [_f64p, c_double, _f64p]
@@ -271,10 +272,11 @@ def gicp(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EP
 
 
 def gicp_trace(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_ROT_EPS, trans_eps=GICP_TRANS_EPS,
-               cycle_window=0):
+               cycle_window=0, solver="schur"):
     """orc_gicp with its per-iteration trace: (T, iterations reported, trace (executed iterations, 16): R (9), t (3)
     after each iteration, the lambda of its first trial, its number of trials, flags (1: lambda inert, 2: accepted
-    with rho >= 1/2), the LM status).  The cycle exit is off unless cycle_window > 0."""
+    with rho >= 1/2), the LM status).  The cycle exit is off unless cycle_window > 0.  solver "schur" is the spec's
+    damped solve, "ldlt" Eigen's pivoted LDLT as fast_gicp uses it (a test reference)."""
     src = _c(src, np.float32).reshape(-1, 3)
     tgt = _c(tgt, np.float32).reshape(-1, 3)
     T = np.zeros(16, np.float64)
@@ -282,7 +284,7 @@ def gicp_trace(src, src_cov, tgt, tgt_cov, max_iter=GICP_MAX_ITER, rot_eps=GICP_
     ex = np.zeros(1, np.int32)
     it = _gicp_lib().orc_gicp_trace(src.reshape(-1), _c(src_cov, np.float64).reshape(-1), len(src), tgt.reshape(-1),
                                     _c(tgt_cov, np.float64).reshape(-1), len(tgt), max_iter, rot_eps, trans_eps,
-                                    int(cycle_window), T, tr.reshape(-1), ex)
+                                    int(cycle_window), T, tr.reshape(-1), ex, {"schur": 0, "ldlt": 1}[solver])
     return T.reshape(4, 4), it, tr[:int(ex[0])]
 
 
@@ -323,6 +325,14 @@ def gicp_lm_solve_sys(sys, lam):
     sys = np.ascontiguousarray(sys, np.float64).reshape(28)
     d = np.zeros(6, np.float64)
     _gicp_lib().orc_gicp_lm_solve(sys, float(lam), d)
+    return d
+
+
+def gicp_lm_solve_ldlt_sys(sys, lam):
+    """The same system solved by Eigen's pivoted LDLT (fast_gicp's solve; a test reference)."""
+    sys = np.ascontiguousarray(sys, np.float64).reshape(28)
+    d = np.zeros(6, np.float64)
+    _gicp_lib().orc_gicp_lm_solve_ldlt(sys, float(lam), d)
     return d
 
 

@@ -633,10 +633,79 @@ void gicp_linearize_spec(const OXform& x, const float* src_xyz, const double* sr
     for (int v = 0; v < NT; v++) sys[v] = lane_tree(part.data(), NT, v);
 }
 
+// Test reference only: the damped solve as fast_gicp performs it, Eigen's LDLT with diagonal pivoting
+// (Eigen 3 LDLT::compute -> ldlt_inplace<Lower>::unblocked, left-looking: the pivot is the largest |diagonal| of the
+// not yet factored part, swapped in place; D's pseudo-inverse zeroes pivots below the smallest normal), then
+// P^T L^-T D^+ L^-1 P (-b).  The spec solves by block elimination (lm_solve_schur); orc_gicp_trace(solver = 1)
+// runs whole chains on this one so tests can measure where the two solves change an LM decision.
+void ldlt_solve_ref(const double* sys, double lambda, double (&d)[6]) {
+    double A[6][6];
+    int h = 0;
+    for (int a = 0; a < 6; a++)
+        for (int c = a; c < 6; c++) {
+            A[c][a] = a == c ? sys[h] + lambda : sys[h];  // the lower triangle of H + lambda I
+            h++;
+        }
+    int tr[6];
+    bool zero = false;
+    for (int k = 0; k < 6; k++) {
+        int p = k;
+        double big = std::fabs(A[k][k]);
+        for (int i = k + 1; i < 6; i++)
+            if (std::fabs(A[i][i]) > big) { big = std::fabs(A[i][i]); p = i; }
+        tr[k] = p;
+        if (p != k) {  // symmetric swap of rows / columns k and p in the lower triangle
+            for (int j = 0; j < k; j++) std::swap(A[k][j], A[p][j]);
+            for (int i = p + 1; i < 6; i++) std::swap(A[i][k], A[i][p]);
+            std::swap(A[k][k], A[p][p]);
+            for (int i = k + 1; i < p; i++) std::swap(A[i][k], A[p][i]);
+        }
+        if (k > 0) {
+            double temp[6];
+            for (int j = 0; j < k; j++) temp[j] = A[j][j] * A[k][j];
+            double s = A[k][0] * temp[0];
+            for (int j = 1; j < k; j++) s = s + A[k][j] * temp[j];
+            A[k][k] = A[k][k] - s;
+            for (int i = k + 1; i < 6; i++) {
+                double w = A[i][0] * temp[0];
+                for (int j = 1; j < k; j++) w = w + A[i][j] * temp[j];
+                A[i][k] = A[i][k] - w;
+            }
+        }
+        const double akk = A[k][k];
+        if (k == 0 && !(std::fabs(akk) > 0.0)) {  // the whole diagonal is zero
+            zero = true;
+            break;
+        }
+        if (std::fabs(akk) > 0.0)
+            for (int i = k + 1; i < 6; i++) A[i][k] = A[i][k] / akk;
+    }
+    double x[6];
+    for (int i = 0; i < 6; i++) x[i] = -sys[21 + i];
+    if (zero) {
+        for (int i = 0; i < 6; i++) d[i] = 0.0;
+        return;
+    }
+    for (int k = 0; k < 6; k++) std::swap(x[k], x[tr[k]]);
+    for (int j = 0; j < 6; j++)
+        for (int i = j + 1; i < 6; i++) x[i] = x[i] - x[j] * A[i][j];
+    for (int i = 0; i < 6; i++) {
+        const double Di = A[i][i];
+        x[i] = std::fabs(Di) > 2.2250738585072014e-308 ? x[i] / Di : 0.0;
+    }
+    for (int i = 4; i >= 0; i--) {
+        double s = A[i + 1][i] * x[i + 1];
+        for (int j = i + 2; j < 6; j++) s = s + A[j][i] * x[j];
+        x[i] = x[i] - s;
+    }
+    for (int k = 5; k >= 0; k--) std::swap(x[k], x[tr[k]]);
+    for (int i = 0; i < 6; i++) d[i] = x[i];
+}
+
 // One LM iteration (LsqRegistration::step_lm) on the reduced system, as the GPU's lm_iteration
 int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double& lambda, const float* src_xyz, int ns,
                       const float* tgt_xyz, const int32_t* corr, const double* mah, double rot_eps, double trans_eps,
-                      double* lambda_used, int* trials = nullptr, int* flags = nullptr) {
+                      double* lambda_used, int* trials = nullptr, int* flags = nullptr, int solver = 0) {
     namespace gm = pcore::gicpm;
     const double y0 = sys[gm::kErr];
     if (lambda < 0.0) lambda = gm::lm_init_lambda(sys);
@@ -647,7 +716,8 @@ int gicp_lm_iteration(const double sys[pcore::gicpm::kTerms], OXform& x, double&
     for (int trial = 0; trial < gm::kLmMaxTrials; trial++) {
         if (trials) *trials = trial + 1;
         double d[6];
-        gm::lm_solve_schur(sys, lambda, d);
+        if (solver == 1) ldlt_solve_ref(sys, lambda, d);
+        else gm::lm_solve_schur(sys, lambda, d);
         if (!gm::all_finite6(d)) return gm::kLmFailed;
         double Rd[3][3], td[3];
         gm::se3_exp(d, Rd, td, gm::kSe3Coef);
@@ -789,7 +859,7 @@ void orc_covariances(const float* xyz, int n, int k, double* out_cov6) {
 // reported (max_iter after a cycle exit); *executed (nullable) the iterations run.
 int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
                    int nt, int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T,
-                   double* trace, int* executed) {
+                   double* trace, int* executed, int solver) {
     namespace gm = pcore::gicpm;
     OXform x;
     for (int r = 0; r < 3; r++) {
@@ -829,7 +899,7 @@ int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const fl
             double lam_used;
             int trials = 0, flags = 0;
             const int st = gicp_lm_iteration(sys, x, lambda, src_xyz, ns, tgt_xyz, corr.data(), mah.data(), rot_eps,
-                                             trans_eps, &lam_used, &trials, &flags);
+                                             trans_eps, &lam_used, &trials, &flags, solver);
             if (trace) {
                 double* tr = trace + (size_t)16 * k;
                 for (int r = 0; r < 3; r++) {
@@ -876,7 +946,7 @@ int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const fl
 int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov, int nt,
              int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T) {
     return orc_gicp_trace(src_xyz, src_cov, ns, tgt_xyz, tgt_cov, nt, max_iter, rot_eps, trans_eps, cycle_window, out_T,
-                          nullptr, nullptr);
+                          nullptr, nullptr, 0);
 }
 
 // The linearisation at T (double 4x4 row-major) two ways, on the spec's correspondences (out_corr, ns):
@@ -929,6 +999,12 @@ void orc_gicp_se3_exp(const double* a6, double* out_T) {
         out_T[4 * r + 3] = td[r];
     }
     out_T[12] = 0.0; out_T[13] = 0.0; out_T[14] = 0.0; out_T[15] = 1.0;
+}
+
+void orc_gicp_lm_solve_ldlt(const double* sys, double lambda, double* out_d) {
+    double d[6];
+    ldlt_solve_ref(sys, lambda, d);
+    for (int a = 0; a < 6; a++) out_d[a] = d[a];
 }
 
 void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d) {

@@ -123,10 +123,11 @@ int orc_gicp(const float* src_xyz, const double* src_cov, int ns, const float* t
 
 /* orc_gicp with a per-iteration trace (nullable; max_iter x 16 doubles: R (9) and t (3) after the iteration, the
  * lambda of its first trial, its trials, flags (1 lambda inert, 2 rho >= 1/2), the LM status 0 accepted /
- * 1 converged / 2 failed); *executed (nullable): the iterations run (rows of the trace). */
+ * 1 converged / 2 failed); *executed (nullable): the iterations run (rows of the trace); solver 0 the spec's block
+ * elimination, 1 Eigen's LDLT (orc_gicp_lm_solve_ldlt, a test reference). */
 int orc_gicp_trace(const float* src_xyz, const double* src_cov, int ns, const float* tgt_xyz, const double* tgt_cov,
                    int nt, int max_iter, double rot_eps, double trans_eps, int cycle_window, double* out_T,
-                   double* trace, int* executed);
+                   double* trace, int* executed, int solver);
 
 /* The linearisation at T (4x4 row-major double) on the spec's correspondences (out_corr: ns, -1 = none):
  * textbook = 0 the spec's arithmetic and reduction order, textbook = 1 an independent long-double restatement of
@@ -139,6 +140,8 @@ void orc_gicp_linearize(const float* src_xyz, const double* src_cov, int ns, con
  * (lm_solve_schur); the double sin / cos of pcore_dmath.h; the spec's correspondences of n float queries. */
 void orc_gicp_se3_exp(const double* a6, double* out_T);
 void orc_gicp_lm_solve(const double* sys, double lambda, double* out_d);
+/* Test reference: the damped solve by Eigen's pivoted LDLT (what fast_gicp uses; orc_gicp_trace solver = 1). */
+void orc_gicp_lm_solve_ldlt(const double* sys, double lambda, double* out_d);
 double orc_sin_d(double x);
 double orc_cos_d(double x);
 double orc_cube_rn(double u);   // step_lm's std::pow(u, 3), rounded once

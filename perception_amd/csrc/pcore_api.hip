@@ -986,7 +986,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     if (use_hist) HIPC(c, dev_reserve(c->icp_corr_hist, (size_t)chunk * kCorrHist * hist_cap));
     HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 1));
-    HIPC(c, dev_reserve(c->icp_iter_stats, 3));
+    HIPC(c, dev_reserve(c->icp_iter_stats, 4));
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
     const size_t order_temp = gicp_order_temp_bytes(chunk);
@@ -1003,7 +1003,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, hipStreamIsCapturing(s, &cap_status));
     const bool timed = cap_status == hipStreamCaptureStatusNone;
     c->icp_ev_used = 0;
-    HIPC(c, hipMemsetAsync(c->icp_iter_stats.p, 0, 3 * sizeof(unsigned long long), s));
+    HIPC(c, hipMemsetAsync(c->icp_iter_stats.p, 0, 4 * sizeof(unsigned long long), s));
     while (timed && c->icp_ev.size() < (size_t)3 * nchunks) {
         hipEvent_t e;
         HIPC(c, hipEventCreate(&e));
@@ -1044,9 +1044,9 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     bool grid_needed = false;
     if (c->grids.p) {
         if (six) {
-            for (int L = 0; L < nl; L++) grid_needed = grid_needed || c->seg_cnt_h[L] > kGridNNMin;
+            for (int L = 0; L < nl; L++) grid_needed = grid_needed || segment_uses_grid(c->seg_cnt_h[L], true);
         } else {
-            grid_needed = c->seg_cnt_h[nl] > kGridNNMin;
+            grid_needed = segment_uses_grid(c->seg_cnt_h[nl], true);
         }
     }
     for (int base = 0; base < num_poses; base += chunk) {
@@ -1133,9 +1133,12 @@ int pcore_get_stats(pcore_ctx* c, pcore_gpu_stats* out, int32_t reset) {
     out->peak_memory_usage = c->peak_mem_mb;
     out->gicp_ms = (float)gicp_ms;
     out->icp_chunks = c->icp_ev_used;
-    unsigned long long it[3] = {0ull, 0ull, 0ull};
+    unsigned long long it[4] = {0ull, 0ull, 0ull, 0ull};
     if (c->icp_ev_used > 0 && c->icp_iter_stats.p)  // the last chunk's end event has completed
         HIPC(c, hipMemcpy(it, c->icp_iter_stats.p, sizeof(it), hipMemcpyDeviceToHost));
+    if (it[3] != 0)
+        return fail(c, PCORE_E_HIP, "evaluate_icp: " + std::to_string(it[3]) +
+                                        " poses needed the grid search in the GICP instance without it");
     out->gicp_iterations = (int64_t)it[0];
     out->gicp_iterations_run = (int64_t)it[1];
     out->gicp_cycle_exits = (int64_t)it[2];

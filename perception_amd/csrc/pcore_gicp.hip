@@ -74,6 +74,10 @@ constexpr int kTlPoses = 1 << 17, kTlWaves = 1 << 14;
 __device__ unsigned long long g_tl_pose[2 * kTlPoses];
 __device__ unsigned long long g_tl_wave[2 * kTlWaves];
 __device__ unsigned int g_tl_nwaves;
+__device__ int g_tl_run[kTlPoses];  // iterations each pose executed (fewer than it reports after a cycle exit)
+extern "C" int pcore_debug_gicp_timeline_run(int* run) {
+    return hipMemcpyFromSymbol(run, HIP_SYMBOL(g_tl_run), sizeof(g_tl_run)) == hipSuccess ? 0 : 1;
+}
 extern "C" int pcore_debug_gicp_timeline(unsigned long long* poses, unsigned long long* waves, unsigned int* nwaves) {
     hipError_t e = hipMemcpyFromSymbol(poses, HIP_SYMBOL(g_tl_pose), sizeof(g_tl_pose));
     if (e == hipSuccess) e = hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_tl_wave), sizeof(g_tl_wave));
@@ -1082,7 +1086,7 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
     p.tcov = g.tgt_cov + (size_t)6 * lo;
     p.tgt = g.tgt + lo;
     p.tquads = g.tgt_quads + (seg >= 0 ? (size_t)16 * g.seg_qoff[seg] : 0);
-    p.use_grid = p.nt > kGridNNMin && g.grids != nullptr && seg >= 0;  // exact grid shell search
+    p.use_grid = seg >= 0 && segment_uses_grid(p.nt, g.grids != nullptr);  // exact grid shell search
     return p;
 }
 
@@ -1124,6 +1128,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
         const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
         if (pose >= num_poses) break;
         const GicpPose P = gicp_pose(g, pose);
+        if (!GRID && P.use_grid && lane == 0 && g.iter_stats)  // the host picked the instance without the search
+            __hip_atomic_fetch_add(g.iter_stats + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef PCORE_GICP_TIMELINE
         const unsigned long long tl_p0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1256,6 +1262,7 @@ gicp_kernel(GicpArgs g, int num_poses) {
         if (lane == 0 && P.gp < kTlPoses) {
             g_tl_pose[2 * P.gp] = tl_p0;
             g_tl_pose[2 * P.gp + 1] = __builtin_amdgcn_s_memrealtime();
+            g_tl_run[P.gp] = iters_run ? iters_run : iters;
         }
 #endif
     }

@@ -177,7 +177,8 @@ struct GicpArgs {
     int32_t* corr_hist;       // nullable: no history
     int32_t corr_hist_cap;
     // the cycle exit's window W (pcore_gicp_math.h cycle_update; 0 = off) and the launch's iteration counters
-    // (nullable; [0] iterations reported, [1] iterations run, [2] cycle exits: one no-return atomic each per pose)
+    // (nullable; [0] iterations reported, [1] iterations run, [2] cycle exits: one no-return atomic each per pose;
+    // [3] poses that needed the grid search in the instance without it -- a host / kernel rule mismatch, an error)
     int32_t cycle_window;
     unsigned long long* iter_stats;
 };
@@ -188,6 +189,12 @@ constexpr int kCorrHistCap = 512;  // source points per history set (poses with 
 // segments above this many points use the exact shell search of their neighbour grid (GICP
 // correspondences and target covariances); smaller ones the brute-force scans
 constexpr int kGridNNMin = 2048;
+
+// The one rule for the exact grid search of a GICP target segment, shared by the host (which launches the
+// gicp_kernel instance holding the search only when some segment needs it) and the kernels (gicp_pose's use_grid)
+__host__ __device__ inline bool segment_uses_grid(int nt, bool grids_present) {
+    return grids_present && nt > kGridNNMin;
+}
 static_assert(kGridNNMin == gicpm::kKeyScanMax, "the key scan covers exactly the segments without the grid search");
 
 // gfx950 allocates a workgroup's LDS in 1,280-byte granules (160 KiB = 128 of them), not the 512 bytes of

@@ -225,25 +225,47 @@ _POSES_CACHE: "OrderedDict[tuple, np.ndarray]" = OrderedDict()
 _POSES_CACHE_MAX = 64
 _POSES_STAT: "OrderedDict[str, tuple]" = OrderedDict()  # abspath -> (stat signature, content digest)
 _SETTLED_NS = 2_000_000_000
+# where the file system's clock cannot be measured (no temporary file can be created: a read-only data set), "settled"
+# is judged on this host's clock with a wider margin instead
+_SETTLED_LOCAL_NS = 60_000_000_000
+_FS_CLOCK: dict = {}  # st_dev -> (offset of the file system's clock from time.time_ns or None, time_ns, monotonic_ns)
+_FS_CLOCK_TTL_NS = 600_000_000_000
 
 
-def _fs_now_ns(directory: str):
-    """The current time on the clock of the file system holding `directory`: the ctime of a temporary file created
-    there (None when none can be created, e.g. a read-only data set)."""
+def _fs_clock_offset(directory: str):
+    """The file system's clock minus this host's (ns): the ctime of a temporary file created in `directory` against
+    time.time_ns() around its creation; None when no file can be created there."""
     import tempfile
 
+    t0 = time.time_ns()
     try:
         fd, tmp = tempfile.mkstemp(prefix=".pcore_clock_", dir=directory)
     except OSError:
         return None
     try:
-        return os.fstat(fd).st_ctime_ns
+        ctime = os.fstat(fd).st_ctime_ns
     finally:
         os.close(fd)
         try:
             os.unlink(tmp)
         except OSError:
             pass
+    return ctime - (t0 + time.time_ns()) // 2
+
+
+def _fs_now_ns(directory: str, dev=None):
+    """The current time on the clock of the file system holding `directory` (None when it cannot be measured).  The
+    clock's offset from this host's is measured once per device (one temporary file, not one per read: ADVICE r05) and
+    measured again after 10 minutes, or at once when this host's wall clock stepped (its advance since the measurement
+    differs from the monotonic clock's by more than 1 s)."""
+    if dev is None:
+        dev = os.stat(directory).st_dev
+    now, mono = time.time_ns(), time.monotonic_ns()
+    ent = _FS_CLOCK.get(dev)
+    if ent is None or now - ent[1] > _FS_CLOCK_TTL_NS or abs((now - ent[1]) - (mono - ent[2])) > 1_000_000_000:
+        ent = (_fs_clock_offset(directory), now, mono)
+        _FS_CLOCK[dev] = ent
+    return None if ent[0] is None else now + ent[0]
 
 
 def _stat_signature(st: os.stat_result) -> tuple:
@@ -260,7 +282,9 @@ def read_poses_txt_cached(path: str, use_cache: bool = True) -> np.ndarray:
     inode, size, mtime, ctime) stay the same: any write after that read sets ctime to the current time, which no
     utime call can set back, so an unchanged signature means unchanged bytes.  "Now" is the file system's own clock
     (the ctime of a temporary file created beside it), not this host's, so a server clock that lags (NFS) cannot make a
-    fresh file look settled; where no temporary file can be created the file is never taken as settled.
+    fresh file look settled.  The file system's clock is this host's plus an offset measured once per
+    device (a temporary file per read wrote into the data set); where no temporary file can be created
+    (a read-only data set) the host's clock stands in with a 60 s margin.
     A file changed within the last 2 s (the kernel's timestamp clock is coarse) is read and hashed every time.  Least-recently-used eviction past 64
     files.  use_cache=False (or PCORE_POSES_CACHE=0) parses every time.  Returns a read-only array."""
     if not use_cache or os.environ.get("PCORE_POSES_CACHE", "1") == "0":
@@ -279,8 +303,14 @@ def read_poses_txt_cached(path: str, use_cache: bool = True) -> np.ndarray:
         sig_read = _stat_signature(os.fstat(f.fileno()))
     key = (apath, _content_digest(data))
     _POSES_STAT.pop(apath, None)
-    fs_now = _fs_now_ns(os.path.dirname(apath)) if sig_open == sig_read else None
-    if fs_now is not None and fs_now - sig_read[4] > _SETTLED_NS:
+    settled = False
+    if sig_open == sig_read:
+        fs_now = _fs_now_ns(os.path.dirname(apath), sig_read[0])
+        if fs_now is not None:
+            settled = fs_now - sig_read[4] > _SETTLED_NS
+        else:
+            settled = time.time_ns() - sig_read[4] > _SETTLED_LOCAL_NS
+    if settled:
         _POSES_STAT[apath] = (sig_read, key[1])
         while len(_POSES_STAT) > _POSES_CACHE_MAX:
             _POSES_STAT.popitem(last=False)

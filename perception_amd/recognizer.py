@@ -544,7 +544,12 @@ class ObjectRecognizer:
         found = [m for m in range(K) if idx[m] >= 0]
         conts = self.adjusted_cont_poses(win[found], np.array(found, np.int32), inp.use_external_pose_list)
         results = [(m, int(cost[m]), int(idx[m]), conts[r]) for r, m in enumerate(found)]
-        if self.debug_dir is not None:
+        dump = self.debug_dir is not None
+        if world > 1:  # rank 0's debug_dir decides, so every rank takes part in the gather
+            flag = torch.tensor([1 if dump else 0], dtype=torch.int32, device=self.device)
+            torch.distributed.broadcast(flag, src=0)
+            dump = bool(flag.item())
+        if dump:
             self._write_cost_dump(inp, n_total, lo, n, adj_all if n > 0 else None, pm if n > 0 else None, world, rank)
         t_end = time.perf_counter()
         # host-side breakdown of the last search (seconds): successor states (poses.txt + IsValidPose), per-state
@@ -585,33 +590,35 @@ class ObjectRecognizer:
         source_cost = (int) oc, total_cost = (int) (rc + oc), transform (GetRawModelToSceneTransform of the adjusted
         pose, column-major), translation, quaternion (x y z w) and lie_rotation (Sophus SO3f log).  The costs are the
         ones this search's argmin used, read back from the device outputs it already holds (no extra launch); with
-        several ranks the shards are gathered on rank 0, which writes the file."""
+        several ranks the kept rows of every shard are gathered on rank 0, which writes the file into its debug_dir
+        (every rank calls this when rank 0's debug_dir is set)."""
         if n > 0:
             rc, oc, _ = self._last_costs
             adj_h, pm_h = adj.cpu().numpy(), pm.cpu().numpy()
         else:
             rc = oc = np.zeros(0, np.float32)
             adj_h, pm_h = np.zeros((0, 16), np.float32), np.zeros(0, np.int32)
-        part = (lo, rc, oc, adj_h, pm_h)
-        if world > 1:
-            parts = [None] * world
-            torch.distributed.all_gather_object(parts, part)
-            if rank != 0:
-                return
-            parts.sort(key=lambda p: p[0])
-            lo, rc, oc, adj_h, pm_h = 0, *(np.concatenate([p[k] for p in parts]) for k in range(1, 5))
         target, source = cvtt_i32(rc), cvtt_i32(oc)
         total = cvtt_i32(np.asarray(rc, np.float32) + np.asarray(oc, np.float32))
         cost = np.where(target < 0, -1, total)
         keep = np.nonzero((cost != -1) & (cost != -2))[0]
-        cont = self.adjusted_cont_poses(adj_h[keep], pm_h[keep], inp.use_external_pose_list)
-        T = self.raw_model_to_scene(cont, pm_h[keep])
+        ids, target, source, cost = keep + lo, target[keep], source[keep], cost[keep]
+        adj_h, pm_h = adj_h[keep], pm_h[keep]
+        if world > 1:  # only the kept rows travel
+            parts = [None] * world
+            torch.distributed.all_gather_object(parts, (lo, ids, target, source, cost, adj_h, pm_h))
+            if rank != 0:
+                return
+            parts.sort(key=lambda p: p[0])
+            ids, target, source, cost, adj_h, pm_h = (np.concatenate([p[k] for p in parts]) for k in range(1, 7))
+        cont = self.adjusted_cont_poses(adj_h, pm_h, inp.use_external_pose_list)
+        T = self.raw_model_to_scene(cont, pm_h)
         lie = so3_log_batch(quat_from_matrix_eigen_batch(T[:, :3, :3], np.float32), np.float32)
         c32 = cont.astype(np.float32)
         poses = []
-        for r, i in enumerate(keep):
-            poses.append({"id": int(lo + i), "target_cost": int(target[i]), "source_cost": int(source[i]),
-                          "total_cost": int(cost[i]),
+        for r in range(len(ids)):
+            poses.append({"id": int(ids[r]), "target_cost": int(target[r]), "source_cost": int(source[r]),
+                          "total_cost": int(cost[r]),
                           "transform": [float(v) for v in T[r].T.reshape(-1)],  # Eigen's column-major data()
                           "translation": [float(v) for v in c32[r, :3]],
                           "quaternion": [float(v) for v in c32[r, 3:7]],

@@ -2,6 +2,8 @@
 
 - YCB proxies: boxes / cylinders with YCB nominal dimensions, every face tessellated.
   The 003_cracker_box proxy (0.060 x 0.158 x 0.210 m, 32 x 32 quads per face) has 12,288 triangles.
+- Scan-like irregular meshes (scan_blob closed, scan_shell open; ~20-24 k triangles, varied triangle sizes and
+  valence, slivers, shuffled face order), as the reference's assimp meshes of real scans are (model.cpp:16-49).
 - Camera: the reference's 640x480 intrinsics (sbpl_perception/config/camera_config.yaml:2-7) and the
   1280x720 variant of C5.
 - Scenes: GT poses rendered with a caller-supplied depth renderer (the GPU RENDER stage on the box, the
@@ -102,7 +104,87 @@ def cylinder_mesh(diameter: float, height: float, segments: int = 64, rings: int
     return np.asarray(tris, dtype=np.float32)
 
 
+def icosphere(level: int):
+    """Unit icosphere: (vertices (V, 3) float64, faces (F, 3) int64, outward winding), F = 20 * 4^level."""
+    t = (1.0 + 5 ** 0.5) / 2.0
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+         (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10),
+         (8, 6, 7), (9, 8, 1)]
+    V = np.asarray(V, np.float64)
+    V /= np.linalg.norm(V, axis=1, keepdims=True)
+    F = np.asarray(F, np.int64)
+    for _ in range(level):
+        e = np.concatenate([F[:, [0, 1]], F[:, [1, 2]], F[:, [2, 0]]])
+        key = np.sort(e, axis=1)
+        uniq, inv = np.unique(key, axis=0, return_inverse=True)
+        mid = V[uniq[:, 0]] + V[uniq[:, 1]]
+        mid /= np.linalg.norm(mid, axis=1, keepdims=True)
+        m = inv.reshape(3, -1).T + len(V)  # midpoints of edges 01, 12, 20
+        V = np.concatenate([V, mid])
+        a, b, c = F[:, 0], F[:, 1], F[:, 2]
+        ab, bc, ca = m[:, 0], m[:, 1], m[:, 2]
+        F = np.concatenate([np.stack([a, ab, ca], 1), np.stack([b, bc, ab], 1), np.stack([c, ca, bc], 1),
+                            np.stack([ab, bc, ca], 1)])
+    return V, F
+
+
+def scan_mesh(semi_axes: Sequence[float], level: int = 5, open_below: Optional[float] = None, split_frac: float = 0.15,
+              seed: int = 0) -> np.ndarray:
+    """A scan-like irregular mesh: an icosphere whose vertex density is warped towards one
+    side (triangle areas vary ~10x, elongated triangles), displaced by low-frequency bumps and per-vertex noise,
+    scaled to an ellipsoid; a fraction of the triangles split at a random point of their longest edge (slivers,
+    T-junctions, uneven valence); optionally cut open (faces whose centroid lies below `open_below` on the warped
+    z axis are dropped: a partial scan); face order shuffled and each face's vertex order rotated (winding kept).
+    Returns (T, 9) float32."""
+    rng = np.random.default_rng(seed)
+    V, F = icosphere(level)
+    d = np.array([0.3, -0.2, 0.93])
+    d /= np.linalg.norm(d)
+    V = V + 0.55 * d
+    V /= np.linalg.norm(V, axis=1, keepdims=True)
+    r = np.ones(len(V))
+    for _ in range(6):  # low-frequency bumps
+        u = rng.normal(size=3)
+        u /= np.linalg.norm(u)
+        r += 0.05 * np.sin(rng.uniform(2.0, 5.0) * (V @ u) + rng.uniform(0, 2 * np.pi))
+    r += rng.normal(0.0, 0.006, len(V))  # sensor-like vertex noise
+    V = V * r[:, None] * np.asarray(semi_axes, np.float64)[None, :]
+    keep = np.ones(len(F), bool)
+    if open_below is not None:
+        cz = V[F].mean(1) @ (d * np.asarray(semi_axes)) / np.linalg.norm(d * np.asarray(semi_axes))
+        keep = cz > open_below * float(np.max(semi_axes))
+    F = F[keep]
+    T = V[F]  # (F, 3, 3)
+    ns = int(split_frac * len(T))
+    sel = rng.choice(len(T), ns, replace=False)
+    tris = [np.delete(T, sel, axis=0)]
+    for t in T[sel]:
+        el = [np.linalg.norm(t[(i + 1) % 3] - t[i]) for i in range(3)]
+        i = int(np.argmax(el))
+        a, b, c = t[i], t[(i + 1) % 3], t[(i + 2) % 3]
+        p = a + rng.uniform(0.1, 0.9) * (b - a)
+        tris.append(np.stack([np.stack([a, p, c]), np.stack([p, b, c])]))
+    T = np.concatenate(tris)
+    T = T[rng.permutation(len(T))]
+    rot = rng.integers(0, 3, len(T))
+    idx = (np.arange(3)[None, :] + rot[:, None]) % 3
+    T = np.take_along_axis(T, idx[:, :, None], axis=1)
+    return T.reshape(-1, 9).astype(np.float32)
+
+
+# scan-like irregular meshes: (semi-axes in metres, icosphere level, open_below, seed)
+SCAN_MESHES = {
+    "scan_blob": ((0.045, 0.075, 0.100), 5, None, 3),    # closed, ~23.5 k triangles
+    "scan_shell": ((0.070, 0.060, 0.080), 5, -0.45, 5),  # open partial scan, ~20 k triangles
+}
+
+
 def ycb_proxy(name: str, k: int = 32) -> Model:
+    if name in SCAN_MESHES:
+        axes, level, open_below, seed = SCAN_MESHES[name]
+        return Model(name=name, tris=scan_mesh(axes, level, open_below, seed=seed))
     kind, dims = YCB_PROXIES[name]
     tris = box_mesh(dims, k) if kind == "box" else cylinder_mesh(*dims)
     return Model(name=name, tris=tris)

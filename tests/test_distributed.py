@@ -69,3 +69,37 @@ def test_gloo_world2_argmin_equals_single_process():
         assert np.array_equal(cost, ref_cost) and np.array_equal(idx, ref_idx)
         assert np.array_equal(ca, ref_cost) and np.array_equal(ia, ref_idx)
         assert np.array_equal(cb, ref2[0]) and np.array_equal(ib, ref2[1])
+
+
+def _forced_worker(q):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        os.environ.pop(k, None)
+    import torch
+    import torch.distributed as dist
+
+    from perception_amd.distributed import allreduce_min_keys_async, exchange_active, init_from_env
+
+    init_from_env("gloo")  # world 1, not forced: no process group
+    before = dist.is_initialized()
+    init_from_env("gloo", force=True)
+    keys = torch.tensor([5, -3, 2 ** 62], dtype=torch.int64)
+    work = allreduce_min_keys_async(keys)
+    ok = work is not None
+    if ok:
+        work.wait()
+    q.put((before, dist.is_initialized(), dist.get_world_size(), exchange_active(), ok, keys.tolist()))
+    dist.destroy_process_group()
+
+
+def test_forced_one_rank_process_group_runs_the_exchange():
+    """bench.py --force-pg / PCORE_FORCE_PG=1: at world size 1 init_from_env starts a one-rank group only when forced,
+    and the exchange then runs (a work handle, keys unchanged by a MIN over one rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(q,))
+    p.start()
+    before, inited, world, active, ok, keys = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert not before and inited and world == 1 and active and ok
+    assert keys == [5, -3, 2 ** 62]

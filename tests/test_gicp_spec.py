@@ -309,6 +309,31 @@ def test_cycle_exit_against_full_length_chains(c3_pairs_120):
     assert exits >= 20 and run_on < 0.75 * run_off
 
 
+def test_schur_and_ldlt_chains_take_the_same_decisions(c3_pairs_120):
+    """the spec's damped solve (3x3 block elimination) against fast_gicp's own (Eigen's pivoted LDLT,
+    restated in the oracle as a test reference) over whole GICP chains on the 120 C3 candidates, every iteration run
+    out: every iteration's LM decision (trials, status) is the same, so the iteration counts are; the transforms
+    agree to 1e-9.  And the two solves agree on the lm_solve_cases systems within 1e-14 cond relative."""
+    worst = 0.0
+    for src, scov_o, _, tgt, tcov_o, _ in c3_pairs_120:
+        T1, it1, tr1 = oracle.gicp_trace(src, scov_o, tgt, tcov_o, solver="schur")
+        T2, it2, tr2 = oracle.gicp_trace(src, scov_o, tgt, tcov_o, solver="ldlt")
+        assert it1 == it2
+        assert np.array_equal(tr1[:, 13], tr2[:, 13]) and np.array_equal(tr1[:, 15], tr2[:, 15])
+        worst = max(worst, float(np.abs(T1 - T2).max()))
+    assert worst < 1e-9
+    for sysv, lam in lm_solve_cases()[:1500]:
+        if not np.isfinite(sysv).all():
+            continue
+        H = np.zeros((6, 6))
+        H[np.triu_indices(6)] = sysv[:21]
+        Hs = H + np.triu(H, 1).T + lam * np.eye(6)
+        if not (np.all(np.linalg.eigvalsh(Hs) > 1e-12 * np.abs(Hs).max()) and np.linalg.cond(Hs) < 1e10):
+            continue
+        d1, d2 = oracle.gicp_lm_solve_sys(sysv, lam), oracle.gicp_lm_solve_ldlt_sys(sysv, lam)
+        assert np.abs(d1 - d2).max() <= 1e-14 * np.linalg.cond(Hs) * np.abs(d2).max() + 1e-300
+
+
 def test_cycle_window_constants_agree():
     """The spec's window is one number in the oracle, the Python host and include/pcore.h."""
     import re

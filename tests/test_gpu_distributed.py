@@ -74,3 +74,25 @@ def test_gloo_world2_product_select_equals_oracle_rule():
     for _, _, _, _, _, (cost, idx) in res:
         assert np.array_equal(cost, ocost) and np.array_equal(idx, oidx)
     assert int(oidx[0]) == w.gt_index[0]
+
+
+def test_rccl_one_rank_lane_pattern_keys_equal_no_process_group():
+    """the RCCL branch executes on the one-GPU box.  tools/rccl_lane_check.py runs in a fresh
+    child process (started with subprocess: no exec, nothing touches the GPU before the process group exists):
+    init_process_group("nccl", world 1, device_id cuda:0), then bench.py's lane pattern (two lanes, a ring of int64
+    key buffers, all_reduce(MIN, async_op=True) issued from the lane's stream, work.wait() before a buffer is
+    refilled).  Every exchanged key buffer equals the keys of the same batch scored with no process group."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(root / "tools" / "rccl_lane_check.py"), "--steps", "12", "--poses", "1000"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["backend"] == "nccl" and res["world_size"] == 1
+    assert res["keys_equal_no_process_group"] and res["exchanges_checked"] == 12
+    assert len(res["keys"]) == 5 and all(k != (2 ** 63 - 1) for k in res["keys"])

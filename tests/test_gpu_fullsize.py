@@ -169,20 +169,28 @@ def test_evaluate_select_keys_equal_evaluate_then_select(tier, monkeypatch):
     assert (keys != PCORE_KEY_NONE).sum().item() >= w.num_models // 2
 
 
+SWEEP_MESHES = {"proxies": ["003_cracker_box", "005_tomato_soup_can", "024_bowl"],
+                # scan-like irregular meshes (synthetic.scan_mesh: ~20-24 k triangles, warped density, slivers,
+                # T-junctions, shuffled faces; scan_shell is open) beside the box proxy
+                "scan": ["scan_blob", "scan_shell", "003_cracker_box"]}
+
+
+@pytest.mark.parametrize("meshes", ["proxies", "scan"])
 @pytest.mark.parametrize("cam,tier", [("640", "auto"), ("640", "0"), ("640", "99"), ("640", "tcap64"),
                                       ("1280", "auto")])
-def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, monkeypatch):
+def test_random_pose_sweep_bit_exact_vs_oracle(cam, tier, meshes, monkeypatch):
     """3,000 random poses of three models (random rotations; behind, across and near the camera plane, off
     screen, far): every pose's costs bit-exact against the oracle with the tile tier chosen from the window
     histogram, forced to the smallest tier, to a 64-sample tile (nearly every pose is scored in chunks of the
     tile, each a full raster clipped to the chunk) and to the whole image -- the conservative pose windows never drop a fragment; at 640x480 and at C5's 1280x720.
-    For 200 of them the sampled z-buffers equal the full-frame render."""
+    For 200 of them the sampled z-buffers equal the full-frame render.  Both on the regularly tessellated YCB
+    proxies and on the scan-like irregular meshes."""
     from perception_amd.model import init_from_eigen_batch
     if tier == "tcap64":
         monkeypatch.setenv("PCORE_FUSED_TCAP", "64")  # nearly every pose is scored in chunks of the tile
     elif tier != "auto":
         monkeypatch.setenv("PCORE_FUSED_TIER", tier)
-    w = workloads.build(names=["003_cracker_box", "005_tomato_soup_can", "024_bowl"], poses_per_model=10,
+    w = workloads.build(names=SWEEP_MESHES[meshes], poses_per_model=10,
                         cam=syn.CAM_640 if cam == "640" else syn.CAM_1280)
     rng = np.random.default_rng(11)
     n = 3000
@@ -248,6 +256,33 @@ def test_c3_scene_icp_sweep_bit_exact_vs_oracle(window):
     assert np.array_equal(_bits(oc.cpu().numpy()), _bits(ooc))
     assert np.array_equal(_bits(df.cpu().numpy()), _bits(odf))
     assert oit.max() == 150 and oit.min() < 20  # converging and non-converging poses both present
+
+
+def test_scan_mesh_icp_bit_exact_vs_oracle():
+    """GICP on the scan-like irregular meshes: 1,200 candidates of a scene of scan_blob, scan_shell and the box
+    proxy, refined and re-scored on the GPU, equal the oracle's adjusted poses, iteration counts and costs bit for bit
+    (spec cycle exit on)."""
+    names = SWEEP_MESHES["scan"]
+    w = workloads.build(names=names, poses_per_model=400)
+    adj, iters, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                 stride=w.stride)
+    sc = w.scene
+    oxyz, ls, le = _label_ranges(w)
+    cov = np.zeros((len(oxyz), 6))
+    for L in range(len(ls)):
+        if le[L] > ls[L]:
+            cov[ls[L]:le[L]] = oracle.covariances(oxyz[ls[L]:le[L]])
+    pm = w.pose_model.cpu().numpy()
+    oadj, oit, orc, ooc, odf = oracle.evaluate_icp(
+        sc.bank.tris, sc.bank.tris_model_count, w.poses.cpu().numpy(), pm, pm, sc.width, sc.height, sc.proj,
+        sc.src_depth_cm, sc.mask, 1.0, w.stride, sc.cx, sc.cy, sc.fx, sc.fy, 100.0, oxyz, cov, ls, le,
+        w.pose_obs_total.cpu().numpy(), 2, True, 0.01)
+    assert np.array_equal(iters.cpu().numpy(), oit)
+    assert np.array_equal(_bits(adj.cpu().numpy()), _bits(oadj))
+    assert np.array_equal(_bits(rc.cpu().numpy()), _bits(orc))
+    assert np.array_equal(_bits(oc.cpu().numpy()), _bits(ooc))
+    assert np.array_equal(_bits(df.cpu().numpy()), _bits(odf))
+    assert (rc.cpu().numpy() >= 0).sum() > 600
 
 
 # ---- true per-GPU sizes of C3, C4 and C5 (BASELINE.json configs[2..4]) ----------------------------------

@@ -165,7 +165,7 @@ def test_read_poses_txt_cached_settled_file_skips_the_read(tmp_path, monkeypatch
     pio.write_poses_txt(p, rows)
     st = os.stat(p)
     real_fs_now = pio._fs_now_ns
-    monkeypatch.setattr(pio, "_fs_now_ns", lambda d: real_fs_now(d) + 10 * pio._SETTLED_NS)  # pretend the file is old
+    monkeypatch.setattr(pio, "_fs_now_ns", lambda d, dev=None: real_fs_now(d, dev) + 10 * pio._SETTLED_NS)  # old file
     a = pio.read_poses_txt_cached(p)
     digests = []
     monkeypatch.setattr(pio, "_content_digest", lambda d: digests.append(1) or b"x" * 16)
@@ -180,13 +180,14 @@ def test_read_poses_txt_cached_settled_file_skips_the_read(tmp_path, monkeypatch
 
 
 def test_read_poses_txt_cached_settles_on_the_file_systems_clock(tmp_path, monkeypatch):
-    """"settled" is judged on the file system's clock (a temporary file's ctime beside the file), so a
-    local clock far ahead of the server's (NFS) does not make a fresh file look settled; a directory where no
-    temporary file can be created never settles (every read hashes)."""
+    """"settled" is judged on the file system's clock (this host's plus an offset measured with a
+    temporary file beside the file), so a local clock far ahead of the server's (NFS) does not make a fresh file look
+    settled -- the step of the local clock is seen and the offset measured again."""
     from perception_amd import io as pio
     import time
     p = str(tmp_path / "poses.txt")
     pio.write_poses_txt(p, np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]]))
+    pio._fs_now_ns(str(tmp_path))  # offset measured before the local clock steps
     real_ns = time.time_ns
     monkeypatch.setattr(pio.time, "time_ns", lambda: real_ns() + 100 * pio._SETTLED_NS)  # local clock far ahead
     a = pio.read_poses_txt_cached(p)
@@ -196,9 +197,42 @@ def test_read_poses_txt_cached_settles_on_the_file_systems_clock(tmp_path, monke
     assert pio.read_poses_txt_cached(p) is a and digests  # fresh on the file system's clock: read and hashed again
     fs_now = pio._fs_now_ns(str(tmp_path))
     assert fs_now is not None and abs(fs_now - real_ns()) < 60 * 10**9
-    monkeypatch.setattr(pio, "_fs_now_ns", lambda d: None)  # no temporary file possible
-    digests.clear()
+
+
+def test_fs_clock_offset_is_measured_once_per_device(tmp_path, monkeypatch):
+    """one temporary file per device (and per 10 minutes), not one per read of a fresh file."""
+    from perception_amd import io as pio
+    calls = []
+    real = pio._fs_clock_offset
+    monkeypatch.setattr(pio, "_fs_clock_offset", lambda d: calls.append(d) or real(d))
+    pio._FS_CLOCK.clear()
+    p = str(tmp_path / "poses.txt")
+    pio.write_poses_txt(p, np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]]))
+    for _ in range(5):
+        pio._POSES_STAT.clear()
+        pio.read_poses_txt_cached(p)
+    assert len(calls) == 1
+
+
+def test_read_only_directory_settles_on_the_local_clock(tmp_path, monkeypatch):
+    """where no temporary file can be created (a read-only data set) a file settles on this host's clock
+    after 60 s instead of never (every search re-read and re-hashed every poses.txt)."""
+    from perception_amd import io as pio
+    import time
+    p = str(tmp_path / "poses.txt")
+    pio.write_poses_txt(p, np.array([[0.1, 0.2, 0.3, 0.0, 0.0, 0.0, 1.0]]))
+    monkeypatch.setattr(pio, "_fs_clock_offset", lambda d: None)  # no temporary file possible
+    pio._FS_CLOCK.clear()
+    pio._POSES_STAT.clear()
+    digests = []
+    real_digest = pio._content_digest
+    monkeypatch.setattr(pio, "_content_digest", lambda d: digests.append(1) or real_digest(d))
+    pio.read_poses_txt_cached(p)
+    pio.read_poses_txt_cached(p)
+    assert len(digests) == 2  # fresh: hashed every time
+    real_ns = time.time_ns
+    monkeypatch.setattr(pio.time, "time_ns", lambda: real_ns() + 2 * pio._SETTLED_LOCAL_NS)  # a minute later
     pio._POSES_STAT.clear()
     pio.read_poses_txt_cached(p)
     pio.read_poses_txt_cached(p)
-    assert len(digests) == 2
+    assert len(digests) == 3  # settled after the first of these reads

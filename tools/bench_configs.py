@@ -8,6 +8,7 @@ multi-GPU configs).  Prints one JSON line per config.  Not the driver's bench (b
   C3  5 objects, 50k poses, render + GICP + re-render + score, 640x480 (+ argmin vs GT)
   C4  21 objects, 200k poses over 8 GPUs -> 25k poses per GPU, render + score
   C5  1 mesh, 1M poses at 1280x720 over 8 GPUs -> 125k poses per GPU, render + score
+  C2scan_blob / C2scan_shell  C2 on a scan-like irregular mesh; C3scan  C3's flow on two scan meshes + the box
 """
 import argparse
 import json
@@ -66,7 +67,7 @@ def run(name, names, per_model, cam, icp, steps, warmup):
     dt = timed(step, steps, warmup)
     cost, idx = decode_keys(keys)
     res = {"config": name, "poses": n, "models": w.num_models, "width": w.scene.width, "height": w.scene.height,
-           "icp": icp, "s_per_step": dt, "poses_per_s": n / dt,
+           "triangles": [int(c) for c in w.scene.bank.tris_model_count], "icp": icp, "s_per_step": dt, "poses_per_s": n / dt,
            "argmin_index": [int(i) for i in idx], "gt_index": [int(i) for i in w.gt_index],
            "argmin_cost": [int(c) for c in cost]}
     if icp:
@@ -170,6 +171,13 @@ def main():
         run("C4/8", list(syn.YCB_PROXIES), int(25000 / 21 * sc), syn.CAM_640, False, a.steps, a.warmup)
     if "C5" in sel:
         run("C5/8", ["003_cracker_box"], int(125000 * sc), syn.CAM_1280, False, a.steps, a.warmup)
+    # the scan-like irregular meshes (synthetic.scan_mesh) in C2's and C3's shape
+    for nm in ("scan_blob", "scan_shell"):
+        if "C2" + nm in sel:
+            run("C2:" + nm, [nm], int(10000 * sc), syn.CAM_640, False, a.steps, a.warmup)
+    if "C3scan" in sel:
+        run("C3:scan", ["scan_blob", "scan_shell", "003_cracker_box"], int(10000 * sc), syn.CAM_640, True, a.steps,
+            a.warmup)
 
 
 if __name__ == "__main__":

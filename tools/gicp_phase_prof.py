@@ -36,7 +36,8 @@ def main():
     torch.cuda.synchronize()
     fn(buf, 0)
     it = iters.cpu().numpy()
-    total = int(it.sum())  # one linearisation + one LM iteration per counted iteration
+    # one linearisation + one LM iteration per executed iteration (a cycle exit reports 150 but runs fewer)
+    total = int(w.core.stats()["gicp_iterations_run"])
     names = ["search", "contributions", "reduction", "LM iteration", "  solves", "  se3 + compose", "  trial errors",
              "  decisions"]
     print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())

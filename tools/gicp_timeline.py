@@ -39,7 +39,11 @@ def main():
         torch.cuda.synchronize()
         assert fn(poses.ctypes.data, waves.ctypes.data, nw.ctypes.data) == 0
     n = int(w.poses.shape[0])
-    its = it.cpu().numpy()
+    run = np.zeros(K_POSES, np.int32)
+    lib.pcore_debug_gicp_timeline_run.argtypes = [ctypes.c_void_p]
+    assert lib.pcore_debug_gicp_timeline_run(run.ctypes.data) == 0
+    its_reported = it.cpu().numpy()
+    its = run[:n].copy()  # the iterations each pose executed (a cycle exit reports 150 but runs fewer)
     ps = poses[:2 * n].reshape(n, 2).astype(np.int64)
     nwv = int(nw[0])
     ws = waves[:2 * nwv].reshape(nwv, 2).astype(np.int64)
@@ -65,7 +69,9 @@ def main():
            "us_per_iteration_mean": float((pose_us[its > 0] / its[its > 0]).mean()),
            "busy_below_90pct_us": float((busy < 0.9 * busy.max()).sum()),
            "busy_below_50pct_us": float((busy < 0.5 * busy.max()).sum()),
-           "iterations_mean": float(its.mean())}
+           "iterations_mean": float(its.mean()), "iterations_reported_mean": float(its_reported.mean()),
+           "tail_pose_reported_at_150": int((its_reported[tail_mask] >= 150).sum()),
+           "poses_run_150": int((its >= 150).sum())}
     # the longest poses: duration, iterations and source points (the stride-8 samples the cloud keeps)
     s8 = w.stride
     hs, ws8 = (w.scene.height + s8 - 1) // s8, w.scene.width // s8
@@ -74,7 +80,8 @@ def main():
     ns = (dbg > 0).sum(dim=(1, 2)).cpu().numpy()
     nt = w.pose_obs_total.cpu().numpy().astype(np.int64)  # targets of the pose's label segment
     top = np.argsort(-pose_us)[:12]
-    res["longest_poses"] = [{"pose": int(i), "us": float(pose_us[i]), "iterations": int(its[i]), "points": int(ns[i]),
+    res["longest_poses"] = [{"pose": int(i), "us": float(pose_us[i]), "iterations": int(its[i]),
+                             "iterations_reported": int(its_reported[i]), "points": int(ns[i]),
                              "targets": int(nt[i]), "start_us": float((ps[i, 0] - t0) / 100.0)} for i in top]
     res["poses_over_512_points"] = int((ns > 512).sum())
     res["points_mean"] = float(ns.mean())
