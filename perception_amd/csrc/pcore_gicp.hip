@@ -780,9 +780,15 @@ __device__ __forceinline__ void xform_identity(Xform& x) {
 #define PCORE_GICP_LDS_ROUNDS 2
 #endif
 constexpr int kLdsPts = 64 * PCORE_GICP_LDS_ROUNDS;
+// the first rounds' source points in LDS as three floats (12 B: the cycle exit's 32-slot ring fits the wave's LDS
+// in the same 1,280-byte granules)
+struct Pt3 {
+    float x, y, z;
+};
+
 struct Round0 {
     double2 (*m)[kLdsPts];
-    float4* s;
+    Pt3* s;
     float4* t;
 };
 
@@ -834,7 +840,7 @@ __device__ __forceinline__ void linearize_round(const Xform& x, const float (&Rf
             r0.m[0][i] = make_double2(M6[0], M6[1]);
             r0.m[1][i] = make_double2(M6[2], M6[3]);
             r0.m[2][i] = make_double2(M6[4], M6[5]);
-            r0.s[i] = sp;
+            r0.s[i] = Pt3{sp.x, sp.y, sp.z};
             r0.t[i] = make_float4(tj.x, tj.y, tj.z, 1.0f);
         } else {
             double2* m2 = reinterpret_cast<double2*>(mah + (size_t)6 * i);
@@ -883,7 +889,7 @@ __device__ __forceinline__ int lm_iteration(const double* sys, Xform& x, double&
         GPROF_TD(p2, xi.t[2]);
         GPROF_ADD(5, p1, p2);
         // the error at x_i (FastGICP::compute_error: this iteration's correspondences and Mahalanobis matrices)
-        auto err_add = [&](const float4& sp, const float4& tj, const double (&M6)[6], double y) {
+        auto err_add = [&](const auto& sp, const float4& tj, const double (&M6)[6], double y) {
             double q[3];
             gicpm::transform_point(xi.R, xi.t, (double)sp.x, (double)sp.y, (double)sp.z, q);
             const double e[3] = {(double)tj.x - q[0], (double)tj.y - q[1], (double)tj.z - q[2]};
@@ -985,10 +991,14 @@ __device__ __forceinline__ unsigned ring_match16(unsigned b0, unsigned b1, unsig
     return (unsigned)eq;
 }
 
-// The cycle exit (pcore_gicp_math.h cycle_update) of one wave: the last 16 float transforms T_f(j) in slot
-// (j - 1) % 16 of an LDS ring, the slots written so far and the run counters.
+// The cycle exit (pcore_gicp_math.h cycle_update) of one wave: the last 32 float transforms T_f(j) in slot
+// (j - 1) % 32 of an LDS ring of two 16-slot banks (words 0..2: slots 0..15, words 3..5: slots 16..31, each bank laid out
+// as xf_lane_words), the slots written so far and the run counters.
+static_assert(gicpm::kCycleLags == 32, "CycleExit holds 32 slots");
+constexpr int kCycleRingWords = 6 * 64;
+
 struct CycleExit {
-    unsigned* ring;  // 3 x 64 words, this wave's
+    unsigned* ring;  // kCycleRingWords, this wave's
     unsigned written;
     gicpm::CycleRun run;
 
@@ -1013,31 +1023,35 @@ struct CycleExit {
         xform_float(x, Rf, tf);
         unsigned b0, b1, b2;
         xf_lane_words(Rf, tf, lane & 3, b0, b1, b2);
-        const int cur = iters + 1, c0 = (cur - 1) & 15;
-        const unsigned hv0 = ring[lane], hv1 = ring[64 + lane], hv2 = ring[128 + lane];
-        const unsigned m = ring_match16(b0, b1, b2, hv0, hv1, hv2) & written;
-        // lag q lives in slot (c0 - q) % 16: in the doubled mask at c0 + 16 - q, so the smallest lag is the highest bit
-        const unsigned t = ((m | (m << 16)) >> c0) & 0xffffu;
-        const int p = t ? 16 - (31 - __builtin_clz(t)) : 0;
-        if ((lane >> 2) == c0) {
-            ring[lane] = b0;
-            ring[64 + lane] = b1;
-            ring[128 + lane] = b2;
+        const int cur = iters + 1, c0 = (cur - 1) & 31, bank = c0 >> 4;
+        const unsigned m0 = ring_match16(b0, b1, b2, ring[lane], ring[64 + lane], ring[128 + lane]);
+        const unsigned m1 = ring_match16(b0, b1, b2, ring[192 + lane], ring[256 + lane], ring[320 + lane]);
+        const unsigned m = (m0 | (m1 << 16)) & written;
+        // lag q lives in slot (c0 - q) % 32: in the doubled mask at c0 + 32 - q, so the smallest lag is the highest bit
+        const unsigned long long mm = (unsigned long long)m | ((unsigned long long)m << 32);
+        const unsigned t = (unsigned)(mm >> c0);
+        const int p = t ? 32 - (31 - __builtin_clz(t)) : 0;
+        if ((lane >> 2) == (c0 & 15)) {
+            unsigned* w = ring + 192 * bank + lane;
+            w[0] = b0;
+            w[64] = b1;
+            w[128] = b2;
         }
         written |= 1u << c0;
         if (!gicpm::cycle_update(run, p, inert, window)) return -1;
-        return (gicpm::cycle_member(cur, p, max_iter) - 1) & 15;
+        return (gicpm::cycle_member(cur, p, max_iter) - 1) & 31;
     }
 
     // the float transform of ring slot s as the pose's result (after the loop: x is written back, not iterated on; the
     // ring was written by the whole wave, read here by every lane)
     __device__ __forceinline__ void member(int s, Xform& x) {
         wave_lds_sync();
+        const unsigned* w = ring + 192 * (s >> 4) + 4 * (s & 15);
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
             for (int v = 0; v < 3; v++) {
-                const double f = (double)__builtin_bit_cast(float, ring[64 * v + 4 * s + r]);
+                const double f = (double)__builtin_bit_cast(float, w[64 * v + r]);
                 if (r < 3) x.R[r][v] = f;
                 else x.t[v] = f;
             }
@@ -1106,11 +1120,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_G
 gicp_kernel(GicpArgs g, int num_poses) {
     __shared__ double sRed[gicpm::kTerms];
     __shared__ double2 sM0[3][kLdsPts];
-    __shared__ float4 sS0[kLdsPts], sT0[kLdsPts];
+    __shared__ Pt3 sS0[kLdsPts];
+    __shared__ float4 sT0[kLdsPts];
     __shared__ int sPose;
     __shared__ double sSe3[4 * gicpm::kSe3Terms];  // se3_exp's series coefficients, read at their use
     __shared__ unsigned sHist[3 * 64];               // the correspondence history's float transforms (below)
-    __shared__ unsigned sCyc[3 * 64];                // the cycle exit's last 16 float transforms (CycleExit)
+    __shared__ unsigned sCyc[kCycleRingWords];       // the cycle exit's last 32 float transforms (CycleExit)
     const int lane = threadIdx.x;
     const Round0 r0{sM0, sS0, sT0};
     if (lane < 4 * gicpm::kSe3Terms) sSe3[lane] = gicpm::kSe3Coef[lane];
@@ -1292,11 +1307,12 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
     extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
     __shared__ double sRed[gicpm::kTerms];
     __shared__ double2 sM0[3][kLdsPts];
-    __shared__ float4 sS0[kLdsPts], sT0[kLdsPts];
+    __shared__ Pt3 sS0[kLdsPts];
+    __shared__ float4 sT0[kLdsPts];
     __shared__ double sX[12];
     __shared__ int sPose, sFlag;
     __shared__ double sSe3[4 * gicpm::kSe3Terms];
-    __shared__ unsigned sCyc[3 * 64];  // wave 0's cycle exit ring
+    __shared__ unsigned sCyc[kCycleRingWords];  // wave 0's cycle exit ring
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const Round0 r0{sM0, sS0, sT0};  // wave 0's
     if (tid < 4 * gicpm::kSe3Terms) sSe3[tid] = gicpm::kSe3Coef[tid];

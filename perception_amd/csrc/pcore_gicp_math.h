@@ -501,8 +501,8 @@ PCORE_UNROLL
 // p > 0 and the last W steps are inert, the pose stops: it reports max_iter iterations and the transform T_f(j') of
 // the cycle member j' = max_iter + 1 (mod p) among its last p iterations -- the float transform the remaining
 // iterations would end on while the cycle holds.  W = 0 runs the iterations out (fast_gicp).
-constexpr int kCycleLags = 16;
-constexpr int kCycleWindow = 8;  // the spec's W (tools/cycle_exit_sim.py: 2,000 C3 candidates, 706 exits)
+constexpr int kCycleLags = 32;
+constexpr int kCycleWindow = 8;  // the spec's W (tools/cycle_exit_sim.py: 2,000 C3 candidates, 766 of 810 capped exit)
 
 struct CycleRun {
     int lag, run, okrun;

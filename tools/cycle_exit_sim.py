@@ -24,7 +24,7 @@ from tests.helpers import SceneCase  # noqa: E402
 
 C3_NAMES = ("003_cracker_box", "004_sugar_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can")
 MAX_ITER = 150
-LAGS = 16
+LAGS = 32  # pcore_gicp_math.h kCycleLags
 
 
 def candidates(per_object, seed):
@@ -44,7 +44,7 @@ def candidates(per_object, seed):
         yield xyz, oracle.covariances(xyz), tgt, seg[lab]
 
 
-def simulate(tr, it, W, need_inert=True, need_rho=True):
+def simulate(tr, it, W, need_inert=True, need_rho=True, lags=LAGS):
     """(exit iteration or 0, predicted final float transform bits (12,) or None)"""
     X = tr[:, :12].astype(np.float32).view(np.uint32)  # float(x_k), k = 1..it (row k - 1)
     ident = np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0], np.float32).view(np.uint32)
@@ -60,7 +60,7 @@ def simulate(tr, it, W, need_inert=True, need_rho=True):
     for k in range(1, it + 1):  # top of iteration k: T_f(k) known, steps 1..k-1 done
         okrun = okrun + 1 if (k >= 2 and ok[k - 2]) else 0
         p = 0
-        for q in range(1, min(LAGS, k - 1) + 1):
+        for q in range(1, min(lags, k - 1) + 1):
             if np.array_equal(Tf[k - 1], Tf[k - 1 - q]):
                 p = q
                 break
@@ -86,11 +86,13 @@ def main():
     iters = np.array([t[1] for t in traces])
     res = {"candidates": len(traces), "at_150": int((iters >= MAX_ITER).sum()), "iterations": int(iters.sum()),
            "variants": []}
-    for W, inert, rhoc in [(2, True, True), (3, True, True), (4, True, True), (6, True, True), (8, True, True),
-                           (12, True, True), (4, False, True), (4, False, False), (8, False, False)]:
+    for W, inert, rhoc, lags in [(2, True, True, 16), (3, True, True, 16), (4, True, True, 16), (6, True, True, 16),
+                                 (8, True, True, 16), (12, True, True, 16), (4, False, True, 16), (4, False, False, 16),
+                                 (8, False, False, 16), (8, True, True, 32), (8, True, True, 64), (16, True, True, 32),
+                                 (16, True, True, 64)]:
         n_exit = saved = wrong_T = wrong_it = 0
         for T, it, tr in traces:
-            k, pred = simulate(tr, it, W, inert, rhoc)
+            k, pred = simulate(tr, it, W, inert, rhoc, lags)
             if not k:
                 continue
             n_exit += 1
@@ -100,7 +102,7 @@ def main():
                 wrong_it += 1
             if not np.array_equal(final, pred):
                 wrong_T += 1
-        v = {"W": W, "need_inert": inert, "need_rho_half": rhoc, "exits": n_exit, "iterations_saved": int(saved),
+        v = {"W": W, "lags": lags, "need_inert": inert, "need_rho_half": rhoc, "exits": n_exit, "iterations_saved": int(saved),
              "saved_frac": saved / max(1, int(iters.sum())), "wrong_transform": wrong_T, "wrong_iterations": wrong_it}
         res["variants"].append(v)
         print(v, flush=True)
