@@ -281,6 +281,12 @@ def main():
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))  # this process only waits for its N rank children
+    # (a rank) stdout carries only the JSON line: anything else written to fd 1 (RCCL prints its version banner there when
+    # the communicator starts) goes to stderr; the line itself goes to the saved descriptor
+    global _JSON_FD
+    _JSON_FD = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(env_world or "1")
     if world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU with matching "
@@ -522,8 +528,10 @@ def main():
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
         line["cpu_reference_path"] = cpu_reference_path(args.ref_cpu_seconds)
-    print(json.dumps(line), flush=True)
+    os.write(_JSON_FD, (json.dumps(line) + "\n").encode())
 
+
+_JSON_FD = 1
 
 if __name__ == "__main__":
     main()

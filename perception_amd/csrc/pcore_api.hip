@@ -985,7 +985,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     const bool use_hist = !getenv("PCORE_GICP_NO_HIST");  // A/B knob (same results)
     if (use_hist) HIPC(c, dev_reserve(c->icp_corr_hist, (size_t)chunk * kCorrHist * hist_cap));
     HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
-    HIPC(c, dev_reserve(c->icp_counter, 1));
+    HIPC(c, dev_reserve(c->icp_counter, 4));  // [0] one-wave queue, [1] heavy queue, [2] heavy poses
     HIPC(c, dev_reserve(c->icp_iter_stats, 4));
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
@@ -1032,6 +1032,14 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.rot_eps = ip->rotation_epsilon;
     g.trans_eps = ip->transformation_epsilon;
     g.work_counter = c->icp_counter.p;
+    g.heavy_counter = c->icp_counter.p + 1;
+    g.heavy_count = c->icp_counter.p + 2;
+    // heavy poses: source points x targets >= 60,000 (e.g. 211 points on a 285-target segment), at most 2 per CU;
+    // PCORE_GICP_HEAVY_COST / PCORE_GICP_HEAVY_MAX for A/B (0: none)
+    g.heavy_cost = 60000;
+    g.heavy_max = 2 * std::max(1, c->dinfo.num_cus);
+    if (const char* e = getenv("PCORE_GICP_HEAVY_COST")) g.heavy_cost = atoll(e);
+    if (const char* e = getenv("PCORE_GICP_HEAVY_MAX")) g.heavy_max = atoi(e);
     g.cycle_window = ip->cycle_exit_window;
     g.iter_stats = c->icp_iter_stats.p;
     g.tgt_quads = c->tgt_quads.p;
@@ -1062,12 +1070,20 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         a.tcap = fused_tier_samples(0, a.ws, a.hs, 0, false, c->dinfo);
         if (const char* e = getenv("PCORE_FUSED_TCAP")) a.tcap = std::min(std::max(atoi(e), 1), a.ws * a.hs);
         if (a.tcap <= 0) a.tcap = a.ws * a.hs;
-        HIPC(c, launch_render_cloud(a, s));
+        // the source covariances in a launch of their own, or (PCORE_COV_FOLD=1, A/B) in render_cloud's launch; either
+        // way bit-identical (pcore_cov.h).  Folded, the C3 step took 13.70 / 13.75 ms against 12.74 / 12.95 ms
+        // (profiles/r06g/): render_cloud's workgroups hold their raster LDS (6 per CU) through the k-NN rounds, where
+        // the covariance launch runs 32 one-wave workgroups per CU.
+        const bool fold = k == 10 && getenv("PCORE_COV_FOLD") && atoi(getenv("PCORE_COV_FOLD")) == 1;
+        a.cloud_cov = fold ? c->icp_cov.p : nullptr;
         hipEvent_t* ev = timed ? c->icp_ev.data() + 3 * c->icp_ev_used : nullptr;
-        if (ev) HIPC(c, hipEventRecord(ev[0], s));
-        HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
+        if (ev && fold) HIPC(c, hipEventRecord(ev[0], s));  // icp_runtime then spans the cloud + covariance launch
+        HIPC(c, launch_render_cloud(a, s));
+        if (ev && !fold) HIPC(c, hipEventRecord(ev[0], s));
+        if (!fold) HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
         g.pose_base = base;
         g.pose_order = nullptr;
+        HIPC(c, hipMemsetAsync(g.heavy_count, 0, sizeof(int32_t), s));
         if (!getenv("PCORE_GICP_INDEX_ORDER")) {  // A/B knob: the queue in index order
             HIPC(c, launch_gicp_order(g, n, c->icp_order_keys.p, c->icp_order_keys.p + chunk, c->icp_order_idx.p,
                                       c->icp_order_idx.p + chunk, c->icp_order_temp.p, order_temp, s));

@@ -1,0 +1,200 @@
+// pcore_cov.h -- the GICP covariances of a point segment (fast_gicp's k-NN covariances with PLANE regularisation;
+// DESIGN.md section 5): one wave per round of 64 query points, brute-force k-NN over the segment with candidates
+// staged through a 64-point LDS tile, double mean / covariance in list order, 6-sweep Jacobi, PLANE regularisation.
+// Shared by covariance_kernel (pcore_gicp.hip: one wave per segment) and render_cloud_kernel (pcore_kernels.hip: the
+// rendered clouds' covariances in the launch that produced them, its four waves taking the query rounds in turn).
+// Bit-identical to the oracle's covariance_one (tests/test_gpu_covariances.py, the GICP parity tests).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#ifndef PCORE_COV_SKIP
+#define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
+#endif
+
+namespace pcore {
+namespace {
+
+constexpr double kPlaneScale = 1.0 - 1e-3;
+
+// LDS writes by some lanes of a wave visible to all its lanes (no block barrier: waves are independent)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
+    const float dx = ax - bx, dy = ay - by, dz = az - bz;
+    return dx * dx + dy * dy + dz * dz;
+}
+
+// Jacobi (6 cyclic sweeps) + PLANE regularisation, same operation order as orc plane_regularize.
+__device__ void plane_regularize(const double c[6], double out[6]) {
+    double A[3][3] = {{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}};
+    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+#pragma unroll 1
+    for (int sweep = 0; sweep < 6; sweep++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const int p = r < 2 ? 0 : 1, q = r == 0 ? 1 : 2, o = 3 - p - q;
+            const double apq = A[p][q];
+            if (apq == 0.0) continue;
+            const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+            if (theta < 0.0) t = -t;
+            const double cc = 1.0 / sqrt(t * t + 1.0);
+            const double ss = t * cc;
+            const double app = A[p][p], aqq = A[q][q];
+            A[p][p] = app - t * apq;
+            A[q][q] = aqq + t * apq;
+            A[p][q] = 0.0;
+            A[q][p] = 0.0;
+            const double aop = A[o][p], aoq = A[o][q];
+            A[o][p] = cc * aop - ss * aoq;
+            A[p][o] = A[o][p];
+            A[o][q] = ss * aop + cc * aoq;
+            A[q][o] = A[o][q];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const double vkp = V[k][p], vkq = V[k][q];
+                V[k][p] = cc * vkp - ss * vkq;
+                V[k][q] = ss * vkp + cc * vkq;
+            }
+        }
+    // smallest eigenvalue's column, first on ties (selects, not a dynamic register index)
+    int m = 0;
+    double am = A[0][0];
+    if (A[1][1] < am) { m = 1; am = A[1][1]; }
+    if (A[2][2] < am) m = 2;
+    const double n0 = m == 0 ? V[0][0] : (m == 1 ? V[0][1] : V[0][2]);
+    const double n1 = m == 0 ? V[1][0] : (m == 1 ? V[1][1] : V[1][2]);
+    const double n2 = m == 0 ? V[2][0] : (m == 1 ? V[2][1] : V[2][2]);
+    out[0] = 1.0 - kPlaneScale * (n0 * n0);
+    out[1] = 0.0 - kPlaneScale * (n0 * n1);
+    out[2] = 0.0 - kPlaneScale * (n0 * n2);
+    out[3] = 1.0 - kPlaneScale * (n1 * n1);
+    out[4] = 0.0 - kPlaneScale * (n1 * n2);
+    out[5] = 1.0 - kPlaneScale * (n2 * n2);
+}
+
+
+// mean / covariance (double, list order) of the listed neighbours and PLANE regularisation (orc covariance_one)
+template <int KMAX>
+__device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[KMAX], int cnt, double* out6) {
+    double mx = 0.0, my = 0.0, mz = 0.0;
+#pragma unroll
+    for (int q = 0; q < KMAX; q++)
+        if (q < cnt) {
+            const float4 p = P[nb[q]];
+            mx += (double)p.x; my += (double)p.y; mz += (double)p.z;
+        }
+    const double kd = (double)cnt;
+    mx = mx / kd; my = my / kd; mz = mz / kd;
+    double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < KMAX; q++)
+        if (q < cnt) {
+            const float4 p = P[nb[q]];
+            const double dx = (double)p.x - mx, dy = (double)p.y - my, dz = (double)p.z - mz;
+            c6[0] += dx * dx; c6[1] += dx * dy; c6[2] += dx * dz;
+            c6[3] += dy * dy; c6[4] += dy * dz; c6[5] += dz * dz;
+        }
+#pragma unroll
+    for (int e = 0; e < 6; e++) c6[e] = c6[e] / kd;
+    double r6[6];
+#if PCORE_COV_SKIP & 1  // ablation timing only (wrong results): no eigen-decomposition / PLANE regularisation
+#pragma unroll
+    for (int e = 0; e < 6; e++) r6[e] = c6[e];
+#else
+    plane_regularize(c6, r6);
+#endif
+#pragma unroll
+    for (int e = 0; e < 6; e++) out6[e] = r6[e];
+}
+
+constexpr int kCovLanes = 64;
+
+// One round of 64 queries i0 + lane of the segment P[0, n): k nearest (distance, index) in the scan's order, their
+// covariance into C[6 i].  `tile`: this wave's kCovLanes points of LDS.
+// KFIXED: k == KMAX known at compile time (GICP's k = 10): the list's last entry and every `q < k` test are static,
+// so the insertion is straight-line code; with a run-time k the compiler indexed nd[k - 1] through s_set_gpr_idx and
+// branched once per list entry.
+template <int KMAX, bool KFIXED>
+__device__ __forceinline__ void cov_knn_round(const float4* P, int n, int k_arg, int i0, int lane, float4* tile,
+                                              double* C) {
+    const int k = KFIXED ? KMAX : k_arg;
+    const int i = i0 + lane;
+    const float4 xi = i < n ? P[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float nd[KMAX];
+    int nb[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) { nd[q] = 0.0f; nb[q] = 0; }
+    int cnt = 0;
+    // the list holds a NaN distance (a non-finite point among the first k candidates): it is no longer sorted,
+    // and only the counting insertion below reproduces orc knn_self's placement
+    bool nan_list = false;
+    // insertion identical to orc knn_self: the new element starts at pos and bubbles down past entries with a
+    // strictly larger distance
+    auto insert_counting = [&](float d, int j) {
+        int pos;
+        if (cnt < k) pos = cnt;
+        else if (d < nd[k - 1]) pos = k - 1;
+        else return;
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < KMAX; q++) c += (q < pos && nd[q] > d) ? 1 : 0;
+        const int fin = pos - c;
+#pragma unroll
+        for (int q = KMAX - 1; q >= 1; q--)
+            if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
+#pragma unroll
+        for (int q = 0; q < KMAX; q++)
+            if (q == fin) { nd[q] = d; nb[q] = j; }
+        if (cnt < k) cnt++;
+        nan_list = nan_list || d != d;
+    };
+#if PCORE_COV_SKIP & 2  // ablation timing only (wrong results): the first k points instead of the k-NN search
+    for (int q = 0; q < KMAX; q++)
+        if (q < k && q < n) { nb[q] = q; cnt = q + 1; }
+    for (int j0 = n; j0 < n; j0 += kCovLanes) {
+#else
+    for (int j0 = 0; j0 < n; j0 += kCovLanes) {
+#endif
+        wave_lds_sync();  // the previous tile is read
+        if (j0 + lane < n) tile[lane] = P[j0 + lane];
+        wave_lds_sync();
+        const int jn = min(kCovLanes, n - j0);
+        float4 xn = tile[0];  // (jn >= 1 here) the next candidate's read is issued before this one's insertion
+        for (int jj = 0; jj < jn; jj++) {
+            const float4 xj = xn;
+            xn = tile[jj + 1 < jn ? jj + 1 : jj];
+            const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
+            const int j = j0 + jj;
+            if (cnt < k || nan_list) {  // the first k candidates (every lane at once), or a NaN list
+                insert_counting(d, j);
+            } else if (d < nd[k - 1]) {
+                // a full, sorted list (no NaN: one could only enter among the first k): the counting insertion's
+                // result in one pass -- the entries greater than d (a suffix, the list being sorted) move right by
+                // one and d takes the first of their slots (d < nd[k - 1], so there is one).  Written from the
+                // end, each entry reads its left neighbour before that one is overwritten: no temporaries.
+                bool g[KMAX];
+#pragma unroll
+                for (int q = 0; q < KMAX; q++) g[q] = q < k && nd[q] > d;
+#pragma unroll
+                for (int q = KMAX - 1; q >= 1; q--) {
+                    if (q < k) {
+                        nd[q] = g[q - 1] ? nd[q - 1] : (g[q] ? d : nd[q]);
+                        nb[q] = g[q - 1] ? nb[q - 1] : (g[q] ? j : nb[q]);
+                    }
+                }
+                nd[0] = g[0] ? d : nd[0];
+                nb[0] = g[0] ? j : nb[0];
+            }
+        }
+    }
+    if (i < n) cov_from_list<KMAX>(P, nb, cnt, C + (size_t)6 * i);
+}
+
+}  // namespace
+}  // namespace pcore

@@ -20,6 +20,7 @@
 #include "pcore_internal.h"
 
 #include <hipcub/hipcub.hpp>
+#include "pcore_cov.h"
 #include "pcore_gicp_math.h"
 
 #include <algorithm>
@@ -34,9 +35,6 @@ namespace pcore {
 namespace {
 
 constexpr int kGThreads = 256;
-#ifndef PCORE_COV_SKIP
-#define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
-#endif
 constexpr int kMaxK = 16;
 // Build with -DPCORE_GICP_PROFILE to accumulate per-phase shader clocks of gicp_kernel (tools only):
 // [0] correspondence search, [1] contributions (+ M stores), [2] wave reduction, [3] LM iteration, which splits into [4] damped
@@ -91,15 +89,6 @@ extern "C" int pcore_debug_gicp_timeline(unsigned long long* poses, unsigned lon
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-constexpr double kPlaneScale = 1.0 - 1e-3;
-
-// LDS writes by some lanes of a wave visible to all its lanes (no block barrier: waves are independent)
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // se3_exp's series coefficients as the kernels read them: an LDS copy through an address-space-3 pointer offset by an
 // opaque zero produced inside the iteration loop, so the loads cannot be hoisted out of it (as literal constants they
 // were hoisted into 64 VGPRs for the whole kernel; a generic pointer made them flat loads) but can be issued together
@@ -109,60 +98,6 @@ __device__ __forceinline__ int opaque_zero() {
     int z;
     asm volatile("s_mov_b32 %0, 0" : "=s"(z));
     return z;
-}
-
-__device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
-    const float dx = ax - bx, dy = ay - by, dz = az - bz;
-    return dx * dx + dy * dy + dz * dz;
-}
-
-// Jacobi (6 cyclic sweeps) + PLANE regularisation, same operation order as orc plane_regularize.
-__device__ void plane_regularize(const double c[6], double out[6]) {
-    double A[3][3] = {{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}};
-    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
-#pragma unroll 1
-    for (int sweep = 0; sweep < 6; sweep++)
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            const int p = r < 2 ? 0 : 1, q = r == 0 ? 1 : 2, o = 3 - p - q;
-            const double apq = A[p][q];
-            if (apq == 0.0) continue;
-            const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-            double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-            if (theta < 0.0) t = -t;
-            const double cc = 1.0 / sqrt(t * t + 1.0);
-            const double ss = t * cc;
-            const double app = A[p][p], aqq = A[q][q];
-            A[p][p] = app - t * apq;
-            A[q][q] = aqq + t * apq;
-            A[p][q] = 0.0;
-            A[q][p] = 0.0;
-            const double aop = A[o][p], aoq = A[o][q];
-            A[o][p] = cc * aop - ss * aoq;
-            A[p][o] = A[o][p];
-            A[o][q] = ss * aop + cc * aoq;
-            A[q][o] = A[o][q];
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const double vkp = V[k][p], vkq = V[k][q];
-                V[k][p] = cc * vkp - ss * vkq;
-                V[k][q] = ss * vkp + cc * vkq;
-            }
-        }
-    // smallest eigenvalue's column, first on ties (selects, not a dynamic register index)
-    int m = 0;
-    double am = A[0][0];
-    if (A[1][1] < am) { m = 1; am = A[1][1]; }
-    if (A[2][2] < am) m = 2;
-    const double n0 = m == 0 ? V[0][0] : (m == 1 ? V[0][1] : V[0][2]);
-    const double n1 = m == 0 ? V[1][0] : (m == 1 ? V[1][1] : V[1][2]);
-    const double n2 = m == 0 ? V[2][0] : (m == 1 ? V[2][1] : V[2][2]);
-    out[0] = 1.0 - kPlaneScale * (n0 * n0);
-    out[1] = 0.0 - kPlaneScale * (n0 * n1);
-    out[2] = 0.0 - kPlaneScale * (n0 * n2);
-    out[3] = 1.0 - kPlaneScale * (n1 * n1);
-    out[4] = 0.0 - kPlaneScale * (n1 * n2);
-    out[5] = 1.0 - kPlaneScale * (n2 * n2);
 }
 
 }  // namespace
@@ -269,137 +204,25 @@ __device__ __forceinline__ void knn_insert_lex(float (&nd)[KMAX], int (&nb)[KMAX
     if (cnt < k) cnt++;
 }
 
-// mean / covariance (double, list order) of the listed neighbours and PLANE regularisation (orc covariance_one)
-template <int KMAX>
-__device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[KMAX], int cnt, double* out6) {
-    double mx = 0.0, my = 0.0, mz = 0.0;
-#pragma unroll
-    for (int q = 0; q < KMAX; q++)
-        if (q < cnt) {
-            const float4 p = P[nb[q]];
-            mx += (double)p.x; my += (double)p.y; mz += (double)p.z;
-        }
-    const double kd = (double)cnt;
-    mx = mx / kd; my = my / kd; mz = mz / kd;
-    double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KMAX; q++)
-        if (q < cnt) {
-            const float4 p = P[nb[q]];
-            const double dx = (double)p.x - mx, dy = (double)p.y - my, dz = (double)p.z - mz;
-            c6[0] += dx * dx; c6[1] += dx * dy; c6[2] += dx * dz;
-            c6[3] += dy * dy; c6[4] += dy * dz; c6[5] += dz * dz;
-        }
-#pragma unroll
-    for (int e = 0; e < 6; e++) c6[e] = c6[e] / kd;
-    double r6[6];
-#if PCORE_COV_SKIP & 1  // ablation timing only (wrong results): no eigen-decomposition / PLANE regularisation
-#pragma unroll
-    for (int e = 0; e < 6; e++) r6[e] = c6[e];
-#else
-    plane_regularize(c6, r6);
-#endif
-#pragma unroll
-    for (int e = 0; e < 6; e++) out6[e] = r6[e];
-}
-
 // ------------------------------------------------------------------------------------------------
 // covariances
 // ------------------------------------------------------------------------------------------------
-// One wave per segment (a pose's rendered cloud or an observed label), one lane per point in rounds of 64; the
-// candidates j of the brute-force scan come through LDS in tiles of 64 points staged by the wave itself, in the
-// scan's order (a 256-thread workgroup per segment left two of its four waves idle on C3's ~111-point clouds).
+// One wave per segment (a pose's rendered cloud or an observed label), one lane per point in rounds of 64 (pcore_cov.h
+// cov_knn_round); a 256-thread workgroup per segment left two of its four waves idle on C3's ~111-point clouds.
 // C3: 2.65 -> 2.61 ms per 50 k clouds -- the time is the insertion block, which the wave runs whenever any lane
 // inserts (k ln(n / k) + k insertions per point), not the candidate loads.
-// KFIXED: k == KMAX known at compile time (GICP's k = 10): the list's last entry and every `q < k` test are static,
-// so the insertion is straight-line code; with a run-time k the compiler indexed nd[k - 1] through s_set_gpr_idx and
-// branched once per list entry.
-constexpr int kCovLanes = 64;
 template <int KMAX, bool KFIXED = false>
 __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts, const int32_t* seg_off,
                                                                const int32_t* seg_cnt, int seg_stride, int k_arg,
                                                                double* cov_out, int max_n) {
-    const int k = KFIXED ? KMAX : k_arg;
     __shared__ float4 tile[kCovLanes];
     const int sg = blockIdx.x;
     const int off = seg_off ? seg_off[sg] : sg * seg_stride;
     const int n = seg_cnt[sg];
     if (n > max_n) return;  // covariance_grid_kernel's segment
     const int lane = threadIdx.x;
-    const float4* P = pts + off;
-    double* C = cov_out + (size_t)6 * off;
-    for (int i0 = 0; i0 < n; i0 += kCovLanes) {
-        const int i = i0 + lane;
-        const float4 xi = i < n ? P[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        float nd[KMAX];
-        int nb[KMAX];
-#pragma unroll
-        for (int q = 0; q < KMAX; q++) { nd[q] = 0.0f; nb[q] = 0; }
-        int cnt = 0;
-        // the list holds a NaN distance (a non-finite point among the first k candidates): it is no longer sorted,
-        // and only the counting insertion below reproduces orc knn_self's placement
-        bool nan_list = false;
-        // insertion identical to orc knn_self: the new element starts at pos and bubbles down past entries with a
-        // strictly larger distance
-        auto insert_counting = [&](float d, int j) {
-            int pos;
-            if (cnt < k) pos = cnt;
-            else if (d < nd[k - 1]) pos = k - 1;
-            else return;
-            int c = 0;
-#pragma unroll
-            for (int q = 0; q < KMAX; q++) c += (q < pos && nd[q] > d) ? 1 : 0;
-            const int fin = pos - c;
-#pragma unroll
-            for (int q = KMAX - 1; q >= 1; q--)
-                if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
-#pragma unroll
-            for (int q = 0; q < KMAX; q++)
-                if (q == fin) { nd[q] = d; nb[q] = j; }
-            if (cnt < k) cnt++;
-            nan_list = nan_list || d != d;
-        };
-#if PCORE_COV_SKIP & 2  // ablation timing only (wrong results): the first k points instead of the k-NN search
-        for (int q = 0; q < KMAX; q++)
-            if (q < k && q < n) { nb[q] = q; cnt = q + 1; }
-        for (int j0 = n; j0 < n; j0 += kCovLanes) {
-#else
-        for (int j0 = 0; j0 < n; j0 += kCovLanes) {
-#endif
-            wave_lds_sync();  // the previous tile is read
-            if (j0 + lane < n) tile[lane] = P[j0 + lane];
-            wave_lds_sync();
-            const int jn = min(kCovLanes, n - j0);
-            float4 xn = tile[0];  // (jn >= 1 here) the next candidate's read is issued before this one's insertion
-            for (int jj = 0; jj < jn; jj++) {
-                const float4 xj = xn;
-                xn = tile[jj + 1 < jn ? jj + 1 : jj];
-                const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
-                const int j = j0 + jj;
-                if (cnt < k || nan_list) {  // the first k candidates (every lane at once), or a NaN list
-                    insert_counting(d, j);
-                } else if (d < nd[k - 1]) {
-                    // a full, sorted list (no NaN: one could only enter among the first k): the counting insertion's
-                    // result in one pass -- the entries greater than d (a suffix, the list being sorted) move right by
-                    // one and d takes the first of their slots (d < nd[k - 1], so there is one).  Written from the
-                    // end, each entry reads its left neighbour before that one is overwritten: no temporaries.
-                    bool g[KMAX];
-#pragma unroll
-                    for (int q = 0; q < KMAX; q++) g[q] = q < k && nd[q] > d;
-#pragma unroll
-                    for (int q = KMAX - 1; q >= 1; q--) {
-                        if (q < k) {
-                            nd[q] = g[q - 1] ? nd[q - 1] : (g[q] ? d : nd[q]);
-                            nb[q] = g[q - 1] ? nb[q - 1] : (g[q] ? j : nb[q]);
-                        }
-                    }
-                    nd[0] = g[0] ? d : nd[0];
-                    nb[0] = g[0] ? j : nb[0];
-                }
-            }
-        }
-        if (i < n) cov_from_list<KMAX>(P, nb, cnt, C + (size_t)6 * i);
-    }
+    for (int i0 = 0; i0 < n; i0 += kCovLanes)
+        cov_knn_round<KMAX, KFIXED>(pts + off, n, k_arg, i0, lane, tile, cov_out + (size_t)6 * off);
 }
 
 // Segments above kGridNNMin points: one thread per point, k-NN by the exact grid shell search
@@ -1104,6 +927,119 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
     return p;
 }
 
+constexpr int kCycleExited = 3;  // coop_pose's flag: wave 0's cycle exit stopped the pose (LmStatus + 1)
+
+// One pose by the NW waves of a workgroup (gicp_wide_kernel's poses; gicp_kernel's heavy poses): every wave searches
+// the iteration's correspondences of rounds r = wave (mod NW) into `corr`, then wave 0 adds the contributions and runs
+// the LM iteration exactly as the one-wave path does -- point i on lane i % 64, in point order -- so the refined pose
+// is bit-identical; x and the iteration's outcome reach the other waves through LDS (sX, sFlag).  `r0`, `sRed`, `ring`:
+// wave 0's LDS.  Every thread of the workgroup calls this; thread 0 writes the pose.
+template <bool GRID, int NW, typename Corr>
+__device__ __forceinline__ void coop_pose(const GicpArgs& g, const GicpPose& P, int wave, int lane, Corr corr,
+                                          double* sRed, const Round0& r0, const lds_cvd* se3c, unsigned* ring,
+                                          double* sX, int* sFlag GPROF_PARAM) {
+    constexpr int NT = 64 * NW;
+    const int tid = wave * 64 + lane;
+#ifdef PCORE_GICP_TIMELINE
+    const unsigned long long tl_p0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    LabelGrid G{};
+    if (GRID && P.use_grid) G = g.grids[P.seg];
+    Xform x;
+    xform_identity(x);
+    double lambda = -1.0;  // wave 0's
+    int iters = 0, iters_run = 0;
+    CycleExit cyc;  // wave 0's
+    cyc.ring = ring;
+    if (wave == 0) cyc.start(lane);
+    const bool run = P.ns > 0 && P.nt > 0;
+    for (int it = 0; run && it < g.max_iter; it++) {
+        iters++;
+        float Rf[3][3], tf[3];
+        xform_float(x, Rf, tf);
+        GPROF_T(t_w0);
+        // correspondences, all waves
+        for (int i0 = wave * 64; i0 < P.ns; i0 += NT) {
+            const int i = i0 + lane;
+            const bool act = i < P.ns;
+            const float4 sp = act ? P.src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float qf[3];
+            gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
+            int j = -1;
+            float best = INFINITY;
+            if (GRID && P.use_grid) {
+                if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
+            } else {
+                scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, j);
+            }
+            if (act) corr[i] = j;
+        }
+        __syncthreads();
+        GPROF_TD(t_w1, Rf[0][0]);
+        GPROF_ADD(0, t_w0, t_w1);
+        if (wave == 0) {
+            double acc[gicpm::kTerms];
+#pragma unroll
+            for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
+            for (int i0 = 0; i0 < P.ns; i0 += 64) {
+                const int i = i0 + lane;
+                linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i, P.use_grid, G, g, P.tquads,
+                                       P.nt, i < P.ns ? corr[i] : -1, nullptr, P.mah, r0, acc, false GPROF_ARG);
+            }
+            GPROF_TD(t_w2, acc[0]);
+            const double* sys = wave_tree_sums(acc, sRed, lane);
+            GPROF_TD(t_w3, sys[0]);
+            bool inert;
+            int st = lm_iteration(sys, x, lambda, P.src, corr, P.mah, P.tgt, P.ns, lane, r0, se3c, g.rot_eps,
+                                  g.trans_eps, inert GPROF_ARG);
+            GPROF_TD(t_w4, st);
+            GPROF_ADD(2, t_w2, t_w3);  // [1]: linearize_round's own marks
+            GPROF_ADD(3, t_w3, t_w4);
+            if (st == gicpm::kLmAccepted && g.cycle_window > 0 && iters < g.max_iter) {
+                const int s2 = cyc.step(x, iters, g.max_iter, g.cycle_window, inert, lane);
+                if (s2 >= 0) {
+                    cyc.member(s2, x);
+                    st = kCycleExited;
+                }
+            }
+            if (lane == 0) {
+                *sFlag = st;
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+#pragma unroll
+                    for (int c = 0; c < 3; c++) sX[3 * r + c] = x.R[r][c];
+                    sX[9 + r] = x.t[r];
+                }
+            }
+        }
+        __syncthreads();
+        const int flag = __builtin_amdgcn_readfirstlane(*sFlag);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) x.R[r][c] = uniform_d(sX[3 * r + c]);
+            x.t[r] = uniform_d(sX[9 + r]);
+        }
+        if (flag == kCycleExited) {
+            iters_run = iters;
+            iters = g.max_iter;
+        }
+        if (flag != gicpm::kLmAccepted) break;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        write_pose(g, P.gp, x, iters);
+        count_iterations(g, iters, iters_run ? iters_run : iters, iters_run != 0);
+#ifdef PCORE_GICP_TIMELINE
+        if (P.gp < kTlPoses) {
+            g_tl_pose[2 * P.gp] = tl_p0;
+            g_tl_pose[2 * P.gp + 1] = __builtin_amdgcn_s_memrealtime();
+            g_tl_run[P.gp] = iters_run ? iters_run : iters;
+        }
+#endif
+    }
+}
+
 // One wave per pose; persistent waves pull poses from a counter.  Each iteration linearises in rounds of 64
 // source points (point i -> lane i % 64, contributions added in point order), reduces the 28 terms by the
 // shuffle-down tree in registers and runs the LM iteration on the wave.  The per-pose iteration chain is
@@ -1111,36 +1047,72 @@ __device__ __forceinline__ GicpPose gicp_pose(const GicpArgs& g, int pose) {
 #ifndef PCORE_GICP_WAVES_PER_EU
 #define PCORE_GICP_WAVES_PER_EU 3
 #endif
+#ifndef PCORE_GICP_NO_COOP
+#define PCORE_GICP_NO_COOP 0  // register-budget experiments: the kernel without the heavy-pose phase
+#endif
 
 // GRID: the kernel holds the exact grid search of large segments (> kGridNNMin targets).  launch_gicp picks the
 // instance without it when no segment of the observation is that large (every C2-C5 label): the search's registers
 // then weigh on no pose (gicp_kernel 12.1 -> 11.9 ms per C3 call).
-template <bool GRID>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
+// NW: waves per workgroup.  The heaviest poses of the queue (GicpArgs::heavy_count, the first entries of the cost
+// order) are refined first, each by a whole workgroup (coop_pose: the NW waves split the correspondence search, the
+// part that grows with points x targets); then every wave pulls the remaining poses one at a time.  A heavy chain that
+// runs all its iterations alone outlasted the rest of the launch (the queue-dry tail).
+template <bool GRID, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PCORE_GICP_WAVES_PER_EU)))
 gicp_kernel(GicpArgs g, int num_poses) {
-    __shared__ double sRed[gicpm::kTerms];
-    __shared__ double2 sM0[3][kLdsPts];
-    __shared__ Pt3 sS0[kLdsPts];
-    __shared__ float4 sT0[kLdsPts];
-    __shared__ int sPose;
+    __shared__ double sRedA[NW][gicpm::kTerms];
+    __shared__ double2 sM0A[NW][3][kLdsPts];
+    __shared__ Pt3 sS0A[NW][kLdsPts];
+    __shared__ float4 sT0A[NW][kLdsPts];
+    __shared__ int sPoseA[NW];
     __shared__ double sSe3[4 * gicpm::kSe3Terms];  // se3_exp's series coefficients, read at their use
-    __shared__ unsigned sHist[3 * 64];               // the correspondence history's float transforms (below)
-    __shared__ unsigned sCyc[kCycleRingWords];       // the cycle exit's last 32 float transforms (CycleExit)
-    const int lane = threadIdx.x;
-    const Round0 r0{sM0, sS0, sT0};
-    if (lane < 4 * gicpm::kSe3Terms) sSe3[lane] = gicpm::kSe3Coef[lane];
+    __shared__ unsigned sHistA[NW][3 * 64];          // the correspondence history's float transforms (below)
+    __shared__ unsigned sCycA[NW][kCycleRingWords];  // the cycle exit's last 32 float transforms (CycleExit)
+    __shared__ double sX[12];                         // coop_pose's broadcast of x and the iteration's outcome
+    __shared__ int sFlag, sCoop;
+    const int wave = NW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+    const int lane = threadIdx.x & 63;
+    double* const sRed = sRedA[wave];
+    int* const pPose = &sPoseA[wave];
+    unsigned* const sHist = sHistA[wave];
+    unsigned* const sCyc = sCycA[wave];
+    const Round0 r0{sM0A[wave], sS0A[wave], sT0A[wave]};
+    if (threadIdx.x < 4 * gicpm::kSe3Terms) sSe3[threadIdx.x] = gicpm::kSe3Coef[threadIdx.x];
     GPROF_DECL;
 #ifdef PCORE_GICP_TIMELINE
     const unsigned long long tl_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    int nheavy = 0;
+    if constexpr (NW > 1 && !PCORE_GICP_NO_COOP) {
+        __syncthreads();  // sSe3 written by the first waves' lanes
+        if (g.heavy_count && g.pose_order)
+            nheavy = __builtin_amdgcn_readfirstlane(min(min(*g.heavy_count, g.heavy_max), num_poses));
+        for (;;) {
+            __syncthreads();  // the previous heavy pose is written and sCoop read
+            if (threadIdx.x == 0) {
+                const int q = atomicAdd(g.heavy_counter, 1);
+                sCoop = q < nheavy ? g.pose_order[q] : -1;
+            }
+            __syncthreads();
+            const int pose = __builtin_amdgcn_readfirstlane(sCoop);
+            if (pose < 0) break;
+            const GicpPose P = gicp_pose(g, pose);
+            if (!GRID && P.use_grid && threadIdx.x == 0 && g.iter_stats)
+                __hip_atomic_fetch_add(g.iter_stats + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            coop_pose<GRID, NW>(g, P, wave, lane, P.corr, sRedA[0], Round0{sM0A[0], sS0A[0], sT0A[0]},
+                                (const lds_cvd*)sSe3, sCycA[0], sX, &sFlag GPROF_ARG);
+        }
+    }
     for (;;) {
         wave_lds_sync();  // the previous pose's reads of sPose are done
         if (lane == 0) {
-            const int q = atomicAdd(g.work_counter, 1);
-            sPose = (g.pose_order && q < num_poses) ? g.pose_order[q] : q;
+            // the poses after the heavy ones, in the cost order
+            const int q = atomicAdd(g.work_counter, 1) + nheavy;
+            *pPose = (g.pose_order && q < num_poses) ? g.pose_order[q] : q;
         }
         wave_lds_sync();
-        const int pose = __builtin_amdgcn_readfirstlane(sPose);  // chunk-local, uniform
+        const int pose = __builtin_amdgcn_readfirstlane(*pPose);  // chunk-local, uniform
         if (pose >= num_poses) break;
         const GicpPose P = gicp_pose(g, pose);
         if (!GRID && P.use_grid && lane == 0 && g.iter_stats)  // the host picked the instance without the search
@@ -1299,11 +1271,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
 // indices go to LDS, and wave 0 then adds the contributions and runs the LM iteration exactly as gicp_kernel
 // does -- point i on lane i % 64, in point order -- so the refined poses are bit-identical; only the
 // nearest-target searches, the expensive part against a whole-scene target, run in parallel.
-constexpr int kCycleExited = 3;  // gicp_wide_kernel's flag: wave 0's cycle exit stopped the pose (LmStatus + 1)
-
 template <int WPP>
 __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num_poses) {
-    constexpr int NT = 64 * WPP;
     extern __shared__ __attribute__((aligned(16))) int32_t jbuf[];  // src_cap correspondences
     __shared__ double sRed[gicpm::kTerms];
     __shared__ double2 sM0[3][kLdsPts];
@@ -1326,95 +1295,8 @@ __global__ void __launch_bounds__(64 * WPP) gicp_wide_kernel(GicpArgs g, int num
         __syncthreads();
         const int pose = __builtin_amdgcn_readfirstlane(sPose);
         if (pose >= num_poses) break;
-        const GicpPose P = gicp_pose(g, pose);
-        LabelGrid G{};
-        if (P.use_grid) G = g.grids[P.seg];
-        Xform x;
-        xform_identity(x);
-        double lambda = -1.0;  // wave 0's
-        int iters = 0, iters_run = 0;
-        CycleExit cyc;  // wave 0's
-        cyc.ring = sCyc;
-        if (wave == 0) cyc.start(lane);
-        const bool run = P.ns > 0 && P.nt > 0;
-        for (int it = 0; run && it < g.max_iter; it++) {
-            iters++;
-            float Rf[3][3], tf[3];
-            xform_float(x, Rf, tf);
-            GPROF_T(t_w0);
-            // correspondences, all waves
-            for (int i0 = wave * 64; i0 < P.ns; i0 += NT) {
-                const int i = i0 + lane;
-                const bool act = i < P.ns;
-                const float4 sp = act ? P.src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                float qf[3];
-                gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, qf);
-                int j = -1;
-                float best = INFINITY;
-                if (P.use_grid) {
-                    if (act) grid_nn(G, g.cell_start, g.grid_pts, P.tgt, P.nt, qf[0], qf[1], qf[2], best, j);
-                } else {
-                    scan_quads(P.tquads, P.nt, qf[0], qf[1], qf[2], best, j);
-                }
-                if (act) jbuf[i] = j;
-            }
-            __syncthreads();
-            GPROF_TD(t_w1, Rf[0][0]);
-            GPROF_ADD(0, t_w0, t_w1);
-            if (wave == 0) {
-                double acc[gicpm::kTerms];
-#pragma unroll
-                for (int v = 0; v < gicpm::kTerms; v++) acc[v] = 0.0;
-                for (int i0 = 0; i0 < P.ns; i0 += 64) {
-                    const int i = i0 + lane;
-                    linearize_round<false>(x, Rf, tf, P.src, P.scov, P.tgt, P.tcov, P.ns, i0 + lane, P.use_grid, G, g,
-                                           P.tquads, P.nt, i < P.ns ? jbuf[i] : -1, nullptr, P.mah, r0, acc, false GPROF_ARG);
-                }
-                GPROF_TD(t_w2, acc[0]);
-                const double* sys = wave_tree_sums(acc, sRed, lane);
-                GPROF_TD(t_w3, sys[0]);
-                bool inert;
-                int st = lm_iteration(sys, x, lambda, P.src, jbuf, P.mah, P.tgt, P.ns, lane, r0, (const lds_cvd*)sSe3,
-                                      g.rot_eps, g.trans_eps, inert GPROF_ARG);
-                GPROF_TD(t_w4, st);
-                GPROF_ADD(2, t_w2, t_w3);  // [1]: linearize_round's own marks
-                GPROF_ADD(3, t_w3, t_w4);
-                if (st == gicpm::kLmAccepted && g.cycle_window > 0 && iters < g.max_iter) {
-                    const int s2 = cyc.step(x, iters, g.max_iter, g.cycle_window, inert, lane);
-                    if (s2 >= 0) {
-                        cyc.member(s2, x);
-                        st = kCycleExited;
-                    }
-                }
-                if (lane == 0) {
-                    sFlag = st;
-#pragma unroll
-                    for (int r = 0; r < 3; r++) {
-#pragma unroll
-                        for (int c = 0; c < 3; c++) sX[3 * r + c] = x.R[r][c];
-                        sX[9 + r] = x.t[r];
-                    }
-                }
-            }
-            __syncthreads();
-            const int flag = __builtin_amdgcn_readfirstlane(sFlag);
-#pragma unroll
-            for (int r = 0; r < 3; r++) {
-#pragma unroll
-                for (int c = 0; c < 3; c++) x.R[r][c] = uniform_d(sX[3 * r + c]);
-                x.t[r] = uniform_d(sX[9 + r]);
-            }
-            if (flag == kCycleExited) {
-                iters_run = iters;
-                iters = g.max_iter;
-            }
-            if (flag != gicpm::kLmAccepted) break;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            write_pose(g, P.gp, x, iters);
-            count_iterations(g, iters, iters_run ? iters_run : iters, iters_run != 0);
-        }
+        coop_pose<true, WPP>(g, gicp_pose(g, pose), wave, lane, jbuf, sRed, r0, (const lds_cvd*)sSe3, sCyc, sX,
+                             &sFlag GPROF_ARG);
     }
     if (wave == 0) GPROF_FLUSH;
 }
@@ -1449,7 +1331,8 @@ hipError_t launch_lm_solve_test(const double* sys, const double* lambda, double*
     return hipGetLastError();
 }
 
-// predicted cost of one GICP iteration of a pose: source points x targets of its segment (the scan)
+// predicted cost of one GICP iteration of a pose: source points x targets of its segment (the scan); the poses at
+// or above g.heavy_cost are counted into *g.heavy_count (the cost order puts them first: gicp_kernel's heavy poses)
 __global__ void gicp_cost_key_kernel(GicpArgs g, int n, uint32_t* keys, int32_t* idx) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1462,6 +1345,7 @@ __global__ void gicp_cost_key_kernel(GicpArgs g, int n, uint32_t* keys, int32_t*
     const unsigned long long c = (unsigned long long)max(g.src_count[i], 0) * nt;
     keys[i] = (uint32_t)min(c >> 4, 0xffffffffull);
     idx[i] = i;
+    if (g.heavy_count && g.heavy_cost > 0 && c >= (unsigned long long)g.heavy_cost) atomicAdd(g.heavy_count, 1);
 }
 
 size_t gicp_order_temp_bytes(int n) {
@@ -1481,11 +1365,18 @@ hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32
                                                         32, s);
 }
 
+#ifndef PCORE_GICP_WG_WAVES
+#define PCORE_GICP_WG_WAVES 4
+#endif
+constexpr int kGicpWgWaves = PCORE_GICP_WG_WAVES;  // gicp_kernel's waves per workgroup (the heavy poses' team)
+
 hipError_t gicp_occupancy_per_cu(int* per_cu) {
     *per_cu = 0;
     int other = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel<true>, 64, 0);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&other, gicp_kernel<false>, 64, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, gicp_kernel<true, kGicpWgWaves>,
+                                                                64 * kGicpWgWaves, 0);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&other, gicp_kernel<false, kGicpWgWaves>, 64 * kGicpWgWaves, 0);
     if (e == hipSuccess) *per_cu = std::min(*per_cu, other);
     return e;
 }
@@ -1493,7 +1384,8 @@ hipError_t gicp_occupancy_per_cu(int* per_cu) {
 hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hipStream_t s, bool grid) {
     if (num_poses <= 0) return hipSuccess;
     const int resident_wgs = std::max(1, d.gicp_resident_wgs), num_cus = std::max(1, d.num_cus);
-    hipError_t e = hipMemsetAsync(g.work_counter, 0, sizeof(int32_t), s);
+    // the one-wave queue's and the heavy queue's counters (heavy_count was set by the cost-key kernel)
+    hipError_t e = hipMemsetAsync(g.work_counter, 0, 2 * sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     // a batch too small to give every SIMD a pose: spread each pose's searches over kGicpWideWpp waves
     const size_t wide_lds = (size_t)g.src_cap * sizeof(int32_t);
@@ -1508,10 +1400,11 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hi
                            num_poses);
         return hipGetLastError();
     }
+    const dim3 wgs(std::min(resident_wgs, (num_poses + kGicpWgWaves - 1) / kGicpWgWaves)), block(64 * kGicpWgWaves);
     if (grid)
-        hipLaunchKernelGGL(gicp_kernel<true>, dim3(std::min(resident_wgs, num_poses)), dim3(64), 0, s, g, num_poses);
+        hipLaunchKernelGGL((gicp_kernel<true, kGicpWgWaves>), wgs, block, 0, s, g, num_poses);
     else
-        hipLaunchKernelGGL(gicp_kernel<false>, dim3(std::min(resident_wgs, num_poses)), dim3(64), 0, s, g, num_poses);
+        hipLaunchKernelGGL((gicp_kernel<false, kGicpWgWaves>), wgs, block, 0, s, g, num_poses);
     return hipGetLastError();
 }
 

@@ -105,6 +105,8 @@ struct FusedArgs {
     float4* cloud_out;
     int32_t* cloud_count;
     int32_t cloud_cap;
+    // the clouds' GICP covariances (k = 10) in the same launch, same slots (6 doubles per point); nullable
+    double* cloud_cov;
     // colour gate of cost_type 1 (compute_costs.cuh:201-240); null / 0 otherwise
     const uint32_t* stri_orig;  // original triangle index of every stream triangle slot
     const float4* tri_lab;      // Lab of every original triangle's colour (reference channel order)
@@ -181,6 +183,13 @@ struct GicpArgs {
     // [3] poses that needed the grid search in the instance without it -- a host / kernel rule mismatch, an error)
     int32_t cycle_window;
     unsigned long long* iter_stats;
+    // heavy poses (gicp_kernel: one workgroup each, its waves splitting the correspondence search): the poses whose
+    // source points x segment targets reach heavy_cost (counted into *heavy_count by the cost-key kernel), at most
+    // heavy_max, dequeued through *heavy_counter before the one-wave queue; heavy_count nullable (none)
+    int32_t* heavy_counter;
+    int32_t* heavy_count;
+    long long heavy_cost;
+    int32_t heavy_max;
 };
 
 constexpr int kCorrHist = 16;      // history sets per pose: lanes 4e .. 4e + 3 of three VGPRs hold set e's 12 floats

@@ -18,6 +18,7 @@
 //   select_kernel          host selection of the reference (int cost, filter, per-model argmin key).
 #include "pcore_internal.h"
 #include "pcore_colour.h"
+#include "pcore_cov.h"
 #include "pcore_fdiv.h"
 
 #include <algorithm>
@@ -1247,6 +1248,17 @@ __global__ void __launch_bounds__(kThreads) render_cloud_kernel(FusedArgs a) {
                 chunk(SampleWin{sw.x0 + c0, sw.y0 + r0, min(cw, sw.nx - c0), min(ch, sw.ny - r0), sw.fastdiv});
     }
     if (tid == 0) a.cloud_count[pose] = carry_s < a.cloud_cap ? carry_s : a.cloud_cap;
+    // the source covariances of the cloud this workgroup has just written: pcore_cov.h's rounds of
+    // 64 queries, round r on wave r % 4, each wave staging candidates through its own 64-point tile in the vertex ring's
+    // LDS (free once the raster is done); the points are read back from the slot (L2, written before the barrier)
+    if (a.cloud_cov) {
+        __syncthreads();  // every chunk's points are written and carry_s is final
+        const int n = carry_s < a.cloud_cap ? carry_s : a.cloud_cap;
+        float4* tile = reinterpret_cast<float4*>(sm.vxy) + wave * kCovLanes;
+        double* C = a.cloud_cov + (size_t)6 * pose * a.cloud_cap;
+        for (int i0 = wave * kCovLanes; i0 < n; i0 += kThreads)
+            cov_knn_round<10, true>(out, n, 10, i0, lane, tile, C);
+    }
 }
 
 hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s) {
