@@ -1034,9 +1034,9 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     g.work_counter = c->icp_counter.p;
     g.heavy_counter = c->icp_counter.p + 1;
     g.heavy_count = c->icp_counter.p + 2;
-    // heavy poses: source points x targets >= 60,000 (e.g. 211 points on a 285-target segment), at most 2 per CU;
-    // PCORE_GICP_HEAVY_COST / PCORE_GICP_HEAVY_MAX for A/B (0: none)
-    g.heavy_cost = 60000;
+    // heavy poses (a -DPCORE_GICP_WG_WAVES=4 build only): source points x targets >= 60,000 (e.g. 211 points on a
+    // 285-target segment), at most 2 per CU; PCORE_GICP_HEAVY_COST / PCORE_GICP_HEAVY_MAX for A/B (0: none)
+    g.heavy_cost = kGicpHeavyBuild ? 60000 : 0;
     g.heavy_max = 2 * std::max(1, c->dinfo.num_cus);
     if (const char* e = getenv("PCORE_GICP_HEAVY_COST")) g.heavy_cost = atoll(e);
     if (const char* e = getenv("PCORE_GICP_HEAVY_MAX")) g.heavy_max = atoi(e);

@@ -43,7 +43,10 @@ constexpr int kMaxK = 16;
 // Each wave sums its clocks in registers and adds them once at exit (no atomics inside the loop); each
 // clock read is ordered after its phase's last result by an asm input dependency.
 #ifdef PCORE_GICP_PROFILE
-constexpr int kGprof = 9;
+constexpr int kGprof = 10;  // [9]: the pose-iterations the sums cover (poses of >= PCORE_GICP_PROF_MIN_NS points)
+#ifndef PCORE_GICP_PROF_MIN_NS
+#define PCORE_GICP_PROF_MIN_NS 0
+#endif
 __device__ unsigned long long g_gicp_prof[kGprof];
 #define GPROF_DECL unsigned long long gp_acc[kGprof] = {}
 #define GPROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -1120,6 +1123,10 @@ gicp_kernel(GicpArgs g, int num_poses) {
 #ifdef PCORE_GICP_TIMELINE
         const unsigned long long tl_p0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef PCORE_GICP_PROFILE
+        unsigned long long gp_snap[kGprof];  // the sums before this pose (restored if the pose is below the size filter)
+        for (int k_ = 0; k_ < kGprof; k_++) gp_snap[k_] = gp_acc[k_];
+#endif
         const LabelGrid G{};  // linearize_round's grid argument, unused here: the searches below load the grid
         Xform x;
         xform_identity(x);
@@ -1241,6 +1248,11 @@ gicp_kernel(GicpArgs g, int num_poses) {
             }
         }
         if (exit_slot >= 0) cyc.member(exit_slot, x);
+#ifdef PCORE_GICP_PROFILE
+        gp_acc[9] += iters_run ? iters_run : iters;
+        if (P.ns < PCORE_GICP_PROF_MIN_NS)
+            for (int k_ = 0; k_ < kGprof; k_++) gp_acc[k_] = gp_snap[k_];
+#endif
         if (lane == 0) {
             write_pose(g, P.gp, x, iters);
             count_iterations(g, iters, iters_run ? iters_run : iters, iters_run != 0);
@@ -1366,7 +1378,7 @@ hipError_t launch_gicp_order(const GicpArgs& g, int n, uint32_t* keys_in, uint32
 }
 
 #ifndef PCORE_GICP_WG_WAVES
-#define PCORE_GICP_WG_WAVES 4
+#define PCORE_GICP_WG_WAVES 1  // 4: the heavy poses by 4-wave workgroups -- measured, no faster
 #endif
 constexpr int kGicpWgWaves = PCORE_GICP_WG_WAVES;  // gicp_kernel's waves per workgroup (the heavy poses' team)
 

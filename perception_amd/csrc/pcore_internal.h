@@ -192,6 +192,12 @@ struct GicpArgs {
     int32_t heavy_max;
 };
 
+#if defined(PCORE_GICP_WG_WAVES) && PCORE_GICP_WG_WAVES > 1
+constexpr bool kGicpHeavyBuild = true;
+#else
+constexpr bool kGicpHeavyBuild = false;
+#endif
+
 constexpr int kCorrHist = 16;      // history sets per pose: lanes 4e .. 4e + 3 of three VGPRs hold set e's 12 floats
 constexpr int kCorrHistCap = 512;  // source points per history set (poses with more search every iteration)
 

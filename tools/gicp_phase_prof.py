@@ -27,7 +27,7 @@ def main():
     lib = _native.load()
     fn = lib.pcore_debug_gicp_profile
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 9)()
+    buf = (ctypes.c_ulonglong * 10)()
     w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total, stride=w.stride)
     torch.cuda.synchronize()
     fn(buf, 1)
@@ -37,7 +37,7 @@ def main():
     fn(buf, 0)
     it = iters.cpu().numpy()
     # one linearisation + one LM iteration per executed iteration (a cycle exit reports 150 but runs fewer)
-    total = int(w.core.stats()["gicp_iterations_run"])
+    total = int(buf[9])  # the executed pose-iterations of the profiled poses (a PCORE_GICP_PROF_MIN_NS build: the large ones)
     names = ["search", "contributions", "reduction", "LM iteration", "  solves", "  se3 + compose", "  trial errors",
              "  decisions"]
     print("pose-iterations", total, "mean iters", it.mean(), "max", it.max())

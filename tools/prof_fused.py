@@ -19,9 +19,10 @@ def main():
     ap.add_argument("--icp", action="store_true")
     ap.add_argument("--c3", action="store_true", help="the 5-object C3 scene")
     ap.add_argument("--iters-json", default=None, help="write the GICP iterations of the last call here (--icp)")
+    ap.add_argument("--mesh", default="003_cracker_box", help="the single mesh of the C2 workload (e.g. scan_blob)")
     a = ap.parse_args()
     names = ["003_cracker_box", "005_tomato_soup_can", "006_mustard_bottle", "010_potted_meat_can",
-             "024_bowl"] if a.c3 else ["003_cracker_box"]
+             "024_bowl"] if a.c3 else [a.mesh]
     w = workloads.build(names=names, poses_per_model=a.poses)
     n = int(w.poses.shape[0])
     its = None
