@@ -116,48 +116,79 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
     w = workloads.build(names=C3_NAMES, poses_per_model=poses_per_model, device=local, rank=rank)
     n = int(w.poses.shape[0])
     dev = w.poses.device
-    out = (torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
-           *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3)))
-    keys = torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev)
+    # batches in flight (PCORE_BENCH_C3_LANES, A/B): step i runs on lane i % L (its own context, stream, scratch,
+    # outputs and key buffer), so one step's GICP tail could overlap the next step's render, clouds and covariances;
+    # every step is still one whole 50k-pose batch completing inside the timed region.  Two lanes measured no faster
+    # (3.95-3.99 vs 3.98-3.99 M poses/s, profiles/r06m/), so the C3 leg runs one
+    L = max(1, int(os.environ.get("PCORE_BENCH_C3_LANES", "1")))
+    lanes = workloads.lanes(w, L)
+    outs = [(torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+             *(torch.empty(n, dtype=torch.float32, device=dev) for _ in range(3))) for _ in range(L)]
+    keys_ring = [torch.full((w.num_models,), PCORE_KEY_NONE, dtype=torch.int64, device=dev) for _ in range(L)]
+    works = [None] * L
+    pending = [False] * L  # the lane's last call is a timed step whose stats are not read yet
     rec = {"gicp_ms": [], "icp_s": [], "run": [], "exits": []}
 
-    def step(record, window):
-        keys.fill_(PCORE_KEY_NONE)
-        adj, it, rc, oc, df = w.core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
-                                                  stride=w.stride, out=out, cycle_exit_window=window)
-        w.core.select(rc, oc, w.pose_model, w.num_models, index_base=w.index_base, keys=keys)
-        if record:
-            st = w.core.stats()  # waits for this step's GICP stage (events), not for the re-score
-            rec["gicp_ms"].append(st["gicp_ms"])
-            rec["icp_s"].append(st["icp_runtime"])
-            rec["run"].append(st["gicp_iterations_run"])
-            rec["exits"].append(st["gicp_cycle_exits"])
-        work = pdist.allreduce_min_keys_async(keys)
-        if work is not None:
-            work.wait()
+    def read_stats(b):
+        st = lanes[b][0].stats()  # waits for that call's GICP stage (its events), not for its re-score
+        rec["gicp_ms"].append(st["gicp_ms"])
+        rec["icp_s"].append(st["icp_runtime"])
+        rec["run"].append(st["gicp_iterations_run"])
+        rec["exits"].append(st["gicp_cycle_exits"])
+        pending[b] = False
+
+    def step(i, record, window):
+        b = i % L
+        core, st = lanes[b]
+        if works[b] is not None:  # the lane's previous exchange completes before its key buffer is rewritten
+            with torch.cuda.stream(st):
+                works[b].wait()
+            works[b] = None
+        if pending[b]:  # the lane's previous call's stats, before this call replaces them
+            read_stats(b)
+        with torch.cuda.stream(st):
+            keys_ring[b].fill_(PCORE_KEY_NONE)
+            adj, it, rc, oc, df = core.evaluate_icp(w.poses, w.pose_model, w.pose_label, w.pose_obs_total,
+                                                    stride=w.stride, out=outs[b], cycle_exit_window=window, stream=st)
+            core.select(rc, oc, w.pose_model, w.num_models, index_base=w.index_base, keys=keys_ring[b], stream=st)
+            works[b] = pdist.allreduce_min_keys_async(keys_ring[b])
+        pending[b] = record
 
     def timed(window):
         for k in rec:
             rec[k] = []
-        for _ in range(max(warmup, 1)):
-            step(False, window)
+        for i in range(max(warmup, 1) + L):  # every lane warmed (scratch, target covariances, tile tier)
+            step(i, False, window)
+        for b in range(L):
+            if works[b] is not None:
+                works[b].wait()
+                works[b] = None
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step(True, window)
+        for i in range(steps):
+            step(i, True, window)
+        for b in range(L):  # every exchange completes inside the timed region
+            if works[b] is not None:
+                works[b].wait()
+                works[b] = None
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
+        for b in range(L):  # the last steps' stats (their work is done)
+            if pending[b]:
+                read_stats(b)
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed, {k: list(v) for k, v in rec.items()}
 
+    last = (steps - 1) % L  # the lane of the last timed step
+    out, keys = outs[last], keys_ring[last]
     # the A/B first: every iteration run out (fast_gicp's loop, cycle_exit_window 0), then the spec's exit -- the
     # measured run -- so out / keys hold the spec's results afterwards
     el_off, rec_off = timed(0)
@@ -201,7 +232,8 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
         "warmup": max(warmup, 1),
         "config": {"workload": "C3: 5 YCB-proxy objects x 10k 6-DoF candidate poses/GPU, render + GICP (fast_gicp LM, "
                                "k 10, <= 150 iterations) + re-render + score + select, 640x480, stride 8",
-                   "poses_per_gpu": n, "objects": C3_NAMES, "parallelism": f"pose-shard x{world}"},
+                   "poses_per_gpu": n, "objects": C3_NAMES, "parallelism": f"pose-shard x{world}",
+                   "batches_in_flight": L},
         "gicp": {"iterations_mean": float(its.mean()), "iterations_p50": float(np.percentile(its, 50)),
                  "iterations_p90": float(np.percentile(its, 90)), "at_max_iterations": int((its >= 150).sum()),
                  "gicp_ms_per_step": g_ms, "icp_stage_ms_per_step": float(np.mean(icp_s)) * 1e3 if icp_s else None,

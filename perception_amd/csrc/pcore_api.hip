@@ -84,6 +84,9 @@ struct pcore_ctx {
     DevBuf<double> icp_mahal;   // GicpArgs::mahal
     DevBuf<int32_t> icp_counter;
     DevBuf<unsigned long long> icp_iter_stats;  // GicpArgs::iter_stats, zeroed per pcore_evaluate_icp
+    // their copy in pinned host memory, made on the call's stream before each chunk's end event (pcore_get_stats reads
+    // it after that event: no synchronous copy, which would wait for every blocking stream of the device)
+    unsigned long long* icp_iter_stats_host = nullptr;
     DevBuf<uint32_t> icp_order_keys;  // 2 x chunk keys (in, out)
     DevBuf<int32_t> icp_order_idx;    // 2 x chunk indices (in, out = GicpArgs::pose_order)
     DevBuf<unsigned char> icp_order_temp;
@@ -313,6 +316,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->model_st_lo); (void)dev_free(c->model_st_hi); (void)dev_free(c->model_box); (void)dev_free(c->proj);
     (void)dev_free(c->fb_ctr); (void)dev_free(c->win_hist);
     if (c->fb_host) (void)hipHostFree(c->fb_host);
+    if (c->icp_iter_stats_host) (void)hipHostFree(c->icp_iter_stats_host);
     (void)dev_free(c->src_depth); (void)dev_free(c->src_mask); (void)dev_free(c->src_s); (void)dev_free(c->lab_s);
     (void)dev_free(c->grids); (void)dev_free(c->cell_start); (void)dev_free(c->grid_pts);
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
@@ -987,6 +991,8 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 4));  // [0] one-wave queue, [1] heavy queue, [2] heavy poses
     HIPC(c, dev_reserve(c->icp_iter_stats, 4));
+    if (!c->icp_iter_stats_host)
+        HIPC(c, hipHostMalloc((void**)&c->icp_iter_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault));
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
     const size_t order_temp = gicp_order_temp_bytes(chunk);
@@ -1091,6 +1097,9 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         }
         if (ev) HIPC(c, hipEventRecord(ev[1], s));
         HIPC(c, launch_gicp(g, n, c->dinfo, s, grid_needed));
+        if (ev)  // the counters so far (the last chunk's copy holds the call's totals)
+            HIPC(c, hipMemcpyAsync(c->icp_iter_stats_host, c->icp_iter_stats.p, 4 * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, s));
         if (ev) {
             HIPC(c, hipEventRecord(ev[2], s));
             c->icp_ev_used++;
@@ -1150,8 +1159,8 @@ int pcore_get_stats(pcore_ctx* c, pcore_gpu_stats* out, int32_t reset) {
     out->gicp_ms = (float)gicp_ms;
     out->icp_chunks = c->icp_ev_used;
     unsigned long long it[4] = {0ull, 0ull, 0ull, 0ull};
-    if (c->icp_ev_used > 0 && c->icp_iter_stats.p)  // the last chunk's end event has completed
-        HIPC(c, hipMemcpy(it, c->icp_iter_stats.p, sizeof(it), hipMemcpyDeviceToHost));
+    if (c->icp_ev_used > 0 && c->icp_iter_stats_host)  // the last chunk's end event (after its copy) has completed
+        for (int i = 0; i < 4; i++) it[i] = c->icp_iter_stats_host[i];
     if (it[3] != 0)
         return fail(c, PCORE_E_HIP, "evaluate_icp: " + std::to_string(it[3]) +
                                         " poses needed the grid search in the GICP instance without it");
