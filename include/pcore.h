@@ -243,6 +243,13 @@ int pcore_debug_lm_solve(const double* d_sys, const double* d_lambda, double* d_
  * (upper triangle, row-major).  1 <= k <= 16. */
 int pcore_debug_covariances(const float* d_xyzw, const int32_t* d_seg_off, const int32_t* d_seg_cnt, int32_t num_segs,
                             int32_t k, double* d_out_cov6, pcore_stream stream);
+/* Test hook (no reference counterpart): the k = 10 covariances of rendered-cloud slots (segment i: d_xyzw + 4 i
+ * seg_stride, d_seg_cnt[i] points) by the threshold k-NN over each cloud's stride-s sample grid (camera fx, fy, cx, cy;
+ * pcore_cov.h), falling back to the brute force where the grid does not allow it: bit-identical to
+ * pcore_debug_covariances for any points. */
+int pcore_debug_covariances_cloud(const float* d_xyzw, const int32_t* d_seg_cnt, int32_t seg_stride, int32_t num_segs,
+                                  float fx, float fy, float cx, float cy, int32_t stride, double* d_out_cov6,
+                                  pcore_stream stream);
 
 /* GenerateSuccessorStates / GetStateImagesUnifiedGPU host work on the device (search_env.cpp:7056-7254,
  * 1535-1576), for the drop-in recognizer's states:

@@ -1086,7 +1086,13 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         if (ev && fold) HIPC(c, hipEventRecord(ev[0], s));  // icp_runtime then spans the cloud + covariance launch
         HIPC(c, launch_render_cloud(a, s));
         if (ev && !fold) HIPC(c, hipEventRecord(ev[0], s));
-        if (!fold) HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
+        // the clouds' covariances: k = 10 by the threshold k-NN over each cloud's sample grid (pcore_cov.h;
+        // PCORE_COV_BRUTE=1 restores the brute-force kernel for A/B), other k by the brute force; bit-identical
+        if (!fold && k == 10 && !getenv("PCORE_COV_BRUTE"))
+            HIPC(c, launch_covariances_cloud(c->icp_cloud.p, c->icp_count.p, nsamp, n, a.fx, a.fy, a.cx, a.cy, p->stride,
+                                             c->icp_cov.p, s));
+        else if (!fold)
+            HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
         g.pose_base = base;
         g.pose_order = nullptr;
         HIPC(c, hipMemsetAsync(g.heavy_count, 0, sizeof(int32_t), s));
@@ -1203,6 +1209,15 @@ int pcore_debug_covariances(const float* d_xyzw, const int32_t* d_seg_off, const
         return PCORE_E_INVALID_ARG;
     return launch_covariances(reinterpret_cast<const float4*>(d_xyzw), d_seg_off, d_seg_cnt, 0, num_segs, k, d_out_cov6,
                               (hipStream_t)stream, INT_MAX) == hipSuccess ? PCORE_OK : PCORE_E_HIP;
+}
+
+int pcore_debug_covariances_cloud(const float* d_xyzw, const int32_t* d_seg_cnt, int32_t seg_stride, int32_t num_segs,
+                                  float fx, float fy, float cx, float cy, int32_t stride, double* d_out_cov6,
+                                  pcore_stream stream) {
+    if (num_segs < 0 || seg_stride < 0 || stride <= 0 || (num_segs > 0 && (!d_xyzw || !d_seg_cnt || !d_out_cov6)))
+        return PCORE_E_INVALID_ARG;
+    return launch_covariances_cloud(reinterpret_cast<const float4*>(d_xyzw), d_seg_cnt, seg_stride, num_segs, fx, fy, cx,
+                                    cy, stride, d_out_cov6, (hipStream_t)stream) == hipSuccess ? PCORE_OK : PCORE_E_HIP;
 }
 
 int pcore_depth_to_cloud(pcore_ctx* c, const int32_t* d_depth, int32_t num_poses, int32_t width, int32_t height,

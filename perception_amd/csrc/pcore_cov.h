@@ -8,6 +8,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #ifndef PCORE_COV_SKIP
 #define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
 #endif
@@ -194,6 +196,164 @@ __device__ __forceinline__ void cov_knn_round(const float4* P, int n, int k_arg,
         }
     }
     if (i < n) cov_from_list<KMAX>(P, nb, cnt, C + (size_t)6 * i);
+}
+
+}  // namespace
+}  // namespace pcore
+
+namespace pcore {
+namespace {
+
+// ---- the threshold k-NN of a rendered cloud (round 6) ----------------------------------------------------------
+// A cloud unprojected from a stride-s sample grid keeps each point's grid cell: (kx, ky) = rint((x / z fx + cx) / s),
+// rint((y / z fy + cy) / s).  The k nearest (distance, index) of a point are the first k of all candidates in that
+// order; any tau at or above the k-th smallest distance keeps them all.  So:
+//   1. tau = the k-th smallest distance to the points of the 7 x 7 grid cells around the query (an LDS map of the
+//      cloud's window gives them; fewer than k there: tau = +inf),
+//   2. one pass over all candidates (the brute-force scan's order and arithmetic) collects the j with d <= tau,
+//   3. the collected ones, in index order, go through the brute-force's insertion: the list is the brute force's,
+//      bit for bit, whatever tau is (tau only bounds what is collected).
+// The brute-force scan runs its insertion block whenever any lane of the wave inserts -- nearly every candidate of a
+// ~100-point cloud; here the insertions are the 49 neighbourhood steps and the ~10-14 collected per lane (tools/
+// knn_threshold_estimate.py), and the full pass is a compare and a predicated LDS store.  A lane collecting more than
+// kThrCap candidates, a cloud whose window exceeds kThrMap cells or holding a non-finite point take the brute force.
+struct CovGrid {
+    float fx, fy, cx, cy;
+    int stride;
+};
+
+constexpr int kThrMap = 1536;  // window cells of the map (ushort point index each; 0xffff = empty)
+constexpr int kThrCap = 24;    // collected candidates per lane
+constexpr int kThrR = 3;       // the neighbourhood: (2 kThrR + 1)^2 cells
+constexpr size_t kThrLdsBytes = kThrMap * 2 + (size_t)kThrCap * kCovLanes * 2 + kCovLanes * 16;
+
+__device__ __forceinline__ void cov_cell(const float4& p, const CovGrid& cg, int& kx, int& ky) {
+    kx = (int)rintf((p.x / p.z * cg.fx + cg.cx) / (float)cg.stride);
+    ky = (int)rintf((p.y / p.z * cg.fy + cg.cy) / (float)cg.stride);
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// the cloud's window and its cell map (ushort point index per cell); false: the brute force serves this segment
+__device__ __forceinline__ bool cov_thr_map(const float4* P, int n, const CovGrid& cg, int lane, unsigned short* map,
+                                            int& kx0, int& ky0, int& wx, int& wy) {
+    if (n > 0xfffe) return false;
+    int x0 = INT_MAX, x1 = INT_MIN, y0 = INT_MAX, y1 = INT_MIN;
+    bool ok = true;
+    for (int i = lane; i < n; i += kCovLanes) {
+        const float4 p = P[i];
+        const bool fin = __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z) && p.z > 0.0f;
+        ok = ok && fin;
+        if (fin) {
+            int kx, ky;
+            cov_cell(p, cg, kx, ky);
+            x0 = min(x0, kx); x1 = max(x1, kx); y0 = min(y0, ky); y1 = max(y1, ky);
+        }
+    }
+    if (__ballot(!ok) != 0ull) return false;
+    x0 = wave_min_i(x0); x1 = wave_max_i(x1); y0 = wave_min_i(y0); y1 = wave_max_i(y1);
+    if (n == 0 || x1 < x0 || y1 < y0) return false;
+    const long long cells = (long long)(x1 - x0 + 1) * (long long)(y1 - y0 + 1);
+    if (cells > kThrMap) return false;
+    kx0 = x0; ky0 = y0; wx = x1 - x0 + 1; wy = y1 - y0 + 1;
+    for (int c = lane; c < (int)cells; c += kCovLanes) map[c] = 0xffff;
+    wave_lds_sync();
+    for (int i = lane; i < n; i += kCovLanes) {
+        int kx, ky;
+        cov_cell(P[i], cg, kx, ky);
+        map[(ky - y0) * wx + (kx - x0)] = (unsigned short)i;  // a shared cell keeps one of its points: any subset bounds
+    }
+    wave_lds_sync();
+    return true;
+}
+
+// One round of 64 queries by the threshold k-NN (k = 10).  Returns false (nothing written) when a lane collects more
+// than kThrCap candidates: the caller runs cov_knn_round for this round.
+__device__ __forceinline__ bool cov_knn_round_thr(const float4* P, int n, int i0, int lane, const CovGrid& cg,
+                                                  const unsigned short* map, int kx0, int ky0, int wx, int wy,
+                                                  unsigned short* list, float4* tile, double* C) {
+    constexpr int K = 10;
+    const int i = i0 + lane;
+    const bool act = i < n;
+    const float4 xi = act ? P[i] : make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+    // 1. tau: the K-th smallest distance over the neighbourhood cells (sorted values, one-pass insertion)
+    float t[K];
+#pragma unroll
+    for (int q = 0; q < K; q++) t[q] = INFINITY;
+    int kx, ky;
+    cov_cell(xi, cg, kx, ky);
+    for (int dv = -kThrR; dv <= kThrR; dv++) {
+        const int cy = ky + dv - ky0;
+        for (int du = -kThrR; du <= kThrR; du++) {
+            const int cx = kx + du - kx0;
+            const bool in = act && cx >= 0 && cx < wx && cy >= 0 && cy < wy;
+            const int j = in ? (int)map[cy * wx + cx] : 0xffff;
+            if (j != 0xffff) {
+                const float4 p = P[j];
+                const float d = sqdist3(xi.x, xi.y, xi.z, p.x, p.y, p.z);
+#pragma unroll
+                for (int q = K - 1; q >= 1; q--) t[q] = t[q - 1] > d ? t[q - 1] : (t[q] > d ? d : t[q]);
+                t[0] = t[0] > d ? d : t[0];
+            }
+        }
+    }
+    const float tau = t[K - 1];
+    // 2. every candidate in scan order; the ones at or below tau are collected (index order)
+    int cnt = 0;
+    for (int j0 = 0; j0 < n; j0 += kCovLanes) {
+        wave_lds_sync();  // the previous tile is read
+        if (j0 + lane < n) tile[lane] = P[j0 + lane];
+        wave_lds_sync();
+        const int jn = min(kCovLanes, n - j0);
+        for (int jj = 0; jj < jn; jj++) {
+            const float4 xj = tile[jj];
+            const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
+            if (act && d <= tau) {
+                if (cnt < kThrCap) list[cnt * kCovLanes + lane] = (unsigned short)(j0 + jj);
+                cnt++;
+            }
+        }
+    }
+    if (__ballot(cnt > kThrCap) != 0ull) return false;
+    // 3. the collected candidates through the brute force's insertion (stable: entries strictly greater move right)
+    float nd[K];
+    int nb[K];
+#pragma unroll
+    for (int q = 0; q < K; q++) { nd[q] = 0.0f; nb[q] = 0; }
+    int len = 0;
+    const int cmax = wave_max_i(cnt);
+    for (int c = 0; c < cmax; c++) {
+        if (c < cnt) {
+            const int j = list[c * kCovLanes + lane];
+            const float4 p = P[j];
+            const float d = sqdist3(xi.x, xi.y, xi.z, p.x, p.y, p.z);
+            if (len < K || d < nd[K - 1]) {
+                const int pos = len < K ? len : K - 1;
+                int g = 0;
+#pragma unroll
+                for (int q = 0; q < K; q++) g += (q < pos && nd[q] > d) ? 1 : 0;
+                const int fin = pos - g;
+#pragma unroll
+                for (int q = K - 1; q >= 1; q--)
+                    if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
+#pragma unroll
+                for (int q = 0; q < K; q++)
+                    if (q == fin) { nd[q] = d; nb[q] = j; }
+                if (len < K) len++;
+            }
+        }
+    }
+    if (act) cov_from_list<K>(P, nb, len, C + (size_t)6 * i);
+    return true;
 }
 
 }  // namespace

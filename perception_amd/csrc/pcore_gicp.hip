@@ -228,6 +228,37 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
         cov_knn_round<KMAX, KFIXED>(pts + off, n, k_arg, i0, lane, tile, cov_out + (size_t)6 * off);
 }
 
+// The rendered clouds' covariances (k = 10): the threshold k-NN where the cloud's sample grid allows it, else the brute
+// force, round by round (pcore_cov.h); bit-identical either way.  Dynamic LDS: kThrLdsBytes.
+__global__ void __launch_bounds__(kCovLanes) covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt,
+                                                                     int seg_stride, CovGrid cg, double* cov_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char thr_lds[];
+    float4* tile = reinterpret_cast<float4*>(thr_lds);
+    unsigned short* map = reinterpret_cast<unsigned short*>(thr_lds + kCovLanes * sizeof(float4));
+    unsigned short* list = map + kThrMap;
+    const int sg = blockIdx.x;
+    const int off = sg * seg_stride;
+    const int n = seg_cnt[sg];
+    const int lane = threadIdx.x;
+    const float4* P = pts + off;
+    double* C = cov_out + (size_t)6 * off;
+    int kx0 = 0, ky0 = 0, wx = 0, wy = 0;
+    const bool thr = cov_thr_map(P, n, cg, lane, map, kx0, ky0, wx, wy);
+    for (int i0 = 0; i0 < n; i0 += kCovLanes) {
+        if (thr && cov_knn_round_thr(P, n, i0, lane, cg, map, kx0, ky0, wx, wy, list, tile, C)) continue;
+        cov_knn_round<10, true>(P, n, 10, i0, lane, tile, C);
+    }
+}
+
+hipError_t launch_covariances_cloud(const float4* pts, const int32_t* seg_cnt, int seg_stride, int num_segs,
+                                    float fx, float fy, float cx, float cy, int stride, double* cov_out, hipStream_t s) {
+    if (num_segs <= 0) return hipSuccess;
+    const CovGrid cg{fx, fy, cx, cy, stride};
+    hipLaunchKernelGGL(covariance_cloud_kernel, dim3(num_segs), dim3(kCovLanes), kThrLdsBytes, s, pts, seg_cnt,
+                       seg_stride, cg, cov_out);
+    return hipGetLastError();
+}
+
 // Segments above kGridNNMin points: one thread per point, k-NN by the exact grid shell search
 template <int KMAX>
 __global__ void __launch_bounds__(kGThreads) covariance_grid_kernel(const float4* pts, int off, int n,

@@ -233,6 +233,9 @@ hipError_t launch_render_cloud(const FusedArgs& a, hipStream_t s);
 // brute-force k-NN covariances, one workgroup per segment; segments above max_n points are skipped
 hipError_t launch_covariances(const float4* pts, const int32_t* seg_off, const int32_t* seg_cnt, int seg_stride,
                               int num_segs, int k, double* cov_out, hipStream_t s, int max_n = 0x7fffffff);
+// the rendered ICP clouds' covariances, k = 10, by pcore_cov.h's threshold k-NN (seg i at pts + i * seg_stride)
+hipError_t launch_covariances_cloud(const float4* pts, const int32_t* seg_cnt, int seg_stride, int num_segs,
+                                    float fx, float fy, float cx, float cy, int stride, double* cov_out, hipStream_t s);
 // covariances of the segments above kGridNNMin points via their grids (grids[first_grid + seg]), one
 // thread per point; seg_off_host / seg_cnt_host: host copies of the segment table
 hipError_t launch_covariances_grid(const float4* pts, const int32_t* seg_off_host, const int32_t* seg_cnt_host,

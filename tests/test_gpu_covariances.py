@@ -62,3 +62,48 @@ def test_gpu_covariances_equal_oracle_bitwise(k):
     for s, o, c in zip(segs, off, cnt):
         want = oracle.covariances(s, k)
         assert _same(got[o:o + c], want), (len(s), k)
+
+
+def _grid_clouds():
+    """Clouds unprojected from a stride-8 sample grid of the 640x480 camera (what render_cloud writes): tilted planes,
+    a sphere cap and a step (a depth discontinuity inside the neighbourhoods), 20 to 467 points."""
+    from perception_amd import synthetic as syn
+    cam, s = syn.CAM_640, 8
+    rng = np.random.default_rng(9)
+    clouds = []
+    for (w, h, x0, y0) in ((12, 10, 30, 20), (23, 20, 10, 5), (8, 3, 50, 40), (27, 17, 3, 30)):
+        kx, ky = np.meshgrid(np.arange(x0, x0 + w), np.arange(y0, y0 + h))
+        u, v = kx * s, ky * s
+        z = 0.8 + 0.0004 * (u - 320) + 0.0003 * (v - 240) + rng.normal(size=u.shape) * 1e-3
+        if w == 27:
+            z = np.where(kx > x0 + 13, z + 0.05, z)  # a step: the far side's neighbourhoods reach across it
+        z = np.round(z * 100) / 100  # the int-centimetre z-buffer's depths
+        x = ((u.astype(np.float32) - np.float32(cam["cx"])) / np.float32(cam["fx"]) * z.astype(np.float32))
+        y = ((v.astype(np.float32) - np.float32(cam["cy"])) / np.float32(cam["fy"]) * z.astype(np.float32))
+        clouds.append(np.stack([x, y, z.astype(np.float32)], -1).reshape(-1, 3).astype(np.float32))
+    return clouds, cam, s
+
+
+def test_gpu_threshold_knn_covariances_equal_oracle_bitwise():
+    """covariance_cloud_kernel (the threshold k-NN over each rendered cloud's sample grid, pcore_cov.h; k = 10) bit for
+    bit against the oracle: on grid-structured clouds (the path it serves) and on every segment of the brute-force test
+    (no grid structure, lattices with ties, duplicates, n < k, a NaN point: the threshold stays a valid bound or the
+    kernel falls back), each in a slot of a strided buffer as the ICP scratch holds them."""
+    grid, cam, s = _grid_clouds()
+    segs = grid + _segments()
+    cap = max(len(x) for x in segs)
+    xyzw = np.zeros((len(segs) * cap, 4), np.float32)
+    for i, x in enumerate(segs):
+        xyzw[i * cap:i * cap + len(x), :3] = x
+    cnt = np.array([len(x) for x in segs], np.int32)
+    dev = torch.device("cuda", 0)
+    pts = torch.from_numpy(xyzw).to(dev)
+    cnt_d = torch.from_numpy(cnt).to(dev)
+    out = torch.full((len(segs) * cap, 6), float("nan"), dtype=torch.float64, device=dev)
+    lib = _native.load()
+    assert lib.pcore_debug_covariances_cloud(pts.data_ptr(), cnt_d.data_ptr(), cap, len(segs), cam["fx"], cam["fy"],
+                                             cam["cx"], cam["cy"], s, out.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for i, x in enumerate(segs):
+        assert _same(got[i * cap:i * cap + len(x)], oracle.covariances(x, 10)), (i, len(x))
