@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpcore.so")
 SOURCES = ["pcore_kernels.hip", "pcore_gicp.hip", "pcore_metrics.hip", "pcore_states.hip", "pcore_api.hip"]
-HEADERS = ["pcore_internal.h", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h", os.path.join("..", "..", "include", "pcore.h")]
+HEADERS = ["pcore_internal.h", "pcore_cov.h", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h", os.path.join("..", "..", "include", "pcore.h")]
 ARCH = os.environ.get("PCORE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -43,7 +43,7 @@ def kernel_source_digest() -> str:
     import hashlib
 
     h = hashlib.sha256(" ".join(flags()).encode())  # the compile flags too: a profile is of one build
-    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h"):
+    for f in ("pcore_kernels.hip", "pcore_internal.h", "pcore_cov.h", "pcore_colour.h", "pcore_fdiv.h", "pcore_streams.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
@@ -55,7 +55,7 @@ def gicp_source_digest() -> str:
     import hashlib
 
     h = hashlib.sha256(" ".join(flags()).encode())
-    for f in ("pcore_gicp.hip", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_internal.h"):
+    for f in ("pcore_gicp.hip", "pcore_cov.h", "pcore_gicp_math.h", "pcore_dmath.h", "pcore_internal.h"):
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

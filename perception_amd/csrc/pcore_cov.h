@@ -225,6 +225,9 @@ struct CovGrid {
 constexpr int kThrMap = 1536;  // window cells of the map (ushort point index each; 0xffff = empty)
 constexpr int kThrCap = 24;    // collected candidates per lane
 constexpr int kThrR = 3;       // the neighbourhood: (2 kThrR + 1)^2 cells
+#ifndef PCORE_THR_UNROLL
+#define PCORE_THR_UNROLL 7  // a neighbourhood row per loop trip: its map reads and point loads issue together
+#endif
 constexpr size_t kThrLdsBytes = kThrMap * 2 + (size_t)kThrCap * kCovLanes * 2 + kCovLanes * 16;
 
 __device__ __forceinline__ void cov_cell(const float4& p, const CovGrid& cg, int& kx, int& ky) {
@@ -293,6 +296,7 @@ __device__ __forceinline__ bool cov_knn_round_thr(const float4* P, int n, int i0
     cov_cell(xi, cg, kx, ky);
     for (int dv = -kThrR; dv <= kThrR; dv++) {
         const int cy = ky + dv - ky0;
+#pragma unroll PCORE_THR_UNROLL
         for (int du = -kThrR; du <= kThrR; du++) {
             const int cx = kx + du - kx0;
             const bool in = act && cx >= 0 && cx < wx && cy >= 0 && cy < wy;

@@ -10,12 +10,13 @@ for SET in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH GR
   i=$((i+1))
 done
 python - "$OUT" <<'PY'
-import csv, glob, json, sys
+import csv, glob, json, os, sys
+KPAT = os.environ.get("KPAT", "covariance_cloud_kernel")
 out = sys.argv[1]
 v = {}
 for p in sorted(glob.glob(out + "/cov_*/run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
-        if "covariance_kernel<10, true>" in r["Kernel_Name"] and int(r["Grid_Size"]) >= 64 * 40000:
+        if KPAT in r["Kernel_Name"] and int(r["Grid_Size"]) >= 64 * 40000:
             v.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 m = {k: sum(x) / len(x) for k, x in v.items()}
 if "SQ_INSTS_VALU" in m and "GRBM_GUI_ACTIVE" in m:
