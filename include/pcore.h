@@ -250,6 +250,11 @@ int pcore_debug_covariances(const float* d_xyzw, const int32_t* d_seg_off, const
 int pcore_debug_covariances_cloud(const float* d_xyzw, const int32_t* d_seg_cnt, int32_t seg_stride, int32_t num_segs,
                                   float fx, float fy, float cx, float cy, int32_t stride, double* d_out_cov6,
                                   pcore_stream stream);
+/* Test hook (no reference counterpart): the last pcore_evaluate_icp call's GICP help board counters (DESIGN.md
+ * section 4, the queue-dry tail): out4 = rounds of 64 correspondences searched by helper waves, owner timeouts
+ * (rounds a late helper left to the owner), helper give-ups, poses registered for help.  Waits for the call's last
+ * GICP launch. */
+int pcore_debug_gicp_help_stats(pcore_ctx* c, int64_t* out4);
 
 /* GenerateSuccessorStates / GetStateImagesUnifiedGPU host work on the device (search_env.cpp:7056-7254,
  * 1535-1576), for the drop-in recognizer's states:

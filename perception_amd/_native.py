@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "pcore_depth_to_cloud", "pcore_select", "pcore_pose_distances",
     "pcore_observed_cloud_bounded", "pcore_set_observation_colors", "pcore_generation", "pcore_get_stats",
     "pcore_count_within", "pcore_state_poses", "pcore_evaluate_select", "pcore_get_tile_info", "pcore_debug_lm_solve",
-    "pcore_debug_covariances", "pcore_debug_covariances_cloud", "pcore_depth_to_cloud_ex",
+    "pcore_debug_covariances", "pcore_debug_covariances_cloud", "pcore_debug_gicp_help_stats", "pcore_depth_to_cloud_ex",
 )
 
 
@@ -134,6 +134,8 @@ def load(auto_build: bool = True) -> ctypes.CDLL:
         L.pcore_debug_lm_solve.argtypes = [vp, vp, vp, i32, vp]
     if hasattr(L, "pcore_debug_covariances"):
         L.pcore_debug_covariances.argtypes = [vp, vp, vp, i32, i32, vp, vp]
+    if hasattr(L, "pcore_debug_gicp_help_stats"):
+        L.pcore_debug_gicp_help_stats.argtypes = [vp, vp]
     if hasattr(L, "pcore_debug_covariances_cloud"):
         f32 = ctypes.c_float
         L.pcore_debug_covariances_cloud.argtypes = [vp, vp, i32, i32, f32, f32, f32, f32, i32, vp, vp]

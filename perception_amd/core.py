@@ -267,6 +267,13 @@ class PoseCore:
                 "icp_chunks": st.icp_chunks, "gicp_iterations": st.gicp_iterations,
                 "gicp_iterations_run": st.gicp_iterations_run, "gicp_cycle_exits": st.gicp_cycle_exits}
 
+    def gicp_help_stats(self) -> dict:
+        """pcore_debug_gicp_help_stats: the last evaluate_icp's GICP help board counters."""
+        out = (ctypes.c_int64 * 4)()
+        self._check(self.lib.pcore_debug_gicp_help_stats(self._h, out))
+        return {"helper_rounds": int(out[0]), "owner_timeouts": int(out[1]), "helper_giveups": int(out[2]),
+                "poses_enlisted": int(out[3])}
+
     def tile_info(self) -> dict:
         """pcore_get_tile_info: the fused window launch's tile tier and the last published window histogram."""
         ti = _native.TileInfo()

@@ -83,7 +83,10 @@ struct pcore_ctx {
     DevBuf<int32_t> icp_corr_hist;  // GicpArgs::corr_hist
     DevBuf<double> icp_mahal;   // GicpArgs::mahal
     DevBuf<int32_t> icp_counter;
-    DevBuf<unsigned long long> icp_iter_stats;  // GicpArgs::iter_stats, zeroed per pcore_evaluate_icp
+    DevBuf<unsigned long long> icp_iter_stats;  // GicpArgs::iter_stats ([0..3]) and help_stats ([4..7]), zeroed per call
+    DevBuf<unsigned> icp_help_ctl;              // GicpArgs::help_ctl (zeroed per launch by launch_gicp)
+    DevBuf<unsigned long long> icp_help_gran;   // GicpArgs::help_gran
+    uint32_t icp_help_tag = 0;                  // GicpArgs::help_tag of the last launch (1..0xFFFF, cycling)
     // their copy in pinned host memory, made on the call's stream before each chunk's end event (pcore_get_stats reads
     // it after that event: no synchronous copy, which would wait for every blocking stream of the device)
     unsigned long long* icp_iter_stats_host = nullptr;
@@ -322,7 +325,7 @@ void pcore_destroy(pcore_ctx* c) {
     (void)dev_free(c->scratch_counts); (void)dev_free(c->scratch_offsets); (void)dev_free(c->scratch_total);
     (void)dev_free(c->tgt); (void)dev_free(c->seg_lo); (void)dev_free(c->seg_hi); (void)dev_free(c->seg_cnt); (void)dev_free(c->tgt_quads); (void)dev_free(c->seg_qoff);
     (void)dev_free(c->tgt_cov_label); (void)dev_free(c->tgt_cov_all);
-    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->scratch_dc_pre); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_iter_stats); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
+    (void)dev_free(c->icp_cloud); (void)dev_free(c->icp_count); (void)dev_free(c->icp_cov); (void)dev_free(c->icp_corr); (void)dev_free(c->icp_corr_hist); (void)dev_free(c->scratch_dc_pre); (void)dev_free(c->icp_mahal); (void)dev_free(c->icp_counter); (void)dev_free(c->icp_iter_stats); (void)dev_free(c->icp_help_ctl); (void)dev_free(c->icp_help_gran); (void)dev_free(c->icp_order_keys); (void)dev_free(c->icp_order_idx); (void)dev_free(c->icp_order_temp);
     (void)dev_free(c->stri_orig); (void)dev_free(c->tri_lab); (void)dev_free(c->obs_lab); (void)dev_free(c->colour_id);
     (void)dev_free(c->metric_part); (void)dev_free(c->tri_rgb); (void)dev_free(c->render_tri);
     for (hipEvent_t e : c->icp_ev) (void)hipEventDestroy(e);
@@ -990,9 +993,18 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     if (use_hist) HIPC(c, dev_reserve(c->icp_corr_hist, (size_t)chunk * kCorrHist * hist_cap));
     HIPC(c, dev_reserve(c->icp_mahal, (size_t)6 * chunk * nsamp));
     HIPC(c, dev_reserve(c->icp_counter, 4));  // [0] one-wave queue, [1] heavy queue, [2] heavy poses
-    HIPC(c, dev_reserve(c->icp_iter_stats, 4));
+    HIPC(c, dev_reserve(c->icp_iter_stats, 8));
     if (!c->icp_iter_stats_host)
-        HIPC(c, hipHostMalloc((void**)&c->icp_iter_stats_host, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+        HIPC(c, hipHostMalloc((void**)&c->icp_iter_stats_host, 8 * sizeof(unsigned long long), hipHostMallocDefault));
+    // the GICP help board (a -DPCORE_GICP_HELP_BOARD=1 build): a slot per resident wave, at most 512 MiB of granules
+    // (PCORE_GICP_HELP=0: no help, A/B)
+    int help_slots = 0;
+    if (kGicpHelpBoard && !(getenv("PCORE_GICP_HELP") && atoi(getenv("PCORE_GICP_HELP")) == 0)) {
+        const size_t per_slot = (size_t)(kHelpXfGranules + nsamp) * sizeof(unsigned long long);
+        help_slots = (int)std::min<size_t>((size_t)std::max(1, c->dinfo.gicp_resident_wgs), ((size_t)512 << 20) / per_slot);
+        HIPC(c, dev_reserve(c->icp_help_ctl, help_ctl_words(help_slots)));
+        HIPC(c, dev_reserve(c->icp_help_gran, (size_t)help_slots * (kHelpXfGranules + nsamp)));
+    }
     HIPC(c, dev_reserve(c->icp_order_keys, (size_t)2 * chunk));
     HIPC(c, dev_reserve(c->icp_order_idx, (size_t)2 * chunk));
     const size_t order_temp = gicp_order_temp_bytes(chunk);
@@ -1009,7 +1021,7 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     HIPC(c, hipStreamIsCapturing(s, &cap_status));
     const bool timed = cap_status == hipStreamCaptureStatusNone;
     c->icp_ev_used = 0;
-    HIPC(c, hipMemsetAsync(c->icp_iter_stats.p, 0, 4 * sizeof(unsigned long long), s));
+    HIPC(c, hipMemsetAsync(c->icp_iter_stats.p, 0, 8 * sizeof(unsigned long long), s));
     while (timed && c->icp_ev.size() < (size_t)3 * nchunks) {
         hipEvent_t e;
         HIPC(c, hipEventCreate(&e));
@@ -1048,6 +1060,10 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
     if (const char* e = getenv("PCORE_GICP_HEAVY_MAX")) g.heavy_max = atoi(e);
     g.cycle_window = ip->cycle_exit_window;
     g.iter_stats = c->icp_iter_stats.p;
+    g.help_ctl = help_slots > 0 ? c->icp_help_ctl.p : nullptr;
+    g.help_gran = help_slots > 0 ? c->icp_help_gran.p : nullptr;
+    g.help_stats = c->icp_iter_stats.p + 4;
+    g.help_slots = help_slots;
     g.tgt_quads = c->tgt_quads.p;
     g.seg_qoff = c->seg_qoff.p;
     g.grids = c->grids.p;
@@ -1101,10 +1117,12 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
                                       c->icp_order_idx.p + chunk, c->icp_order_temp.p, order_temp, s));
             g.pose_order = c->icp_order_idx.p + chunk;
         }
+        c->icp_help_tag = c->icp_help_tag % 0xFFFFu + 1u;  // a new tag for every launch on this context's board
+        g.help_tag = c->icp_help_tag;
         if (ev) HIPC(c, hipEventRecord(ev[1], s));
         HIPC(c, launch_gicp(g, n, c->dinfo, s, grid_needed));
         if (ev)  // the counters so far (the last chunk's copy holds the call's totals)
-            HIPC(c, hipMemcpyAsync(c->icp_iter_stats_host, c->icp_iter_stats.p, 4 * sizeof(unsigned long long),
+            HIPC(c, hipMemcpyAsync(c->icp_iter_stats_host, c->icp_iter_stats.p, 8 * sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, s));
         if (ev) {
             HIPC(c, hipEventRecord(ev[2], s));
@@ -1174,6 +1192,16 @@ int pcore_get_stats(pcore_ctx* c, pcore_gpu_stats* out, int32_t reset) {
     out->gicp_iterations_run = (int64_t)it[1];
     out->gicp_cycle_exits = (int64_t)it[2];
     if (reset) c->peak_mem_mb = 0.0;
+    return PCORE_OK;
+}
+
+int pcore_debug_gicp_help_stats(pcore_ctx* c, int64_t* out4) {
+    if (!c || !out4) return PCORE_E_INVALID_ARG;
+    HIPC(c, hipSetDevice(c->device));
+    for (int i = 0; i < 4; i++) out4[i] = 0;
+    if (c->icp_ev_used <= 0 || !c->icp_iter_stats_host) return PCORE_OK;
+    HIPC(c, hipEventSynchronize(c->icp_ev[3 * (c->icp_ev_used - 1) + 2]));  // after the last chunk's copy
+    for (int i = 0; i < 4; i++) out4[i] = (int64_t)c->icp_iter_stats_host[4 + i];
     return PCORE_OK;
 }
 

@@ -1074,6 +1074,308 @@ __device__ __forceinline__ void coop_pose(const GicpArgs& g, const GicpPose& P, 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// The help board (GicpArgs::help_*; VERDICT r05 next #5, the launch's queue-dry tail).  Once the pose queue has run
+// dry, the waves that find it empty become helpers, and the waves still refining a pose of kHelpMinRounds or more
+// rounds of 64 source points (each looks at the board's dry word every iteration: one load, read an iteration later)
+// list themselves on the board.  The first helper to enlist a listed pose zeroes its slot's granules and raises the
+// slot's flag; from the next iteration on the owner shares each searching iteration's correspondence search with up to
+// rounds - 1 helpers, by rounds of 64 points (help_search, help_attached).  A wave's slot is its workgroup index.
+// Hand-offs between workgroups take the R2 form of cdna_hip_programming.md section 6, guideline 16: every shared value
+// travels in an 8-byte granule {tag, value} written by one agent-scope atomic store and polled by agent-scope atomic
+// loads until its tag matches, so no fence is needed.  A tag is the launch's tag (GicpArgs::help_tag) and the epoch: a
+// wave that has seen the queue dry takes no further pose, so a slot is helped for one pose at most, and the epoch of
+// the pose's iteration `it` is it + 1, so epochs only grow.  The results are the owner's own search's bit for bit: a
+// helper runs the same float queries (the published bits) through the same scan.  Every wait is bounded
+// (kHelpTimeoutTicks of the 100 MHz clock): an owner whose helper is late searches that round itself, a helper whose
+// owner has moved on gives up, and every helper leaves once all of the launch's poses are written (or after
+// kHelpLifeTicks).  Measured: owners that registered from every fourth iteration with a zeroing loop of their own cost
+// the iteration loop 8 VGPRs; helpers that scanned every wave's posted pose instead of a list slowed the launch.
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr unsigned long long kHelpTimeoutTicks = 200000;   // 2 ms
+constexpr unsigned long long kHelpLifeTicks = 100000000;  // 1 s
+#ifndef PCORE_HELP_MIN_ROUNDS
+#define PCORE_HELP_MIN_ROUNDS 3
+#endif
+constexpr int kHelpMinRounds = PCORE_HELP_MIN_ROUNDS;  // two rounds: one helper saves about what the hand-offs cost
+
+
+__device__ __forceinline__ unsigned hb_load(const unsigned* p) {
+    return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long hb_load64(const unsigned long long* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void hb_store(unsigned* p, unsigned v) {
+    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void hb_store64(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned hb_add(unsigned* p, unsigned v) {
+    return __hip_atomic_fetch_add((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The board's arguments, read from the kernarg segment where they are used (behind an opaque offset): as kernel
+// arguments held in registers they were live through the whole persistent loop, for code that runs in the tail only.
+struct HelpRef {
+    unsigned* ctl;
+    unsigned long long* gran;
+    unsigned long long* stats;
+    int slots, cap;
+    unsigned tag;  // the launch's tag (GicpArgs::help_tag, 1..0xFFFF)
+};
+__device__ __forceinline__ HelpRef help_ref() {
+    typedef __attribute__((address_space(4))) const GicpArgs kargs_t;
+    typedef __attribute__((address_space(4))) const char kbytes_t;
+    kargs_t* a = (kargs_t*)((kbytes_t*)__builtin_amdgcn_kernarg_segment_ptr() + opaque_zero());  // gicp_kernel's g
+    return {a->help_ctl, a->help_gran, a->help_stats, a->help_slots, a->src_cap, a->help_tag};
+}
+__device__ __forceinline__ void hb_count(const HelpRef& h, int k) {
+    if (h.stats) __hip_atomic_fetch_add((gu64*)(h.stats + k), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// control words after [0] dry, [1] poses finished, [2] poses listed, [3] unused: per list entry the listed slot
+// ((rounds << 24) | (slot + 1)) and its helpers (kHelpFull once its pose is done); per slot its claim word and flag
+constexpr unsigned kHelpFull = 0xFFFFu;
+__device__ __forceinline__ int hb_stride(const HelpRef& h) { return (h.slots + 3) & ~3; }
+__device__ __forceinline__ unsigned* hb_list(const HelpRef& h) { return h.ctl + 4; }
+__device__ __forceinline__ unsigned* hb_helpers(const HelpRef& h) { return h.ctl + 4 + hb_stride(h); }
+__device__ __forceinline__ unsigned* hb_claim(const HelpRef& h) { return h.ctl + 4 + 2 * hb_stride(h); }
+__device__ __forceinline__ unsigned* hb_flag(const HelpRef& h) { return h.ctl + 4 + 3 * hb_stride(h); }
+__device__ __forceinline__ unsigned long long* hb_gran(const HelpRef& h, int slot) {
+    return h.gran + (size_t)slot * (kHelpXfGranules + h.cap);
+}
+__device__ __forceinline__ unsigned long long hb_now() { return __builtin_amdgcn_s_memrealtime(); }
+// a granule's tag: the launch's tag and the epoch (a granule left by an earlier launch never matches)
+__device__ __forceinline__ unsigned hb_tag(const HelpRef& h, unsigned e) { return (h.tag << 16) | e; }
+
+// round r's correspondences (point 64 r + lane), exactly as the iteration's own search finds them
+__device__ __forceinline__ int help_round_scan(const GicpPose& P, int r, const float (&Rf)[3][3], const float (&tf)[3],
+                                               int lane) {
+    const int i = 64 * r + lane;
+    int j = -1;
+    if (i < P.ns) {
+        const float4 sp = P.src[i];
+        float q[3];
+        gicpm::query_f(Rf, tf, sp.x, sp.y, sp.z, q);
+        float best = INFINITY;
+        scan_quads(P.tquads, P.nt, q[0], q[1], q[2], best, j);
+    }
+    return j;
+}
+
+// The owner's side before its pose is shared, once an iteration (hstate: -1 = watching the dry word, -3 = listed,
+// watching its flag; >= 0 = the slot, shared).  `hv` is the word loaded at the previous iteration (read here, so its
+// latency hides behind an iteration), reloaded for the next one.
+__device__ __forceinline__ void help_watch(int& hstate, unsigned& hv, int np, int lane) {
+    const HelpRef g = help_ref();
+    const int w = blockIdx.x;
+    if (__builtin_amdgcn_readfirstlane(hv)) {
+        if (hstate == -3) {  // enlisted: the slot's granules are zeroed
+            hstate = w;
+            return;
+        }
+        if (w >= g.slots) {  // no slot of its own (a board smaller than the launch)
+            hstate = -2;
+            return;
+        }
+        unsigned k = 0;  // the queue ran dry: list the pose
+        if (lane == 0) k = hb_add(g.ctl + 2, 1u);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if ((int)k >= g.slots) {
+            hstate = -2;
+            return;
+        }
+        if (lane == 0) hb_store(hb_list(g) + k, ((unsigned)np << 24) | (unsigned)(w + 1));
+        hstate = -3;
+        hv = 0u;
+    }
+    if (lane == 0) hv = hb_load(hstate == -3 ? hb_flag(g) + w : g.ctl);
+}
+
+// An enlisted pose's search of one iteration (epoch e) into cset: the transform published in the slot's granules,
+// round 0 searched by the owner, every further round claimed from the slot's counter by whoever asks first (the
+// owner included); the rounds helpers took are read from their granules.
+__device__ __forceinline__ void help_search(const GicpPose& P, int s, unsigned e, const float (&Rf)[3][3],
+                                            const float (&tf)[3], int32_t* cset, int lane) {
+    const HelpRef g = help_ref();
+    const int npass = (P.ns + 63) >> 6;
+    unsigned long long* gr = hb_gran(g, s);
+    unsigned* claim = hb_claim(g) + s;
+    const unsigned long long T = (unsigned long long)hb_tag(g, e) << 32;
+    if (lane < 4) {  // granule 3 r + c: row r of R (r = 3: t), as xf_lane_words lays them out (no indexed selects)
+        unsigned b0, b1, b2;
+        xf_lane_words(Rf, tf, lane, b0, b1, b2);
+        hb_store64(gr + 3 * lane, T | b0);
+        hb_store64(gr + 3 * lane + 1, T | b1);
+        hb_store64(gr + 3 * lane + 2, T | b2);
+    } else if (lane < 6) {  // granules 12, 13: the pose and its rounds
+        hb_store64(gr + 8 + lane, T | (lane == 4 ? (unsigned)P.pose + 1u : (unsigned)npass));
+    }
+    if (lane == 0) hb_store(claim, (e << 16) | 1u);  // round 0 is the owner's
+    unsigned long long mine0 = 0ull, mine1 = 0ull;
+    int c = 0;
+    for (;;) {
+        const int j = help_round_scan(P, c, Rf, tf, lane);
+        if (64 * c + lane < P.ns) cset[64 * c + lane] = j;
+        if (c < 64) mine0 |= 1ull << c;
+        else mine1 |= 1ull << (c - 64);
+        unsigned old = 0;
+        if (lane == 0) old = hb_add(claim, 1u);
+        old = __builtin_amdgcn_readfirstlane(old);
+        if ((old >> 16) != e || (int)(old & 0xffffu) >= npass) break;
+        c = (int)(old & 0xffffu);
+    }
+    for (int r = 1; r < npass; r++) {
+        if (((r < 64 ? mine0 >> r : mine1 >> (r - 64)) & 1ull) != 0ull) continue;
+        const int i = 64 * r + lane;
+        const bool act = i < P.ns;
+        const unsigned long long t0 = hb_now();
+        unsigned long long v = 0ull;
+        bool got = false;
+        for (;;) {
+            if (act) v = hb_load64(gr + kHelpXfGranules + i);
+            if (__ballot(act && (v >> 32) != (T >> 32)) == 0ull) {
+                got = true;
+                break;
+            }
+            if (hb_now() - t0 > kHelpTimeoutTicks) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (got) {
+            if (act) cset[i] = (int32_t)(unsigned)v;
+        } else {  // the helper is late: the owner searches the round (the same correspondences)
+            const int j = help_round_scan(P, r, Rf, tf, lane);
+            if (act) cset[i] = j;
+            if (lane == 0) hb_count(g, 1);
+        }
+    }
+}
+
+// A helper attached to slot s: claims rounds of the published epochs until the pose is done.
+__device__ __forceinline__ void help_attached(const GicpArgs& ga, const HelpRef& g, int s, int np, int lane,
+                                              unsigned long long born) {
+    unsigned long long* gr = hb_gran(g, s);
+    unsigned* claim = hb_claim(g) + s;
+    for (;;) {
+        unsigned w = 0;
+        if (lane == 0) w = hb_load(claim);
+        w = __builtin_amdgcn_readfirstlane(w);
+        if ((w >> 16) == 0xFFFFu || hb_now() - born > kHelpLifeTicks) return;
+        if ((w >> 16) == 0u || (int)(w & 0xffffu) >= np) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        if (lane == 0) w = hb_add(claim, 1u);
+        w = __builtin_amdgcn_readfirstlane(w);
+        const unsigned e = w >> 16;
+        const int c = (int)(w & 0xffffu);
+        if (e == 0u || e == 0xFFFFu || c >= np) continue;
+        // the transform and pose of epoch e (their granules may land after the claim word)
+        const unsigned T = hb_tag(g, e);
+        const unsigned long long t0 = hb_now();
+        unsigned bits = 0;
+        bool ok = false;
+        for (;;) {
+            unsigned long long v = 0ull;
+            if (lane < 14) v = hb_load64(gr + lane);
+            const unsigned tag = (unsigned)(v >> 32);
+            // the owner has moved on (this launch's tag, a later epoch)
+            if (__ballot(lane < 14 && (tag >> 16) == g.tag && (tag & 0xffffu) > e) != 0ull) break;
+            if (__ballot(lane < 14 && tag != T) == 0ull) {
+                bits = (unsigned)v;
+                ok = true;
+                break;
+            }
+            if (hb_now() - t0 > kHelpTimeoutTicks) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok) {
+            if (lane == 0) hb_count(g, 2);
+            continue;
+        }
+        float Rf[3][3], tf[3];
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+#pragma unroll
+            for (int b = 0; b < 3; b++) Rf[a][b] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 3 * a + b));
+            tf[a] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 9 + a));
+        }
+        const GicpPose P = gicp_pose(ga, (int)__builtin_amdgcn_readlane(bits, 12) - 1);
+        const int j = help_round_scan(P, c, Rf, tf, lane);
+        if (64 * c + lane < P.ns)
+            hb_store64(gr + kHelpXfGranules + 64 * c + lane, ((unsigned long long)T << 32) | (unsigned)j);
+        if (lane == 0) hb_count(g, 0);
+    }
+}
+
+// A wave whose queue ran dry: marks the queue dry, then helps listed poses (a pose of np rounds takes np - 1 helpers;
+// the first to enlist zeroes the slot's granules, drains the stores, then raises the flag) until every pose of the
+// launch is written.
+__device__ __forceinline__ void help_loop(const GicpArgs& ga, int num_poses, int lane) {
+    const HelpRef g = help_ref();
+    if (lane == 0) hb_store(g.ctl, 1u);
+    const unsigned long long born = hb_now();
+    const unsigned* list = hb_list(g);
+    unsigned* helpers = hb_helpers(g);
+    for (;;) {
+        unsigned fin = 0, nl = 0;
+        if (lane == 0) {
+            fin = hb_load(g.ctl + 1);
+            nl = hb_load(g.ctl + 2);
+        }
+        fin = __builtin_amdgcn_readfirstlane(fin);
+        const int n = min((int)__builtin_amdgcn_readfirstlane(nl), g.slots);
+        if ((int)fin >= num_poses || hb_now() - born > kHelpLifeTicks) return;
+        int slot = -1, np = 0;
+        for (int b = 0; b < n && slot < 0; b += 64) {
+            const int k = b + lane;
+            unsigned e = 0, h = kHelpFull;
+            if (k < n) {
+                e = hb_load(list + k);
+                h = hb_load(helpers + k);
+            }
+            const int npk = (int)(e >> 24);
+            unsigned long long m = __ballot(e != 0u && h != kHelpFull && (int)h < npk - 1);
+            while (m != 0ull) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const unsigned el = __builtin_amdgcn_readlane(e, l);
+                const int npl = (int)(el >> 24), sl = (int)(el & 0xFFFFFFu) - 1;
+                unsigned cw = 0;  // a pose that is done: its entry marked full for everyone
+                if (lane == 0) cw = hb_load(hb_claim(g) + sl);
+                if ((__builtin_amdgcn_readfirstlane(cw) >> 16) == 0xFFFFu) {
+                    if (lane == 0) hb_store(helpers + b + l, kHelpFull);
+                    continue;
+                }
+                unsigned got = 0;
+                if (lane == 0) got = hb_add(helpers + b + l, 1u);
+                got = __builtin_amdgcn_readfirstlane(got);
+                if ((int)got < npl - 1) {
+                    slot = sl;
+                    np = npl;
+                    if (got == 0u) {  // the first helper: the slot's granules zeroed and drained, then the flag
+                        unsigned long long* gr = hb_gran(g, slot);
+                        if (lane < kHelpXfGranules) hb_store64(gr + lane, 0ull);
+                        for (int i = lane; i < 64 * np; i += 64) hb_store64(gr + kHelpXfGranules + i, 0ull);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) {
+                            hb_store(hb_flag(g) + slot, 1u);
+                            hb_count(g, 3);
+                        }
+                    }
+                    break;
+                }
+            }
+        }
+        if (slot < 0) {
+            __builtin_amdgcn_s_sleep(127);
+            continue;
+        }
+        help_attached(ga, g, slot, np, lane, born);
+    }
+}
+
 // One wave per pose; persistent waves pull poses from a counter.  Each iteration linearises in rounds of 64
 // source points (point i -> lane i % 64, contributions added in point order), reduces the 28 terms by the
 // shuffle-down tree in registers and runs the LM iteration on the wave.  The per-pose iteration chain is
@@ -1175,6 +1477,13 @@ gicp_kernel(GicpArgs g, int num_poses) {
         unsigned long long kept = 0ull;
         int ring = 0;
         const int sub = lane & 3;
+        // the help board (one-wave workgroups; help_watch): -2 = no help, -1 / -3 = watching, else the slot
+        int hslot = -2;
+        unsigned hv = 0u;  // the board word loaded at an iteration's top, read at the next one's
+        if constexpr (kGicpHelpBoard && NW == 1 && !GRID)  // the grid instance keeps its registers for the search
+            if (P.ns > 64 * (kHelpMinRounds - 1) && P.ns <= 64 * kHelpMaxRounds && !P.use_grid && g.max_iter < 0xFFFF &&
+                help_ref().ctl)
+                hslot = -1;
         if (P.ns > 0 && P.nt > 0) {
             for (int it = 0; it < g.max_iter; it++) {
                 iters++;
@@ -1205,6 +1514,11 @@ gicp_kernel(GicpArgs g, int num_poses) {
                         }
                     }
                     cset = hbase + (size_t)__builtin_amdgcn_readfirstlane(e) * g.corr_hist_cap;
+                }
+                if (hslot == -1 || hslot == -3) help_watch(hslot, hv, (P.ns + 63) >> 6, lane);
+                if (hslot >= 0 && !reuse) {  // the search shared with the helpers; the contributions read cset
+                    help_search(P, hslot, (unsigned)it + 1u, Rf, tf, cset, lane);
+                    reuse = true;
                 }
 #ifdef PCORE_GICP_PROFILE
                 gp_acc[8] += reuse ? 1ull : 0ull;
@@ -1287,6 +1601,13 @@ gicp_kernel(GicpArgs g, int num_poses) {
         if (lane == 0) {
             write_pose(g, P.gp, x, iters);
             count_iterations(g, iters, iters_run ? iters_run : iters, iters_run != 0);
+            if (kGicpHelpBoard && NW == 1 && !GRID) {
+                const HelpRef h = help_ref();
+                if (h.ctl) {
+                    if (hslot >= 0 || hslot == -3) hb_store(hb_claim(h) + blockIdx.x, kHelpClosed);
+                    hb_add(h.ctl + 1, 1u);  // poses finished (the helpers leave at num_poses)
+                }
+            }
         }
 #ifdef PCORE_GICP_TIMELINE
         if (lane == 0 && P.gp < kTlPoses) {
@@ -1296,6 +1617,8 @@ gicp_kernel(GicpArgs g, int num_poses) {
         }
 #endif
     }
+    if constexpr (kGicpHelpBoard && NW == 1 && !GRID)
+        if (help_ref().ctl) help_loop(g, num_poses, lane);
     GPROF_FLUSH;
 #ifdef PCORE_GICP_TIMELINE
     if (lane == 0) {
@@ -1444,10 +1767,14 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hi
         return hipGetLastError();
     }
     const dim3 wgs(std::min(resident_wgs, (num_poses + kGicpWgWaves - 1) / kGicpWgWaves)), block(64 * kGicpWgWaves);
+    GicpArgs ga = g;
+    if (!kGicpHelpBoard || kGicpWgWaves != 1 || grid) ga.help_ctl = nullptr;  // the one-wave grid-free instance only
+    if (ga.help_ctl && (e = hipMemsetAsync(ga.help_ctl, 0, help_ctl_words(ga.help_slots) * sizeof(unsigned), s)) != hipSuccess)
+        return e;
     if (grid)
-        hipLaunchKernelGGL((gicp_kernel<true, kGicpWgWaves>), wgs, block, 0, s, g, num_poses);
+        hipLaunchKernelGGL((gicp_kernel<true, kGicpWgWaves>), wgs, block, 0, s, ga, num_poses);
     else
-        hipLaunchKernelGGL((gicp_kernel<false, kGicpWgWaves>), wgs, block, 0, s, g, num_poses);
+        hipLaunchKernelGGL((gicp_kernel<false, kGicpWgWaves>), wgs, block, 0, s, ga, num_poses);
     return hipGetLastError();
 }
 

@@ -190,7 +190,33 @@ struct GicpArgs {
     int32_t* heavy_count;
     long long heavy_cost;
     int32_t heavy_max;
+    // the help board (gicp_kernel, one-wave workgroups; pcore_gicp.hip): once the pose queue runs dry, the waves that
+    // find it empty help the waves still refining large poses with their correspondence searches.  help_ctl (zeroed per
+    // launch, help_ctl_words): [0] queue dry, [1] poses finished, [2] poses listed, [3] unused, then help_slots
+    // entries each of the list, its helpers, the claim words and the flags.  help_gran per slot (= workgroup): 16
+    // granules {tag, value} of the transform (12), the pose (+ 1) and its rounds, then src_cap granules {tag,
+    // correspondence}.  help_stats (zeroed per call, nullable): [0] rounds searched by helpers, [1] owner timeouts,
+    // [2] helper give-ups, [3] poses enlisted.  help_ctl nullptr: no help.
+    unsigned* help_ctl;
+    unsigned long long* help_gran;
+    unsigned long long* help_stats;
+    int32_t help_slots;
+    uint32_t help_tag;  // 1..0xFFFF, a different one for every launch: the granules' tags are (help_tag << 16) | epoch
 };
+
+// The help board is built, bit-identical and measured, but off: the launch's tail is the
+// 150-iteration chains of the smallest poses (one round of 64 points, nothing to share), and the board's code in the
+// iteration loop (the dry-word load; 16 more VGPRs, 93 more SGPR spills) cost 3 % with the board idle.
+// -DPCORE_GICP_HELP_BOARD=1 builds it (PCORE_GICP_HELP=0 then turns it off per call).
+#ifndef PCORE_GICP_HELP_BOARD
+#define PCORE_GICP_HELP_BOARD 0
+#endif
+constexpr bool kGicpHelpBoard = PCORE_GICP_HELP_BOARD;
+constexpr unsigned kHelpClosed = 0xFFFF0000u;  // a help slot's claim word once its pose is done (epoch 0xFFFF)
+constexpr int kHelpMaxRounds = 128;            // poses of at most 128 rounds (8,192 points) are helped
+constexpr int kHelpXfGranules = 16;            // per slot, ahead of its src_cap correspondence granules
+// the help board's zeroed control words for `slots` slots (a multiple of 16 bytes)
+inline size_t help_ctl_words(int slots) { return 4 + 4 * (size_t)((slots + 3) & ~3); }
 
 #if defined(PCORE_GICP_WG_WAVES) && PCORE_GICP_WG_WAVES > 1
 constexpr bool kGicpHeavyBuild = true;

@@ -83,6 +83,10 @@ def main():
     res["longest_poses"] = [{"pose": int(i), "us": float(pose_us[i]), "iterations": int(its[i]),
                              "iterations_reported": int(its_reported[i]), "points": int(ns[i]),
                              "targets": int(nt[i]), "start_us": float((ps[i, 0] - t0) / 100.0)} for i in top]
+    end_us = (ps[:, 1] - t0) / 100.0
+    res["last_poses"] = [{"pose": int(i), "start_us": float((ps[i, 0] - t0) / 100.0), "end_us": float(end_us[i]),
+                          "iterations": int(its[i]), "points": int(ns[i]), "targets": int(nt[i])}
+                         for i in np.argsort(-end_us)[:8]]
     res["poses_over_512_points"] = int((ns > 512).sum())
     res["points_mean"] = float(ns.mean())
     res["segment_targets"] = sorted(set(int(v) for v in nt))
