@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <type_traits>
 
 #ifndef PCORE_COV_SKIP
 #define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
@@ -82,8 +83,8 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
 
 
 // mean / covariance (double, list order) of the listed neighbours and PLANE regularisation (orc covariance_one)
-template <int KMAX>
-__device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[KMAX], int cnt, double* out6) {
+template <int KMAX, class Pts>
+__device__ __forceinline__ void cov_from_list(const Pts& P, const int (&nb)[KMAX], int cnt, double* out6) {
     double mx = 0.0, my = 0.0, mz = 0.0;
 #pragma unroll
     for (int q = 0; q < KMAX; q++)
@@ -116,6 +117,18 @@ __device__ __forceinline__ void cov_from_list(const float4* P, const int (&nb)[K
 }
 
 constexpr int kCovLanes = 64;
+
+// the threshold k-NN's point sources: the cloud in global memory, or its copy in the wave's LDS (x, y, z floats)
+struct GlobalPts {
+    const float4* p;
+    __device__ __forceinline__ float4 operator[](int j) const { return p[j]; }
+};
+struct LdsPts {
+    const float* p;
+    __device__ __forceinline__ float4 operator[](int j) const {
+        return make_float4(p[3 * j], p[3 * j + 1], p[3 * j + 2], 0.0f);
+    }
+};
 
 // One round of 64 queries i0 + lane of the segment P[0, n): k nearest (distance, index) in the scan's order, their
 // covariance into C[6 i].  `tile`: this wave's kCovLanes points of LDS.
@@ -195,7 +208,7 @@ __device__ __forceinline__ void cov_knn_round(const float4* P, int n, int k_arg,
             }
         }
     }
-    if (i < n) cov_from_list<KMAX>(P, nb, cnt, C + (size_t)6 * i);
+    if (i < n) cov_from_list<KMAX>(GlobalPts{P}, nb, cnt, C + (size_t)6 * i);
 }
 
 }  // namespace
@@ -228,7 +241,16 @@ constexpr int kThrR = 3;       // the neighbourhood: (2 kThrR + 1)^2 cells
 #ifndef PCORE_THR_UNROLL
 #define PCORE_THR_UNROLL 7  // a neighbourhood row per loop trip: its map reads and point loads issue together
 #endif
-constexpr size_t kThrLdsBytes = kThrMap * 2 + (size_t)kThrCap * kCovLanes * 2 + kCovLanes * 16;
+// clouds of at most kThrLdsPts points are copied into the wave's LDS (12 B a point) for the neighbourhood, collecting
+// and insertion reads; larger ones are read from global memory through a 64-point tile (the same results).  128 keeps
+// the launch's 6 LDS granules per wave: 1.63 / 1.66 ms per C3 call against 1.70 / 1.70 without the copy; 232 points
+// take a seventh granule and 1.73 / 1.75 ms (profiles/r06n/).
+#ifndef PCORE_THR_LDS_PTS
+#define PCORE_THR_LDS_PTS 128
+#endif
+constexpr int kThrLdsPts = PCORE_THR_LDS_PTS;
+constexpr size_t kThrPtsBytes = (size_t)kThrLdsPts * 12 > kCovLanes * 16 ? (size_t)kThrLdsPts * 12 : kCovLanes * 16;
+constexpr size_t kThrLdsBytes = kThrMap * 2 + (size_t)kThrCap * kCovLanes * 2 + kThrPtsBytes;
 
 __device__ __forceinline__ void cov_cell(const float4& p, const CovGrid& cg, int& kx, int& ky) {
     kx = (int)rintf((p.x / p.z * cg.fx + cg.cx) / (float)cg.stride);
@@ -281,12 +303,17 @@ __device__ __forceinline__ bool cov_thr_map(const float4* P, int n, const CovGri
 
 // One round of 64 queries by the threshold k-NN (k = 10).  Returns false (nothing written) when a lane collects more
 // than kThrCap candidates: the caller runs cov_knn_round for this round.
-__device__ __forceinline__ bool cov_knn_round_thr(const float4* P, int n, int i0, int lane, const CovGrid& cg,
-                                                  const unsigned short* map, int kx0, int ky0, int wx, int wy,
-                                                  unsigned short* list, float4* tile, double* C) {
+template <bool LDS_PTS>
+__device__ __forceinline__ bool cov_knn_round_thr(const float4* Pg, const float* lds_pts, int n, int i0, int lane,
+                                                  const CovGrid& cg, const unsigned short* map, int kx0, int ky0, int wx,
+                                                  int wy, unsigned short* list, float4* tile, double* C) {
     constexpr int K = 10;
     const int i = i0 + lane;
     const bool act = i < n;
+    typedef typename std::conditional<LDS_PTS, LdsPts, GlobalPts>::type PtsT;
+    PtsT P;
+    if constexpr (LDS_PTS) P.p = lds_pts;
+    else P.p = Pg;
     const float4 xi = act ? P[i] : make_float4(0.0f, 0.0f, 1.0f, 0.0f);
     // 1. tau: the K-th smallest distance over the neighbourhood cells (sorted values, one-pass insertion)
     float t[K];
@@ -313,17 +340,28 @@ __device__ __forceinline__ bool cov_knn_round_thr(const float4* P, int n, int i0
     const float tau = t[K - 1];
     // 2. every candidate in scan order; the ones at or below tau are collected (index order)
     int cnt = 0;
-    for (int j0 = 0; j0 < n; j0 += kCovLanes) {
-        wave_lds_sync();  // the previous tile is read
-        if (j0 + lane < n) tile[lane] = P[j0 + lane];
-        wave_lds_sync();
-        const int jn = min(kCovLanes, n - j0);
-        for (int jj = 0; jj < jn; jj++) {
-            const float4 xj = tile[jj];
+    if constexpr (LDS_PTS) {
+        for (int j = 0; j < n; j++) {
+            const float4 xj = P[j];
             const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
             if (act && d <= tau) {
-                if (cnt < kThrCap) list[cnt * kCovLanes + lane] = (unsigned short)(j0 + jj);
+                if (cnt < kThrCap) list[cnt * kCovLanes + lane] = (unsigned short)j;
                 cnt++;
+            }
+        }
+    } else {
+        for (int j0 = 0; j0 < n; j0 += kCovLanes) {
+            wave_lds_sync();  // the previous tile is read
+            if (j0 + lane < n) tile[lane] = Pg[j0 + lane];
+            wave_lds_sync();
+            const int jn = min(kCovLanes, n - j0);
+            for (int jj = 0; jj < jn; jj++) {
+                const float4 xj = tile[jj];
+                const float d = sqdist3(xi.x, xi.y, xi.z, xj.x, xj.y, xj.z);
+                if (act && d <= tau) {
+                    if (cnt < kThrCap) list[cnt * kCovLanes + lane] = (unsigned short)(j0 + jj);
+                    cnt++;
+                }
             }
         }
     }

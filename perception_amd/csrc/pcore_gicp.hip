@@ -233,8 +233,9 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
 __global__ void __launch_bounds__(kCovLanes) covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt,
                                                                      int seg_stride, CovGrid cg, double* cov_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char thr_lds[];
-    float4* tile = reinterpret_cast<float4*>(thr_lds);
-    unsigned short* map = reinterpret_cast<unsigned short*>(thr_lds + kCovLanes * sizeof(float4));
+    float4* tile = reinterpret_cast<float4*>(thr_lds);  // the global path's tile, or the cloud's points (LDS path)
+    float* lpts = reinterpret_cast<float*>(thr_lds);
+    unsigned short* map = reinterpret_cast<unsigned short*>(thr_lds + kThrPtsBytes);
     unsigned short* list = map + kThrMap;
     const int sg = blockIdx.x;
     const int off = sg * seg_stride;
@@ -244,8 +245,24 @@ __global__ void __launch_bounds__(kCovLanes) covariance_cloud_kernel(const float
     double* C = cov_out + (size_t)6 * off;
     int kx0 = 0, ky0 = 0, wx = 0, wy = 0;
     const bool thr = cov_thr_map(P, n, cg, lane, map, kx0, ky0, wx, wy);
+    bool in_lds = thr && n <= kThrLdsPts;
+    if (in_lds) {
+        for (int j = lane; j < n; j += kCovLanes) {
+            const float4 p = P[j];
+            lpts[3 * j] = p.x;
+            lpts[3 * j + 1] = p.y;
+            lpts[3 * j + 2] = p.z;
+        }
+        wave_lds_sync();
+    }
     for (int i0 = 0; i0 < n; i0 += kCovLanes) {
-        if (thr && cov_knn_round_thr(P, n, i0, lane, cg, map, kx0, ky0, wx, wy, list, tile, C)) continue;
+        if (in_lds) {
+            if (cov_knn_round_thr<true>(P, lpts, n, i0, lane, cg, map, kx0, ky0, wx, wy, list, tile, C)) continue;
+            wave_lds_sync();  // the brute force's tile overwrites the points: every lane is done with them
+            in_lds = false;   // the later rounds read the cloud from global memory
+        } else if (thr && cov_knn_round_thr<false>(P, lpts, n, i0, lane, cg, map, kx0, ky0, wx, wy, list, tile, C)) {
+            continue;
+        }
         cov_knn_round<10, true>(P, n, 10, i0, lane, tile, C);
     }
 }
