@@ -235,18 +235,30 @@ struct CovGrid {
     int stride;
 };
 
-constexpr int kThrMap = 1536;  // window cells of the map (ushort point index each; 0xffff = empty)
-constexpr int kThrCap = 24;    // collected candidates per lane
+// The launch's LDS per wave (map + lists + points) sets its occupancy: 6 granules (a 1,536-cell map, 24-entry lists,
+// 128 points) gave 5 waves per SIMD and 1.61-1.65 ms per C3 call; 5 granules (1,024 / 20 / 96) 1.50-1.53 ms;
+// 4 granules (768 / 20 / 64) 1.48-1.50 ms, and with 8 waves per SIMD (64 VGPRs, 7 spilled; PCORE_COV_WAVES_PER_EU)
+// 1.45-1.46 ms (profiles/r06m2..4/).  Clouds whose window exceeds the map, or lanes collecting more than the list
+// holds, take the brute force (the same results).
+#ifndef PCORE_THR_MAP
+#define PCORE_THR_MAP 768
+#endif
+#ifndef PCORE_THR_CAP
+#define PCORE_THR_CAP 20
+#endif
+constexpr int kThrMap = PCORE_THR_MAP;  // window cells of the map (ushort point index each; 0xffff = empty)
+static_assert(kThrMap % 8 == 0 && kThrCap % 4 == 0, "the LDS regions stay 16-byte aligned");
+constexpr int kThrCap = PCORE_THR_CAP;  // collected candidates per lane
 constexpr int kThrR = 3;       // the neighbourhood: (2 kThrR + 1)^2 cells
 #ifndef PCORE_THR_UNROLL
 #define PCORE_THR_UNROLL 7  // a neighbourhood row per loop trip: its map reads and point loads issue together
 #endif
 // clouds of at most kThrLdsPts points are copied into the wave's LDS (12 B a point) for the neighbourhood, collecting
-// and insertion reads; larger ones are read from global memory through a 64-point tile (the same results).  128 keeps
-// the launch's 6 LDS granules per wave: 1.63 / 1.66 ms per C3 call against 1.70 / 1.70 without the copy; 232 points
-// take a seventh granule and 1.73 / 1.75 ms (profiles/r06n/).
+// and insertion reads; larger ones are read from global memory through a 64-point tile (the same results).  With the
+// 1,536-cell map: 128 points (6 LDS granules per wave) 1.63 / 1.66 ms per C3 call against 1.70 / 1.70 without the
+// copy; 232 points (a seventh granule) 1.73 / 1.75 ms (profiles/r06n/).
 #ifndef PCORE_THR_LDS_PTS
-#define PCORE_THR_LDS_PTS 128
+#define PCORE_THR_LDS_PTS 64
 #endif
 constexpr int kThrLdsPts = PCORE_THR_LDS_PTS;
 constexpr size_t kThrPtsBytes = (size_t)kThrLdsPts * 12 > kCovLanes * 16 ? (size_t)kThrLdsPts * 12 : kCovLanes * 16;

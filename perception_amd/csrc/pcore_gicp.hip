@@ -230,7 +230,11 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
 
 // The rendered clouds' covariances (k = 10): the threshold k-NN where the cloud's sample grid allows it, else the brute
 // force, round by round (pcore_cov.h); bit-identical either way.  Dynamic LDS: kThrLdsBytes.
-__global__ void __launch_bounds__(kCovLanes) covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt,
+#ifndef PCORE_COV_WAVES_PER_EU
+#define PCORE_COV_WAVES_PER_EU 8  // 64 VGPRs (7 spilled): 8 waves per SIMD, which the 4-granule LDS allows (pcore_cov.h)
+#endif
+__global__ void __launch_bounds__(kCovLanes) __attribute__((amdgpu_waves_per_eu(PCORE_COV_WAVES_PER_EU)))
+covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt,
                                                                      int seg_stride, CovGrid cg, double* cov_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char thr_lds[];
     float4* tile = reinterpret_cast<float4*>(thr_lds);  // the global path's tile, or the cloud's points (LDS path)
