@@ -247,8 +247,8 @@ struct CovGrid {
 #define PCORE_THR_CAP 20
 #endif
 constexpr int kThrMap = PCORE_THR_MAP;  // window cells of the map (ushort point index each; 0xffff = empty)
-static_assert(kThrMap % 8 == 0 && kThrCap % 4 == 0, "the LDS regions stay 16-byte aligned");
 constexpr int kThrCap = PCORE_THR_CAP;  // collected candidates per lane
+static_assert(kThrMap % 8 == 0 && kThrCap % 4 == 0, "the LDS regions stay 16-byte aligned");
 constexpr int kThrR = 3;       // the neighbourhood: (2 kThrR + 1)^2 cells
 #ifndef PCORE_THR_UNROLL
 #define PCORE_THR_UNROLL 7  // a neighbourhood row per loop trip: its map reads and point loads issue together
