@@ -11,6 +11,9 @@
 #include <climits>
 #include <type_traits>
 
+#ifndef PCORE_JACOBI_SKIP
+#define PCORE_JACOBI_SKIP 0
+#endif
 #ifndef PCORE_COV_SKIP
 #define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
 #endif
@@ -43,6 +46,13 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
             const int p = r < 2 ? 0 : 1, q = r == 0 ? 1 : 2, o = 3 - p - q;
             const double apq = A[p][q];
             if (apq == 0.0) continue;
+#if PCORE_JACOBI_SKIP  // timing study only (not the spec): a negligible off-diagonal entry is not rotated
+            {
+                const double g = 100.0 * fabs(apq);
+                if (sweep >= PCORE_JACOBI_SKIP && fabs(A[p][p]) + g == fabs(A[p][p]) && fabs(A[q][q]) + g == fabs(A[q][q]))
+                    continue;
+            }
+#endif
             const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
             double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
             if (theta < 0.0) t = -t;
