@@ -485,11 +485,20 @@ void plane_regularize(const double c[6], double out[6]) {
     double A[3][3] = {{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}};
     double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
     static const int PQ[3][2] = {{0, 1}, {0, 2}, {1, 2}};
-    for (int sweep = 0; sweep < 6; sweep++)
+    // at most 6 cyclic sweeps; a rotation is skipped when |A_pq| <= max(2 eps max_i |A_ii|, the smallest normal double)
+    // (Eigen JacobiSVD's threshold), and a sweep without a rotation ends the loop
+    for (int sweep = 0; sweep < 6; sweep++) {
+        bool rotated = false;
         for (int r = 0; r < 3; r++) {
             const int p = PQ[r][0], q = PQ[r][1], o = 3 - p - q;
             const double apq = A[p][q];
-            if (apq == 0.0) continue;
+            const double d0 = std::fabs(A[0][0]), d1 = std::fabs(A[1][1]), d2 = std::fabs(A[2][2]);
+            double dm = d0 > d1 ? d0 : d1;
+            dm = dm > d2 ? dm : d2;
+            double thr = 4.440892098500626e-16 * dm;
+            thr = thr > 2.2250738585072014e-308 ? thr : 2.2250738585072014e-308;
+            if (std::fabs(apq) <= thr) continue;
+            rotated = true;
             const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
             double t = 1.0 / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
             if (theta < 0.0) t = -t;
@@ -511,6 +520,8 @@ void plane_regularize(const double c[6], double out[6]) {
                 V[k][q] = ss * vkp + cc * vkq;
             }
         }
+        if (!rotated) break;
+    }
     int m = 0;
     if (A[1][1] < A[m][m]) m = 1;
     if (A[2][2] < A[m][m]) m = 2;

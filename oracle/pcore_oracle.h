@@ -102,7 +102,7 @@ void orc_evaluate(const float* tris, int num_tris, const int32_t* tris_model_cou
  * pcore_gicp_math.h, shared with the kernels, and held to the independent textbook restatement below):
  *  - covariance: k nearest points of the same cloud (float squared distance, ties -> lower index,
  *    list ordered by (distance, index)), double mean / covariance over k_eff = min(k, n), PLANE
- *    regularisation C = U diag(1, 1, 1e-3) U^T from 6 cyclic Jacobi sweeps (double, sqrt/div only);
+ *    regularisation C = U diag(1, 1, 1e-3) U^T from at most 6 cyclic Jacobi sweeps with a 2-eps rotation threshold (double, sqrt/div only);
  *  - per iteration: correspondence of the float query float(T) s = the first strict minimum over the target
  *    segment of the three-FMA key (|q'-t'|^2 - |q'|^2 about the segment's origin; segments of <= 2048 targets) or
  *    of the float squared distance (larger segments); Mahalanobis (C_t + R C_s R^T)^-1, J = [skew(q) | -I];

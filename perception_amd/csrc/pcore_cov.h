@@ -1,6 +1,6 @@
 // pcore_cov.h -- the GICP covariances of a point segment (fast_gicp's k-NN covariances with PLANE regularisation;
 // DESIGN.md section 5): one wave per round of 64 query points, brute-force k-NN over the segment with candidates
-// staged through a 64-point LDS tile, double mean / covariance in list order, 6-sweep Jacobi, PLANE regularisation.
+// staged through a 64-point LDS tile, double mean / covariance in list order, Jacobi (<= 6 thresholded sweeps), PLANE regularisation.
 // Shared by covariance_kernel (pcore_gicp.hip: one wave per segment) and render_cloud_kernel (pcore_kernels.hip: the
 // rendered clouds' covariances in the launch that produced them, its four waves taking the query rounds in turn).
 // Bit-identical to the oracle's covariance_one (tests/test_gpu_covariances.py, the GICP parity tests).
@@ -11,9 +11,6 @@
 #include <climits>
 #include <type_traits>
 
-#ifndef PCORE_JACOBI_SKIP
-#define PCORE_JACOBI_SKIP 0
-#endif
 #ifndef PCORE_COV_SKIP
 #define PCORE_COV_SKIP 0  // ablation timing builds only: bit 0 skips the PLANE regularisation, bit 1 the k-NN search
 #endif
@@ -22,6 +19,8 @@ namespace pcore {
 namespace {
 
 constexpr double kPlaneScale = 1.0 - 1e-3;
+constexpr double kJacobiEps2 = 4.440892098500626e-16;    // 2 eps (double)
+constexpr double kJacobiTiny = 2.2250738585072014e-308;  // the smallest normal double (Eigen's considerAsZero)
 
 // LDS writes by some lanes of a wave visible to all its lanes (no block barrier: waves are independent)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -35,24 +34,26 @@ __device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx,
     return dx * dx + dy * dy + dz * dz;
 }
 
-// Jacobi (6 cyclic sweeps) + PLANE regularisation, same operation order as orc plane_regularize.
+// Jacobi (at most 6 cyclic sweeps) + PLANE regularisation, same operation order as orc plane_regularize.  A rotation
+// is skipped when its off-diagonal entry is at most 2 eps times the largest diagonal magnitude (Eigen JacobiSVD's
+// convergence threshold, which fast_gicp's PLANE regularisation runs), and a sweep without a rotation ends the loop.
 __device__ void plane_regularize(const double c[6], double out[6]) {
     double A[3][3] = {{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}};
     double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
 #pragma unroll 1
-    for (int sweep = 0; sweep < 6; sweep++)
+    for (int sweep = 0; sweep < 6; sweep++) {
+        bool rotated = false;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
             const int p = r < 2 ? 0 : 1, q = r == 0 ? 1 : 2, o = 3 - p - q;
             const double apq = A[p][q];
-            if (apq == 0.0) continue;
-#if PCORE_JACOBI_SKIP  // timing study only (not the spec): a negligible off-diagonal entry is not rotated
-            {
-                const double g = 100.0 * fabs(apq);
-                if (sweep >= PCORE_JACOBI_SKIP && fabs(A[p][p]) + g == fabs(A[p][p]) && fabs(A[q][q]) + g == fabs(A[q][q]))
-                    continue;
-            }
-#endif
+            const double d0 = fabs(A[0][0]), d1 = fabs(A[1][1]), d2 = fabs(A[2][2]);
+            double dm = d0 > d1 ? d0 : d1;
+            dm = dm > d2 ? dm : d2;
+            double thr = kJacobiEps2 * dm;
+            thr = thr > kJacobiTiny ? thr : kJacobiTiny;
+            if (fabs(apq) <= thr) continue;
+            rotated = true;
             const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
             double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
             if (theta < 0.0) t = -t;
@@ -75,6 +76,8 @@ __device__ void plane_regularize(const double c[6], double out[6]) {
                 V[k][q] = ss * vkp + cc * vkq;
             }
         }
+        if (!rotated) break;
+    }
     // smallest eigenvalue's column, first on ties (selects, not a dynamic register index)
     int m = 0;
     double am = A[0][0];

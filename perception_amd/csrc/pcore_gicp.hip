@@ -11,7 +11,7 @@
 //
 //   covariance_kernel  one wave per segment (a pose's rendered cloud or an observed label): brute-force
 //                      k-NN of every point inside its segment (candidates staged through LDS), double
-//                      mean / covariance, 6-sweep Jacobi, PLANE regularisation.
+//                      mean / covariance, Jacobi (<= 6 sweeps, thresholded), PLANE regularisation.
 //   gicp_kernel        one wave per pose: per-lane sequential partial sums of J^T M J / J^T M e / e^T M e,
 //                      the shuffle-down tree in registers (wave_tree_sums), the LM iteration (uniform: the
 //                      damped solve by 3x3 block elimination, se3_exp, the trial), the correspondence history, then
