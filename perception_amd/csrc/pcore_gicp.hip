@@ -402,6 +402,9 @@ typedef __attribute__((address_space(4))) const f4v cf4v;
 #ifndef PCORE_SCAN2_UNROLL
 #define PCORE_SCAN2_UNROLL 2  // scan_quads2: quad pairs per loop trip
 #endif
+#ifndef PCORE_SCAN_PAIRQ
+#define PCORE_SCAN_PAIRQ 0  // scan_quads2: one compare per pair of quads per chain (A/B)
+#endif
 
 __device__ __forceinline__ void scan_quads(const float* seg_quads, int nt, float qx, float qy, float qz, float& best,
                                            int& j) {
@@ -485,6 +488,38 @@ __device__ __forceinline__ void scan_quads2(const float* seg_quads, int nt, floa
     };
     int o = 0;
     const cf4v* q = tq;
+#if PCORE_SCAN_PAIRQ
+    // each chain compares once per PAIR of quads (8 keys): chain A takes quads o, o + 1 and chain B o + 2, o + 3 of
+    // every four; a chain's index is the pair's first quad (a pair past the segment's last quad is that quad alone).
+    // The first strict minimum per chain, the lower pair on a tie between chains, then the first of the pair's 8 keys
+    // equal to the minimum: the same (key, index) minimum as the per-quad chains.
+#pragma unroll PCORE_SCAN2_UNROLL
+    for (; o + 4 <= nq; o += 4, q += 16) {
+        float ma0, mb0, ma1, mb1;
+        qmin2(q, ma0, mb0);
+        qmin2(q + 4, ma1, mb1);
+        const float pa = fminf(ma0, ma1), pb = fminf(mb0, mb1);
+        if (pa < aA) { aA = pa; oaA = o; }
+        if (pb < bA) { bA = pb; obA = o; }
+        qmin2(q + 8, ma0, mb0);
+        qmin2(q + 12, ma1, mb1);
+        const float ra = fminf(ma0, ma1), rb = fminf(mb0, mb1);
+        if (ra < aB) { aB = ra; oaB = o + 2; }
+        if (rb < bB) { bB = rb; obB = o + 2; }
+    }
+    for (; o < nq; o += 2, q += 8) {  // the last one to three quads: pairs (or a lone quad) into chain A
+        float ma, mb;
+        qmin2(q, ma, mb);
+        if (o + 1 < nq) {
+            float ma1, mb1;
+            qmin2(q + 4, ma1, mb1);
+            ma = fminf(ma, ma1);
+            mb = fminf(mb, mb1);
+        }
+        if (ma < aA) { aA = ma; oaA = o; }
+        if (mb < bA) { bA = mb; obA = o; }
+    }
+#else
 #pragma unroll PCORE_SCAN2_UNROLL
     for (; o + 2 <= nq; o += 2, q += 8) {
         float ma, mb;
@@ -501,16 +536,29 @@ __device__ __forceinline__ void scan_quads2(const float* seg_quads, int nt, floa
         if (ma < aA) { aA = ma; oaA = o; }
         if (mb < bA) { bA = mb; obA = o; }
     }
+#endif
     if (aB < aA || (aB == aA && oaB >= 0 && oaB < oaA)) { aA = aB; oaA = oaB; }
     if (bB < bA || (bB == bA && obB >= 0 && obB < obA)) { bA = bB; obA = obB; }
-    auto element = [&](int oq, float m, float qx, float qy, float qz) {
+    auto element1 = [&](int oq, float m, float qx, float qy, float qz, int& k) {  // first key == m in quad oq, or 4
         const float* Q = seg_quads + 16 + 16 * oq;
         const float4 X = *reinterpret_cast<const float4*>(Q), Y = *reinterpret_cast<const float4*>(Q + 4);
         const float4 Z = *reinterpret_cast<const float4*>(Q + 8), T = *reinterpret_cast<const float4*>(Q + 12);
-        const int k = gicpm::nn_key(X.x, Y.x, Z.x, T.x, qx, qy, qz) == m ? 0
-                    : gicpm::nn_key(X.y, Y.y, Z.y, T.y, qx, qy, qz) == m ? 1
-                    : gicpm::nn_key(X.z, Y.z, Z.z, T.z, qx, qy, qz) == m ? 2 : 3;
-        return min(4 * oq + k, nt - 1);
+        k = gicpm::nn_key(X.x, Y.x, Z.x, T.x, qx, qy, qz) == m ? 0
+          : gicpm::nn_key(X.y, Y.y, Z.y, T.y, qx, qy, qz) == m ? 1
+          : gicpm::nn_key(X.z, Y.z, Z.z, T.z, qx, qy, qz) == m ? 2
+          : gicpm::nn_key(X.w, Y.w, Z.w, T.w, qx, qy, qz) == m ? 3 : 4;
+    };
+    auto element = [&](int oq, float m, float qx, float qy, float qz) {
+        int k;
+        element1(oq, m, qx, qy, qz, k);
+#if PCORE_SCAN_PAIRQ
+        if (k == 4 && oq + 1 < nq) {  // the pair's second quad
+            element1(oq + 1, m, qx, qy, qz, k);
+            k += 4;
+        }
+#endif
+        // one of the keys equals m (same FMAs); the clamp only keeps a broken match inside the segment
+        return min(4 * oq + min(k, PCORE_SCAN_PAIRQ ? 7 : 3), nt - 1);
     };
     ja = fa && aA < INFINITY ? element(oaA, aA, ax, ay, az) : -1;
     jb = fb && bA < INFINITY ? element(obA, bA, bx, by, bz) : -1;
