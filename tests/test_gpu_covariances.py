@@ -90,7 +90,13 @@ def test_gpu_threshold_knn_covariances_equal_oracle_bitwise():
     (no grid structure, lattices with ties, duplicates, n < k, a NaN point: the threshold stays a valid bound or the
     kernel falls back), each in a slot of a strided buffer as the ICP scratch holds them."""
     grid, cam, s = _grid_clouds()
-    segs = grid + _segments()
+    # clustered clouds in front of the camera that share few sample-grid cells: the map keeps one point per cell, so the
+    # neighbourhood bound is loose or infinite and the lists overflow -- a cloud small enough for the LDS copy (the
+    # brute force then overwrites the copy with its tile) and a larger one
+    rng = np.random.default_rng(21)
+    clustered = [np.stack([rng.normal(size=n) * 0.002, rng.normal(size=n) * 0.002, 0.8 + rng.random(n) * 0.1], -1)
+                 .astype(np.float32) for n in (50, 90)]
+    segs = grid + clustered + _segments()
     cap = max(len(x) for x in segs)
     xyzw = np.zeros((len(segs) * cap, 4), np.float32)
     for i, x in enumerate(segs):
