@@ -264,6 +264,8 @@ PCORE_UNROLL
 // J^T M J with M positive definite, lambda = 1e-9 max|H_aa| > 0 unless H = 0): a zero diagonal gives d = 0 (Eigen's
 // LDLT of the zero matrix); a non-finite system gives a non-finite d, which stops the pose (lm_iteration's guard).
 // The dependent chain is two adjugates, two 3-term products and two divisions deep, against the LDLT's six pivot steps.
+// On the device the wave holds one system (every lane the same), so each group of three quotients runs as one division
+// sequence on lanes 0..2 (lane_div): the same IEEE divisions as the host's.
 PCORE_GHD void lm_solve_schur(const double* sys, double lambda, double (&d)[6]) {
     // upper triangles (00 01 02 11 12 22) of the rotation block A and the translation block C, + lambda on the diagonal
     const double A[6] = {sys[0] + lambda, sys[1], sys[2], sys[6] + lambda, sys[7], sys[11] + lambda};
@@ -302,19 +304,35 @@ PCORE_UNROLL
     const double u2 = fma_d(dC, r2, -dot3f(P20, P21, P22, r3, r4, r5));
     double aS[6], dS;
     adj_sym3(St, aS, dS);
-    const double x0 = dot3f(aS[0], aS[1], aS[2], u0, u1, u2) / dS;
-    const double x1 = dot3f(aS[1], aS[3], aS[4], u0, u1, u2) / dS;
-    const double x2 = dot3f(aS[2], aS[4], aS[5], u0, u1, u2) / dS;
+    const double nx[3] = {dot3f(aS[0], aS[1], aS[2], u0, u1, u2), dot3f(aS[1], aS[3], aS[4], u0, u1, u2),
+                          dot3f(aS[2], aS[4], aS[5], u0, u1, u2)};
+    double x[3];
+#if PCORE_LANE_PAR
+    // the wave holds one system: the three quotients on lanes 0..2 in one division sequence (the same IEEE divisions)
+    const double dSv[3] = {dS, dS, dS};
+    lane_div<3>(nx, dSv, x);
+#else
+    for (int i = 0; i < 3; i++) x[i] = nx[i] / dS;
+#endif
     // w = r_trans - B^T x_rot
-    const double w0 = r3 - dot3f(B00, B10, B20, x0, x1, x2);
-    const double w1 = r4 - dot3f(B01, B11, B21, x0, x1, x2);
-    const double w2 = r5 - dot3f(B02, B12, B22, x0, x1, x2);
-    d[0] = x0;
-    d[1] = x1;
-    d[2] = x2;
-    d[3] = dot3f(aC[0], aC[1], aC[2], w0, w1, w2) / dC;
-    d[4] = dot3f(aC[1], aC[3], aC[4], w0, w1, w2) / dC;
-    d[5] = dot3f(aC[2], aC[4], aC[5], w0, w1, w2) / dC;
+    const double w0 = r3 - dot3f(B00, B10, B20, x[0], x[1], x[2]);
+    const double w1 = r4 - dot3f(B01, B11, B21, x[0], x[1], x[2]);
+    const double w2 = r5 - dot3f(B02, B12, B22, x[0], x[1], x[2]);
+    d[0] = x[0];
+    d[1] = x[1];
+    d[2] = x[2];
+    const double nt[3] = {dot3f(aC[0], aC[1], aC[2], w0, w1, w2), dot3f(aC[1], aC[3], aC[4], w0, w1, w2),
+                          dot3f(aC[2], aC[4], aC[5], w0, w1, w2)};
+#if PCORE_LANE_PAR
+    const double dCv[3] = {dC, dC, dC};
+    double y[3];
+    lane_div<3>(nt, dCv, y);
+    d[3] = y[0];
+    d[4] = y[1];
+    d[5] = y[2];
+#else
+    for (int i = 0; i < 3; i++) d[3 + i] = nt[i] / dC;
+#endif
 }
 
 // se3_exp's four functions of theta as even power series in u = theta^2 (Horner, fused), used below theta^2 = 1/4:
