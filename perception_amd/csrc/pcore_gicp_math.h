@@ -123,6 +123,9 @@ PCORE_GHD void adj_sym3(const double (&m)[6], double (&a)[6], double& det) {
 // instruction sequence and the results return through v_readlane.  Every lane still performs the same IEEE
 // operation on the same operands as the scalar code, so the results are bit-identical to the host's (the oracle
 // runs the scalar path).
+#ifndef PCORE_SE3_LANE_SERIES
+#define PCORE_SE3_LANE_SERIES 1  // se3_exp's four series on lanes 0..3: gicp_kernel -0.8..-1.7 % in 4 of 4 pairs (profiles/r06se/)
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 #define PCORE_LANE_PAR 1
 __device__ __forceinline__ int lane_index() {
@@ -359,12 +362,24 @@ constexpr double kSe3Coef[4 * kSe3Terms] = {
 // its own before the next, 32 LDS round trips in a row); the host passes kSe3Coef.
 template <typename P>
 PCORE_GHD void se3_series(P c, double u, double (&out)[4]) {
+#if PCORE_LANE_PAR && PCORE_SE3_LANE_SERIES
+    // the wave holds one step: series f on lane f & 3 (its coefficients read per lane), the four results by v_readlane
+    const int f = lane_index() & 3;
+    double v = c[4 * (kSe3Terms - 1) + f];
+PCORE_UNROLL
+    for (int k = kSe3Terms - 2; k >= 0; k--) v = fma_d(v, u, c[4 * k + f]);
+    out[0] = read_lane_d<0>(v);
+    out[1] = read_lane_d<1>(v);
+    out[2] = read_lane_d<2>(v);
+    out[3] = read_lane_d<3>(v);
+#else
 PCORE_UNROLL
     for (int f = 0; f < 4; f++) out[f] = c[4 * (kSe3Terms - 1) + f];
 PCORE_UNROLL
     for (int k = kSe3Terms - 2; k >= 0; k--)
 PCORE_UNROLL
         for (int f = 0; f < 4; f++) out[f] = fma_d(out[f], u, c[4 * k + f]);
+#endif
 }
 
 // se3_exp (fast_gicp so3.hpp): so3_exp's quaternion (imag = sin(theta/2)/theta, real = cos(theta/2)), Eigen's
