@@ -119,7 +119,8 @@ def c3_leg(steps: int, warmup: int, local: int, rank: int, world: int, poses_per
     # batches in flight (PCORE_BENCH_C3_LANES, A/B): step i runs on lane i % L (its own context, stream, scratch,
     # outputs and key buffer), so one step's GICP tail could overlap the next step's render, clouds and covariances;
     # every step is still one whole 50k-pose batch completing inside the timed region.  Two lanes measured no faster
-    # (3.95-3.99 vs 3.98-3.99 M poses/s, profiles/r06m/), so the C3 leg runs one
+    # (3.95-3.99 vs 3.98-3.99 M poses/s, profiles/r06m/; 4.34-4.35 vs 4.30-4.35 M at the final build, profiles/r06c3l/),
+    # so the C3 leg runs one
     L = max(1, int(os.environ.get("PCORE_BENCH_C3_LANES", "1")))
     lanes = workloads.lanes(w, L)
     outs = [(torch.empty((n, 16), dtype=torch.float32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
