@@ -64,17 +64,18 @@ def test_gpu_covariances_equal_oracle_bitwise(k):
         assert _same(got[o:o + c], want), (len(s), k)
 
 
-def _grid_clouds():
-    """Clouds unprojected from a stride-8 sample grid of the 640x480 camera (what render_cloud writes): tilted planes,
-    a sphere cap and a step (a depth discontinuity inside the neighbourhoods), 20 to 467 points."""
+def _grid_clouds(cam_name="640"):
+    """Clouds unprojected from a stride-8 sample grid of the camera (what render_cloud writes): tilted planes, a step
+    (a depth discontinuity inside the neighbourhoods), 24 to 1,000 points -- the last one's window (40 x 25 cells) is
+    larger than the kernel's LDS map, which sends it to the brute force."""
     from perception_amd import synthetic as syn
-    cam, s = syn.CAM_640, 8
+    cam, s = (syn.CAM_640 if cam_name == "640" else syn.CAM_1280), 8
     rng = np.random.default_rng(9)
     clouds = []
-    for (w, h, x0, y0) in ((12, 10, 30, 20), (23, 20, 10, 5), (8, 3, 50, 40), (27, 17, 3, 30)):
+    for (w, h, x0, y0) in ((12, 10, 30, 20), (23, 20, 10, 5), (8, 3, 50, 40), (27, 17, 3, 30), (40, 25, 20, 10)):
         kx, ky = np.meshgrid(np.arange(x0, x0 + w), np.arange(y0, y0 + h))
         u, v = kx * s, ky * s
-        z = 0.8 + 0.0004 * (u - 320) + 0.0003 * (v - 240) + rng.normal(size=u.shape) * 1e-3
+        z = 0.8 + 0.0004 * (u - cam["cx"]) + 0.0003 * (v - cam["cy"]) + rng.normal(size=u.shape) * 1e-3
         if w == 27:
             z = np.where(kx > x0 + 13, z + 0.05, z)  # a step: the far side's neighbourhoods reach across it
         z = np.round(z * 100) / 100  # the int-centimetre z-buffer's depths
@@ -84,12 +85,13 @@ def _grid_clouds():
     return clouds, cam, s
 
 
-def test_gpu_threshold_knn_covariances_equal_oracle_bitwise():
+@pytest.mark.parametrize("cam_name", ["640", "1280"])
+def test_gpu_threshold_knn_covariances_equal_oracle_bitwise(cam_name):
     """covariance_cloud_kernel (the threshold k-NN over each rendered cloud's sample grid, pcore_cov.h; k = 10) bit for
     bit against the oracle: on grid-structured clouds (the path it serves) and on every segment of the brute-force test
     (no grid structure, lattices with ties, duplicates, n < k, a NaN point: the threshold stays a valid bound or the
     kernel falls back), each in a slot of a strided buffer as the ICP scratch holds them."""
-    grid, cam, s = _grid_clouds()
+    grid, cam, s = _grid_clouds(cam_name)
     # clustered clouds in front of the camera that share few sample-grid cells: the map keeps one point per cell, so the
     # neighbourhood bound is loose or infinite and the lists overflow -- a cloud small enough for the LDS copy (the
     # brute force then overwrites the copy with its tile) and a larger one
