@@ -1098,16 +1098,26 @@ int pcore_evaluate_icp(pcore_ctx* c, const float* d_poses, const int32_t* d_pose
         // the covariance launch runs 32 one-wave workgroups per CU.
         const bool fold = k == 10 && getenv("PCORE_COV_FOLD") && atoi(getenv("PCORE_COV_FOLD")) == 1;
         a.cloud_cov = fold ? c->icp_cov.p : nullptr;
+        // PCORE_COV_GICP=1: the covariances in gicp_kernel's pose prologue instead (launch_gicp runs the covariance
+        // launch itself when it picks a kernel without the prologue); bit-identical
+        const bool gfold = !fold && k == 10 && !getenv("PCORE_COV_BRUTE") && getenv("PCORE_COV_GICP") &&
+                           atoi(getenv("PCORE_COV_GICP")) == 1;
+        g.cov_fold = gfold ? c->icp_cov.p : nullptr;
+        g.cov_fx = a.fx;
+        g.cov_fy = a.fy;
+        g.cov_cx = a.cx;
+        g.cov_cy = a.cy;
+        g.cov_stride = p->stride;
         hipEvent_t* ev = timed ? c->icp_ev.data() + 3 * c->icp_ev_used : nullptr;
         if (ev && fold) HIPC(c, hipEventRecord(ev[0], s));  // icp_runtime then spans the cloud + covariance launch
         HIPC(c, launch_render_cloud(a, s));
         if (ev && !fold) HIPC(c, hipEventRecord(ev[0], s));
         // the clouds' covariances: k = 10 by the threshold k-NN over each cloud's sample grid (pcore_cov.h;
         // PCORE_COV_BRUTE=1 restores the brute-force kernel for A/B), other k by the brute force; bit-identical
-        if (!fold && k == 10 && !getenv("PCORE_COV_BRUTE"))
+        if (!fold && !gfold && k == 10 && !getenv("PCORE_COV_BRUTE"))
             HIPC(c, launch_covariances_cloud(c->icp_cloud.p, c->icp_count.p, nsamp, n, a.fx, a.fy, a.cx, a.cy, p->stride,
                                              c->icp_cov.p, s));
-        else if (!fold)
+        else if (!fold && !gfold)
             HIPC(c, launch_covariances(c->icp_cloud.p, nullptr, c->icp_count.p, nsamp, n, k, c->icp_cov.p, s));
         g.pose_base = base;
         g.pose_order = nullptr;

@@ -233,20 +233,14 @@ __global__ void __launch_bounds__(kCovLanes) covariance_kernel(const float4* pts
 #ifndef PCORE_COV_WAVES_PER_EU
 #define PCORE_COV_WAVES_PER_EU 8  // 64 VGPRs (7 spilled): 8 waves per SIMD, which the 4-granule LDS allows (pcore_cov.h)
 #endif
-__global__ void __launch_bounds__(kCovLanes) __attribute__((amdgpu_waves_per_eu(PCORE_COV_WAVES_PER_EU)))
-covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt,
-                                                                     int seg_stride, CovGrid cg, double* cov_out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char thr_lds[];
+// One rendered cloud's covariances by one wave: P[0, n) -> C[6 i], thr_lds = kThrLdsBytes of the wave's LDS.  Used by
+// covariance_cloud_kernel (one wave per cloud) and by gicp_kernel's pose prologue (GicpArgs::cov_fold).
+__device__ __forceinline__ void cov_cloud_segment(const float4* P, int n, const CovGrid& cg, int lane,
+                                                  unsigned char* thr_lds, double* C) {
     float4* tile = reinterpret_cast<float4*>(thr_lds);  // the global path's tile, or the cloud's points (LDS path)
     float* lpts = reinterpret_cast<float*>(thr_lds);
     unsigned short* map = reinterpret_cast<unsigned short*>(thr_lds + kThrPtsBytes);
     unsigned short* list = map + kThrMap;
-    const int sg = blockIdx.x;
-    const int off = sg * seg_stride;
-    const int n = seg_cnt[sg];
-    const int lane = threadIdx.x;
-    const float4* P = pts + off;
-    double* C = cov_out + (size_t)6 * off;
     int kx0 = 0, ky0 = 0, wx = 0, wy = 0;
     const bool thr = cov_thr_map(P, n, cg, lane, map, kx0, ky0, wx, wy);
     bool in_lds = thr && n <= kThrLdsPts;
@@ -269,6 +263,19 @@ covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt,
         }
         cov_knn_round<10, true>(P, n, 10, i0, lane, tile, C);
     }
+}
+
+// gicp_kernel's call of it: not inlined, so the k-NN's registers do not add to those of the iteration loop
+__device__ __attribute__((noinline)) void cov_cloud_segment_call(const float4* P, int n, CovGrid cg, int lane,
+                                                                 unsigned char* thr_lds, double* C) {
+    cov_cloud_segment(P, n, cg, lane, thr_lds, C);
+}
+
+__global__ void __launch_bounds__(kCovLanes) __attribute__((amdgpu_waves_per_eu(PCORE_COV_WAVES_PER_EU)))
+covariance_cloud_kernel(const float4* pts, const int32_t* seg_cnt, int seg_stride, CovGrid cg, double* cov_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char thr_lds[];
+    const int off = blockIdx.x * seg_stride;
+    cov_cloud_segment(pts + off, seg_cnt[blockIdx.x], cg, threadIdx.x, thr_lds, cov_out + (size_t)6 * off);
 }
 
 hipError_t launch_covariances_cloud(const float4* pts, const int32_t* seg_cnt, int seg_stride, int num_segs,
@@ -1200,6 +1207,18 @@ __device__ __forceinline__ HelpRef help_ref() {
     kargs_t* a = (kargs_t*)((kbytes_t*)__builtin_amdgcn_kernarg_segment_ptr() + opaque_zero());  // gicp_kernel's g
     return {a->help_ctl, a->help_gran, a->help_stats, a->help_slots, a->src_cap, a->help_tag};
 }
+// The covariance prologue's arguments (GicpArgs::cov_fold), read from the kernarg segment at each pose in the same way:
+// as registers they were live through the iteration loop (146 -> 167 VGPRs, 96 -> 149 SGPRs spilled)
+struct CovFoldRef {
+    double* out;
+    CovGrid cg;
+};
+__device__ __forceinline__ CovFoldRef cov_fold_ref() {
+    typedef __attribute__((address_space(4))) const GicpArgs kargs_t;
+    typedef __attribute__((address_space(4))) const char kbytes_t;
+    kargs_t* a = (kargs_t*)((kbytes_t*)__builtin_amdgcn_kernarg_segment_ptr() + opaque_zero());  // gicp_kernel's g
+    return {a->cov_fold, {a->cov_fx, a->cov_fy, a->cov_cx, a->cov_cy, a->cov_stride}};
+}
 __device__ __forceinline__ void hb_count(const HelpRef& h, int k) {
     if (h.stats) __hip_atomic_fetch_add((gu64*)(h.stats + k), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1522,6 +1541,15 @@ gicp_kernel(GicpArgs g, int num_poses) {
         const GicpPose P = gicp_pose(g, pose);
         if (!GRID && P.use_grid && lane == 0 && g.iter_stats)  // the host picked the instance without the search
             __hip_atomic_fetch_add(g.iter_stats + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (const CovFoldRef cf = cov_fold_ref(); cf.out) {
+            // the pose's source covariances first, in the LDS of its first rounds' trial inputs (written only by the
+            // linearisation below): covariance_cloud_kernel's code, so bit-identical; point i's covariance is
+            // written and later read by lane i % 64
+            static_assert(kThrLdsBytes <= sizeof(sM0A[0]), "the covariance scratch fits the wave's trial-input LDS");
+            cov_cloud_segment_call(P.src, P.ns, cf.cg, lane, reinterpret_cast<unsigned char*>(&sM0A[wave][0][0]),
+                              cf.out + (size_t)6 * pose * g.src_cap);
+            wave_lds_sync();
+        }
 #ifdef PCORE_GICP_TIMELINE
         const unsigned long long tl_p0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1829,14 +1857,20 @@ hipError_t launch_gicp(const GicpArgs& g, int num_poses, const DeviceInfo& d, hi
         if (e[0] == 'n') wide = false;
         else if (e[0] == 'w' && wide_lds <= kGicpWideMaxLds) wide = true;
     }
+    GicpArgs ga = g;
+    if (ga.cov_fold && (wide || kGicpWgWaves != 1)) {  // only the one-wave gicp_kernel has the covariance prologue
+        e = launch_covariances_cloud(g.src, g.src_count, g.src_cap, num_poses, g.cov_fx, g.cov_fy, g.cov_cx, g.cov_cy,
+                                     g.cov_stride, ga.cov_fold, s);
+        if (e != hipSuccess) return e;
+        ga.cov_fold = nullptr;
+    }
     if (wide) {
         const int wgs = std::min(num_poses, num_cus * 2);
-        hipLaunchKernelGGL(gicp_wide_kernel<kGicpWideWpp>, dim3(wgs), dim3(64 * kGicpWideWpp), wide_lds, s, g,
+        hipLaunchKernelGGL(gicp_wide_kernel<kGicpWideWpp>, dim3(wgs), dim3(64 * kGicpWideWpp), wide_lds, s, ga,
                            num_poses);
         return hipGetLastError();
     }
     const dim3 wgs(std::min(resident_wgs, (num_poses + kGicpWgWaves - 1) / kGicpWgWaves)), block(64 * kGicpWgWaves);
-    GicpArgs ga = g;
     if (!kGicpHelpBoard || kGicpWgWaves != 1 || grid) ga.help_ctl = nullptr;  // the one-wave grid-free instance only
     if (ga.help_ctl && (e = hipMemsetAsync(ga.help_ctl, 0, help_ctl_words(ga.help_slots) * sizeof(unsigned), s)) != hipSuccess)
         return e;

@@ -202,6 +202,11 @@ struct GicpArgs {
     unsigned long long* help_stats;
     int32_t help_slots;
     uint32_t help_tag;  // 1..0xFFFF, a different one for every launch: the granules' tags are (help_tag << 16) | epoch
+    // the source covariances computed by gicp_kernel itself, in each pose's prologue (nullptr: a launch of their own
+    // wrote src_cov first): cov_fold = src_cov, and the rendered clouds' sample grid of the threshold k-NN (pcore_cov.h)
+    double* cov_fold;
+    float cov_fx, cov_fy, cov_cx, cov_cy;
+    int32_t cov_stride;
 };
 
 // The help board is built, bit-identical and measured, but off: the launch's tail is the
