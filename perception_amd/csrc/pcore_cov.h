@@ -212,11 +212,12 @@ __device__ __forceinline__ void cov_knn_round(const float4* P, int n, int k_arg,
 #pragma unroll
                 for (int q = KMAX - 1; q >= 1; q--) {
                     if (q < k) {
-                        nd[q] = g[q - 1] ? nd[q - 1] : (g[q] ? d : nd[q]);
+                        // the same value as g[q - 1] ? nd[q - 1] : (g[q] ? d : nd[q]) on a sorted list without NaN
+                        nd[q] = __builtin_amdgcn_fmed3f(nd[q - 1], nd[q], d);
                         nb[q] = g[q - 1] ? nb[q - 1] : (g[q] ? j : nb[q]);
                     }
                 }
-                nd[0] = g[0] ? d : nd[0];
+                nd[0] = fminf(nd[0], d);
                 nb[0] = g[0] ? j : nb[0];
             }
         }
@@ -356,9 +357,11 @@ __device__ __forceinline__ bool cov_knn_round_thr(const float4* Pg, const float*
             if (j != 0xffff) {
                 const float4 p = P[j];
                 const float d = sqdist3(xi.x, xi.y, xi.z, p.x, p.y, p.z);
+                // t stays sorted: entry q becomes the median of (t[q - 1], t[q], d) -- one v_med3_f32 each (no NaN:
+                // the points are finite) where the selects took a compare and two v_cndmask
 #pragma unroll
-                for (int q = K - 1; q >= 1; q--) t[q] = t[q - 1] > d ? t[q - 1] : (t[q] > d ? d : t[q]);
-                t[0] = t[0] > d ? d : t[0];
+                for (int q = K - 1; q >= 1; q--) t[q] = __builtin_amdgcn_fmed3f(t[q - 1], t[q], d);
+                t[0] = fminf(t[0], d);
             }
         }
     }
@@ -392,10 +395,14 @@ __device__ __forceinline__ bool cov_knn_round_thr(const float4* Pg, const float*
     }
     if (__ballot(cnt > kThrCap) != 0ull) return false;
     // 3. the collected candidates through the brute force's insertion (stable: entries strictly greater move right)
+    // The list's unfilled entries hold +inf, so one form serves the filling and the full list: the entries strictly
+    // greater than d (a suffix of the sorted list, +inf included) move right by one and d takes the first of their
+    // slots -- the counting insertion's placement, since d is finite (the points are) and each j exceeds the listed
+    // ones.  Values by one v_med3_f32 per entry, indices by the same compares.
     float nd[K];
     int nb[K];
 #pragma unroll
-    for (int q = 0; q < K; q++) { nd[q] = 0.0f; nb[q] = 0; }
+    for (int q = 0; q < K; q++) { nd[q] = INFINITY; nb[q] = 0; }
     int len = 0;
     const int cmax = wave_max_i(cnt);
     for (int c = 0; c < cmax; c++) {
@@ -403,19 +410,18 @@ __device__ __forceinline__ bool cov_knn_round_thr(const float4* Pg, const float*
             const int j = list[c * kCovLanes + lane];
             const float4 p = P[j];
             const float d = sqdist3(xi.x, xi.y, xi.z, p.x, p.y, p.z);
-            if (len < K || d < nd[K - 1]) {
-                const int pos = len < K ? len : K - 1;
-                int g = 0;
+            if (d < nd[K - 1]) {
+                bool g[K];
 #pragma unroll
-                for (int q = 0; q < K; q++) g += (q < pos && nd[q] > d) ? 1 : 0;
-                const int fin = pos - g;
+                for (int q = 0; q < K; q++) g[q] = nd[q] > d;
 #pragma unroll
-                for (int q = K - 1; q >= 1; q--)
-                    if (q > fin && q <= pos) { nd[q] = nd[q - 1]; nb[q] = nb[q - 1]; }
-#pragma unroll
-                for (int q = 0; q < K; q++)
-                    if (q == fin) { nd[q] = d; nb[q] = j; }
-                if (len < K) len++;
+                for (int q = K - 1; q >= 1; q--) {
+                    nd[q] = __builtin_amdgcn_fmed3f(nd[q - 1], nd[q], d);
+                    nb[q] = g[q - 1] ? nb[q - 1] : (g[q] ? j : nb[q]);
+                }
+                nd[0] = fminf(nd[0], d);
+                nb[0] = g[0] ? j : nb[0];
+                len = len < K ? len + 1 : K;
             }
         }
     }
